@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""bench.py -- SRTP protect+unprotect throughput on MI355X (BASELINE.json).
+
+A "step" = one srtp_encrypt_batch + one srtp_decrypt_batch over the whole
+device-resident packet arena (config 2 by default: 1M x 1200-B RTP packets,
+AES_CM_128_HMAC_SHA1_80, one session).  Every step uses a fresh tx/rx
+session pair (a receiver must not see the same indices twice: replay
+protection, src/srtp/replay.c:32-62), created outside the timed region.
+
+value = RTP bytes per step over all ranks / step time, in GiB/s
+        (N*L / (t_protect + t_unprotect)).
+roofline: the dominant kernel's algorithmic bytes per launch (packets x
+        (2L + T): read L, write L + T, or read L + T, write L) over its
+        average launch time, timed with HIP events on the launch stream.
+
+Multi-GPU (config 5): one process per GPU, rank r protects/unprotects its
+contiguous 1M-packet shard of one 8M-packet stream, continuing the
+stream state exactly where rank r-1's shard ends (srtp_stream_import).
+Packets are independent once their index is known, so there is no data
+collective; RCCL all-reduces the per-rank counters and the max time.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+METRIC = ("GiB/s + Mpkt/s SRTP protect+unprotect, 1200B RTP pkts, "
+          "device-resident")
+
+CONFIGS = {
+    2: dict(suite=1, n=1 << 20, length=1200, nsess=1,
+            name="AES_CM_128_HMAC_SHA1_80 1Mx1200B 1 session"),
+    3: dict(suite=5, n=1 << 20, length=1200, nsess=1,
+            name="AEAD_AES_256_GCM 1Mx1200B 1 session"),
+    4: dict(suite=1, n=1 << 20, length=None, nsess=1 << 16,
+            name="AES_CM_128_HMAC_SHA1_80 64K sessions mixed 200/1400B"),
+    5: dict(suite=1, n=1 << 20, length=1200, nsess=1,
+            name="AES_CM_128_HMAC_SHA1_80 8Mx1200B sharded (1M/GPU)"),
+}
+
+
+def shard_state(rank, per_rank, s0, ssrc, receiver):
+    """Stream state after a sequential sender/receiver processed packets
+    0 .. rank*per_rank-1 with seq = (s0+i) mod 2^16 (srtp.c:203-213,
+    279-280; replay.c:32-62)."""
+    import re_amd.srtp as P
+    st = P.StreamState()
+    last = s0 + rank * per_rank - 1
+    st.ssrc = ssrc
+    st.roc = last >> 16
+    st.s_l = last & 0xffff
+    st.s_l_set = 1
+    if receiver:
+        st.replay_rtp_lix = last
+        st.replay_rtp_bitmap = (1 << 64) - 1 if rank * per_rank >= 64 else \
+            (1 << (rank * per_rank)) - 1
+    return st
+
+
+def cpu_baseline(cfg):
+    """Reference src/srtp (oracle/_ref, OpenSSL) on the host cores, bounded
+    sample; falls back to the portable restatement (kind "port")."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    threads = max(1, min(16, os.cpu_count() or 1))
+    length = cfg["length"] or 0          # 0 = mixed 200/1400 in ref_bench
+    if os.path.exists(ref):
+        per = 60000 if cfg["suite"] < 4 else 150000
+        nsess = min(cfg["nsess"], 4096)
+        try:
+            out = subprocess.run(
+                [ref, str(cfg["suite"]), str(length), str(per), str(threads),
+                 str(nsess)], capture_output=True, text=True, timeout=300,
+                check=True).stdout
+            r = json.loads(out.strip().splitlines()[-1])
+            return {"value": round(r["gib_s"], 4), "unit": "GiB/s",
+                    "mpkt_s": round(r["mpairs_s"], 4), "cores": threads,
+                    "kind": "reference",
+                    "sample": "%d protect+unprotect pairs (%s B) on %d "
+                              "threads, one struct srtp pair per thread, "
+                              "reference src/srtp + OpenSSL %s" % (
+                                  r["pairs"], length or "200/1400",
+                                  threads, "libcrypto"),
+                    "seconds": round(r["seconds"], 3)}
+        except Exception as e:  # pragma: no cover
+            print("cpu_baseline: reference run failed: %s" % e,
+                  file=sys.stderr)
+    from tests import oracle_lib as O
+    n = 3000
+    t0 = time.perf_counter()
+    ok = O.lib().oracle_bench_pairs(cfg["suite"], cfg["length"] or 800, n)
+    dt = time.perf_counter() - t0
+    L = cfg["length"] or 800
+    return {"value": round(ok * L / dt / 2**30, 5), "unit": "GiB/s",
+            "mpkt_s": round(ok / dt / 1e6, 5), "cores": 1, "kind": "port",
+            "sample": "%d pairs through the portable C restatement" % n}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=None,
+                    help="BASELINE.json config (2,3,4,5); default 2, or 5 "
+                         "when --gpus > 1")
+    ap.add_argument("--packets", type=int, default=None,
+                    help="override packets per GPU (testing only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary to attach (profiles/*.json)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import re_amd.srtp as P
+    from re_amd import workload as W
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg_id = args.config or (5 if args.gpus > 1 else 2)
+    cfg = dict(CONFIGS[cfg_id])
+    if args.packets:
+        cfg["n"] = args.packets
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    P.load()
+
+    n, suite, nsess = cfg["n"], cfg["suite"], cfg["nsess"]
+    s0 = 65000
+    if cfg_id == 5:
+        s0 = (65000 + rank * n)           # global index of this shard
+    lengths = cfg["length"] if cfg["length"] else W.mixed_lengths(n)
+    sess = W.random_sessions(n, nsess) if nsess > 1 else None
+    arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
+                                          sess=sess)
+    arena = torch.from_numpy(arena_h).to(dev)
+    plain = arena.clone() if not args.no_verify else None
+    klen = P.key_len(suite) + P.salt_len(suite)
+    keys = W.make_keys(nsess, klen)
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes_stream(stream)
+    L = cfg["length"] or 800
+    tag = P.tag_len(suite)
+    rtp_bytes = int(np.asarray(end - pos, dtype=np.int64).sum())
+
+    def make_sessions():
+        e1, tx = P.alloc_many(nsess, suite, keys.tobytes())
+        e2, rx = P.alloc_many(nsess, suite, keys.tobytes())
+        assert not e1 and not e2, (e1, e2, P.lib().srtp_gpu_error())
+        if cfg_id == 5 and rank > 0:
+            assert tx[0].import_(shard_state(rank, n, 65000,
+                                             W.SSRC_BASE, False)) == 0
+            assert rx[0].import_(shard_state(rank, n, 65000,
+                                             W.SSRC_BASE, True)) == 0
+        return tx, rx
+
+    def step(tx, rx):
+        p, e = pos.copy(), end.copy()
+        rc, err = P.device_batch("srtp_encrypt", tx, arena.data_ptr(),
+                                 arena.numel(), p, e, cap, sess, sptr)
+        assert rc == 0, (rc, P.lib().srtp_gpu_error())
+        bad = int((err != 0).sum())
+        rc, err = P.device_batch("srtp_decrypt", rx, arena.data_ptr(),
+                                 arena.numel(), p, e, cap, sess, sptr)
+        assert rc == 0, (rc, P.lib().srtp_gpu_error())
+        bad += int((err != 0).sum())
+        return bad
+
+    # ---- warmup (untimed) ----
+    for _ in range(args.warmup):
+        tx, rx = make_sessions()
+        step(tx, rx)
+        for s in tx + rx:
+            s.close()
+    torch.cuda.synchronize()
+    sess_sets = [make_sessions() for _ in range(args.steps)]
+    P.prof_enable(True)
+    P.prof_read()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    errors = 0
+    for k in range(args.steps):
+        errors += step(*sess_sets[k])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    prof = P.prof_read()
+    P.prof_enable(False)
+    elapsed = t1 - t0
+    counters = torch.tensor([n * args.steps, rtp_bytes * args.steps, errors],
+                            dtype=torch.float64, device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tot_pkts, tot_bytes, tot_err = [float(x) for x in counters.tolist()]
+    T = float(tmax.item())
+    verified = None
+    if plain is not None:
+        verified = bool(torch.equal(arena, plain)) and tot_err == 0
+
+    for ss in sess_sets:
+        for s in ss[0] + ss[1]:
+            s.close()
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel ----
+    kern = []
+    for slot, (ms, launches, jobs) in prof.items():
+        prot = slot >= 16
+        pkt = jobs / launches
+        nbytes = pkt * (2 * L + tag)
+        avg_ms = ms / launches
+        kern.append({"slot": slot, "dir": "protect" if prot else "unprotect",
+                     "avg_ms": avg_ms, "launches": launches,
+                     "pkts_per_launch": pkt, "bytes_per_launch": nbytes,
+                     "gbs": nbytes / (avg_ms * 1e-3) / 1e9})
+    kern.sort(key=lambda d: -d["avg_ms"] * d["launches"])
+    dom = kern[0] if kern else None
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get("bytes_per_launch")
+    roof = None
+    if dom:
+        roof = {"bound": "hbm", "achieved": round(dom["gbs"], 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "k_ctr_hmac" if (dom["slot"] & 8) == 0 else "k_gcm",
+                "dir": dom["dir"],
+                "avg_launch_ms": round(dom["avg_ms"], 4),
+                "pkts_per_launch": dom["pkts_per_launch"],
+                "bytes_per_launch": dom["bytes_per_launch"],
+                "kernels": [{k: (round(v, 4) if isinstance(v, float) else v)
+                             for k, v in d.items()} for d in kern]}
+    gib = tot_bytes / T / 2**30
+    line = {
+        "metric": METRIC,
+        "value": round(gib, 4),
+        "unit": "GiB/s",
+        "mpkt_s": round(tot_pkts / T / 1e6, 4),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(T / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": "config%d: %s" % (cfg_id, cfg["name"]),
+                   "packets_per_gpu": n, "pkt_len": cfg["length"] or
+                   "200/1400", "suite": P.suite_name(suite),
+                   "sessions": nsess, "parallelism": "shard%d" % world},
+        "hbm_frac_e2e": round(tot_pkts / world * (4 * L + 2 * tag) /
+                              (T / 1) / 1e9 / HBM_PEAK_GBS, 4),
+        "errors": int(tot_err),
+        "verified_roundtrip": verified,
+        "roofline": roof,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg)
+    print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def ctypes_stream(stream):
+    """raw hipStream_t of a torch stream (None for the null stream)"""
+    h = stream.cuda_stream
+    return h if h else None
+
+
+if __name__ == "__main__":
+    main()

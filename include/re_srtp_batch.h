@@ -1,0 +1,108 @@
+/**
+ * @file re_srtp_batch.h  Batched SRTP/SRTCP -- extension (no reference
+ * counterpart; the reference API is one mbuf per call).
+ *
+ * Semantics: a batch of n packets gives exactly the results of n sequential
+ * re_srtp.h calls in array order -- per-packet errno, the mbuf pos/end the
+ * call would leave, the same bytes, and the same evolution of the ROC,
+ * s_l, replay windows and SRTCP index (src/srtp/srtp.h:23-38).
+ *
+ * Two entry families:
+ *   srtp_*_mbufs   host-resident packets (mbuf array), staged through
+ *                  pinned memory; the end-to-end path (socket -> GPU ->
+ *                  socket).  srtp_encrypt() etc. are this with n = 1.
+ *   srtp_*_batch   device-resident arena: packet bytes already in HBM,
+ *                  per-packet (pos, end, cap) windows, results in place.
+ */
+#ifndef RE_SRTP_BATCH_H
+#define RE_SRTP_BATCH_H
+
+#include "re_srtp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int srtp_encrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
+		       size_t n);
+int srtp_decrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
+		       size_t n);
+int srtcp_encrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
+			size_t n);
+int srtcp_decrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
+			size_t n);
+
+/**
+ * Device-resident batch.  arena is a device pointer (hipMalloc'ed); packet
+ * i occupies arena[pos[i], end[i]) and may grow up to cap[i] (the mbuf
+ * `size` analog: protect appends the tag there).  pos[i] must be a multiple
+ * of 4.  pos/end/cap/err/sess are host arrays; pos/end are updated like
+ * mbuf->pos/end.  sessv[sess[i]] is packet i's session (sess == NULL: all
+ * packets use sessv[0]).  stream: hipStream_t or NULL (default stream).
+ * Returns 0 if the batch ran (per-packet results in err[]), else an errno
+ * (EINVAL for bad arguments, EIO for a HIP failure).
+ */
+struct srtp_batch {
+	uint8_t *arena;
+	size_t arena_size;
+	uint32_t *pos;
+	uint32_t *end;
+	const uint32_t *cap;
+	int32_t *err;
+	const uint32_t *sess;
+	size_t n;
+	void *stream;
+};
+
+int srtp_encrypt_batch(struct srtp **sessv, size_t nsess,
+		       struct srtp_batch *b);
+int srtp_decrypt_batch(struct srtp **sessv, size_t nsess,
+		       struct srtp_batch *b);
+int srtcp_encrypt_batch(struct srtp **sessv, size_t nsess,
+			struct srtp_batch *b);
+int srtcp_decrypt_batch(struct srtp **sessv, size_t nsess,
+			struct srtp_batch *b);
+
+/**
+ * Stream state export/import (checkpoint/resume and multi-GPU hand-off:
+ * lets a second context continue an SSRC exactly where another left it).
+ * Layout follows struct srtp_stream (src/srtp/srtp.h:29-38).
+ */
+struct srtp_stream_state {
+	uint64_t replay_rtp_bitmap, replay_rtp_lix;
+	uint64_t replay_rtcp_bitmap, replay_rtcp_lix;
+	uint32_t ssrc;
+	uint32_t roc;
+	uint16_t s_l;
+	uint8_t s_l_set;
+	uint8_t pad;
+	uint32_t rtcp_index;
+};
+
+int srtp_stream_export(const struct srtp *srtp, uint32_t ssrc,
+		       struct srtp_stream_state *st);
+int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st);
+
+/** Batched session setup: n contexts in one GPU launch (key agility). */
+int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
+		    const uint8_t *keys, size_t key_bytes, int flags);
+
+/** last HIP-level error text (diagnostics) */
+const char *srtp_gpu_error(void);
+
+/**
+ * Kernel timing (diagnostics, used by bench.py): when enabled, every
+ * crypto kernel launch is bracketed by HIP events on its own stream.
+ * srtp_gpu_prof_read() returns and resets, per kernel class
+ * slot = protect*16 + gcm*8 + aes256*4 + shift, the summed device
+ * milliseconds, launch count and packet count.
+ */
+void srtp_gpu_prof(int enable);
+void srtp_gpu_prof_read(double ms[32], uint64_t launches[32],
+			uint64_t jobs[32]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,185 @@
+/*
+ * dev_common.h -- CDNA4 device primitives for the SRTP kernels.
+ *
+ * AES (FIPS-197) as a one-T-table cipher whose table lives in LDS:
+ *   - T0[x] = (2s, s, s, 3s) and T1 = rotl8(T0), s = S[x], as LE words.
+ *   - LDS image: 256 entries x 256 B.  Entry e holds 32 replicas of T0[e]
+ *     at bytes [0,128) and 32 replicas of T1[e] at [128,256).  Lane l reads
+ *     replica (l & 31): a ds_read_b32 wave-instruction is serviced as two
+ *     32-lane groups over 32 banks, so every lane of a group hits its own
+ *     bank whatever the table index -> conflict-free random lookups.
+ *   - Address generation is one v_perm_b32: ((byte k of x) << 8) | lane*4.
+ *   - A middle round column is T0[a]^T1[b]^rotl16(T0[c]^T1[d]^rotl16(rk)),
+ *     so round keys for rounds 1..nr-1 are stored pre-rotated (rk16).
+ * SHA-1 (FIPS 180-4) with a rolling 16-word schedule, one packet per lane.
+ * GHASH (SP 800-38D) with OpenSSL's 4-bit Shoup table (gcm_gmult_4bit
+ * layout: i*H table + rem_4bit reduction), table in LDS.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TT_BYTES 65536u
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n)
+{
+	return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
+
+__device__ __forceinline__ uint32_t rot16(uint32_t x)
+{
+	return __builtin_amdgcn_alignbit(x, x, 16);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+	return __builtin_amdgcn_perm(x, x, 0x00010203u);
+}
+
+/* LDS T-table address of byte k of x for this lane (laneoff = (lane&31)*4) */
+#define TT_ADDR(x, k, laneoff) \
+	__builtin_amdgcn_perm((x), (laneoff), 0x0C0C0000u | ((4u + (k)) << 8))
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *smem, uint32_t a)
+{
+	return *(const uint32_t *)(smem + a);
+}
+
+/* Fill the replicated T0/T1 image (all threads of the block) */
+__device__ __forceinline__ void tt_fill(uint8_t *smem, const uint32_t *T0g)
+{
+	uint32_t *s = (uint32_t *)smem;
+	for (uint32_t i = threadIdx.x; i < TT_BYTES / 4; i += blockDim.x) {
+		uint32_t e = i >> 6, r = i & 63;
+		uint32_t t = T0g[e];
+		s[i] = r < 32 ? t : rotl32(t, 8);
+	}
+}
+
+/*
+ * One AES block encryption.  rk: 4*(NR+1) words; words 4..4*NR-1 (rounds
+ * 1..NR-1) are rot16'd, round 0 and NR are plain.
+ */
+template <int NR>
+__device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
+					  const uint32_t *rk, uint32_t &s0,
+					  uint32_t &s1, uint32_t &s2,
+					  uint32_t &s3)
+{
+	s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+#pragma unroll
+	for (int r = 1; r < NR; r++) {
+		const uint32_t *k = rk + 4 * r;
+		uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
+		uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo) + 128);
+		uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
+		uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
+		uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
+		uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo) + 128);
+		uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
+		uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
+		uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
+		uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo) + 128);
+		uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
+		uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
+		uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
+		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo) + 128);
+		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
+		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
+		s0 = a0 ^ b1 ^ rot16(c2 ^ d3 ^ k[0]);
+		s1 = a1 ^ b2 ^ rot16(c3 ^ d0 ^ k[1]);
+		s2 = a2 ^ b3 ^ rot16(c0 ^ d1 ^ k[2]);
+		s3 = a3 ^ b0 ^ rot16(c1 ^ d2 ^ k[3]);
+	}
+	{
+		const uint32_t *k = rk + 4 * NR;
+		/* S[x] = byte1 of T0[x] = byte2 of T0[x] = byte3 of T1[x] */
+		uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
+		uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo));
+		uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
+		uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
+		uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
+		uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo));
+		uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
+		uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
+		uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
+		uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo));
+		uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
+		uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
+		uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
+		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo));
+		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
+		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
+		s0 = __builtin_amdgcn_perm(a0, b1, 0x0C0C0105u) ^
+		     __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu) ^ k[0];
+		s1 = __builtin_amdgcn_perm(a1, b2, 0x0C0C0105u) ^
+		     __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu) ^ k[1];
+		s2 = __builtin_amdgcn_perm(a2, b3, 0x0C0C0105u) ^
+		     __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu) ^ k[2];
+		s3 = __builtin_amdgcn_perm(a3, b0, 0x0C0C0105u) ^
+		     __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu) ^ k[3];
+	}
+}
+
+/* ---- SHA-1 compression, W[] holds the 16 big-endian message words ---- */
+__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16])
+{
+	uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#define SHA_ROUND(i, f, K)                                                   \
+	do {                                                                 \
+		uint32_t wi;                                                 \
+		if ((i) < 16) {                                              \
+			wi = w[(i) & 15];                                    \
+		} else {                                                     \
+			wi = rotl32(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ \
+				    w[((i) + 2) & 15] ^ w[(i) & 15], 1);     \
+			w[(i) & 15] = wi;                                    \
+		}                                                            \
+		uint32_t t = rotl32(a, 5) + (f) + e + (K) + wi;              \
+		e = d; d = c; c = rotl32(b, 30); b = a; a = t;               \
+	} while (0)
+#pragma unroll
+	for (int i = 0; i < 20; i++)
+		SHA_ROUND(i, (d ^ (b & (c ^ d))), 0x5a827999u);
+#pragma unroll
+	for (int i = 20; i < 40; i++)
+		SHA_ROUND(i, (b ^ c ^ d), 0x6ed9eba1u);
+#pragma unroll
+	for (int i = 40; i < 60; i++)
+		SHA_ROUND(i, ((b & c) | (d & (b | c))), 0x8f1bbcdcu);
+#pragma unroll
+	for (int i = 60; i < 80; i++)
+		SHA_ROUND(i, (b ^ c ^ d), 0xca62c1d6u);
+#undef SHA_ROUND
+	h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+/* ---- GHASH: Z = (X) * H with the 4-bit table at tab (LDS or global) ---- */
+/* X given as 4 big-endian words x0..x3 (x0 = bytes 0..3).  rem4 in LDS. */
+__device__ __forceinline__ void ghash_mul(uint32_t &x0, uint32_t &x1,
+					  uint32_t &x2, uint32_t &x3,
+					  const uint8_t *tab,
+					  const uint32_t *rem4)
+{
+	uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+	uint32_t xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+	for (int wi = 3; wi >= 0; wi--) {
+		uint32_t xw = xs[wi];
+#pragma unroll
+		for (int nb = 0; nb < 8; nb++) {
+			/* byte order: word bytes 3..0 are X[4wi+3..4wi] (BE),
+			 * low nibble of each byte first */
+			uint32_t sh = (uint32_t)((nb >> 1) * 8 + ((nb & 1) ? 4 : 0));
+			uint32_t nib = (xw >> sh) & 0xfu;
+			uint32_t rem = z3 & 0xfu;
+			z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+			z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+			z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+			z0 = (z0 >> 4) ^ rem4[rem];
+			const uint4 t = *(const uint4 *)(tab + nib * 16u);
+			z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+		}
+	}
+	x0 = z0; x1 = z1; x2 = z2; x3 = z3;
+}

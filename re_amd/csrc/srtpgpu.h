@@ -1,0 +1,157 @@
+/*
+ * srtpgpu.h -- the thin C-ABI shim between the C host library and the HIP
+ * kernels (re_amd/csrc/hip/srtp_kernels.hip).  Plain C types only.
+ *
+ * The host C code (re_amd/csrc/host/srtp.c) keeps every piece of SRTP
+ * *state* (ROC, s_l, replay windows, SRTCP index, stream table -- exactly
+ * the reference's struct srtp_stream, src/srtp/srtp.h:29-38) and turns each
+ * packet into one `struct sgpu_job`.  The GPU does all *cipher and MAC*
+ * arithmetic: AES-CTR keystream (src/aes/openssl/aes.c:136-171), AES-GCM
+ * (aes.c:183-249), HMAC-SHA1 (src/hmac/openssl/hmac.c:78-95) and the session
+ * key derivation (src/srtp/misc.c:44-73, srtp.c:33-72).
+ */
+#ifndef SRTPGPU_H
+#define SRTPGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-direction device crypto context (one per struct comp) -------- */
+/* Built on the GPU by sgpu_setup_sessions(); never touched by the host.  */
+enum {
+	SGPU_MODE_CTR = 0,
+	SGPU_MODE_GCM = 1,
+};
+
+struct sgpu_comp {              /* 640 bytes, 16-B aligned */
+	uint32_t rk[60];        /* AES round keys, LE words of the byte
+				   schedule; rounds 1..nr-1 stored rot16 */
+	uint32_t nr;            /* 10 or 14 */
+	uint32_t mode;          /* SGPU_MODE_* */
+	uint32_t tag_len;       /* HMAC truncation (0 for GCM) */
+	uint32_t flags;         /* bit0 has_aes, bit1 has_hmac */
+	uint32_t k_s[4];        /* session salt k_s (14 B used), LE words */
+	uint32_t ipad[5];       /* HMAC-SHA1 inner midstate */
+	uint32_t opad[5];       /* HMAC-SHA1 outer midstate */
+	uint32_t pad0[2];
+	uint32_t htab[16][4];   /* GHASH 4-bit Shoup table (i * H) */
+};
+
+struct sgpu_session {           /* rtp = comp[0], rtcp = comp[1] */
+	struct sgpu_comp comp[2];
+};
+
+/* input to the setup kernel (one per session) */
+struct sgpu_keyreq {
+	uint8_t master[48];     /* master key ‖ master salt */
+	uint32_t cipher_bytes;  /* 16 or 32 */
+	uint32_t salt_bytes;    /* 14 or 12 */
+	uint32_t tag_len;       /* 4, 10 or 0 */
+	uint32_t mode;          /* SGPU_MODE_* */
+	uint32_t hash;          /* 1: HMAC-SHA1 suites */
+	uint32_t rtcp_encrypted;/* !(flags & SRTP_UNENCRYPTED_SRTCP) */
+	uint32_t pad[2];
+};
+
+/* ---- per-packet job (host -> device), 48 bytes ------------------------- */
+enum {
+	SJ_PROTECT      = 1u << 0,  /* 0 = unprotect */
+	SJ_CIPHER       = 1u << 1,  /* apply keystream over [c_off,c_off+c_len) */
+	SJ_HMAC         = 1u << 2,  /* HMAC-SHA1 over [0,a_len) ‖ trailer? */
+	SJ_GCM          = 1u << 3,  /* AES-GCM (AAD [0,a_len) ‖ trailer?) */
+	SJ_TRAILER      = 1u << 4,  /* append BE32(trailer) to the MAC/AAD input */
+	SJ_STORE_TRAIL  = 1u << 5,  /* protect: store BE32(trailer) at t_off */
+	SJ_CIPHER_IF_OK = 1u << 6,  /* unprotect HMAC: decrypt only if tag ok */
+	SJ_ROC_AT_TAG   = 1u << 7,  /* unprotect HMAC: if tag ok write BE32(trailer)
+				       at tag_off (srtp.c:342-344) */
+	SJ_GCM_IV       = 1u << 8,  /* IV per srtp_iv_calc_gcm (misc.c:93-105) */
+	SJ_UNDO         = 1u << 9,  /* re-apply keystream only (CTR involution) */
+	SJ_SKIP         = 1u << 15, /* no GPU work (host-decided error) */
+};
+
+struct sgpu_job {
+	uint32_t off;       /* packet start (mbuf start position) in arena */
+	uint32_t comp;      /* index of sgpu_comp in the device table */
+	uint32_t a_len;     /* HMAC message prefix / GCM AAD prefix, bytes */
+	uint32_t c_off;     /* cipher region start, bytes from off (4-aligned) */
+	uint32_t c_len;     /* cipher region length, bytes */
+	uint32_t tag_off;   /* where the tag is written / read, from off */
+	uint32_t t_off;     /* where SJ_STORE_TRAIL stores the trailer */
+	uint32_t trailer;   /* ROC or E‖SRTCP-index (host order) */
+	uint32_t ssrc;      /* for the IV */
+	uint32_t ixhi;      /* (uint32_t)(ix >> 16) */
+	uint32_t ixlo;      /* (uint16_t)ix */
+	uint32_t flags;     /* SJ_* */
+};
+
+/* verdict bits returned per job (unprotect) */
+enum {
+	SV_TAG_OK   = 1u << 0,
+	SV_CIPHERED = 1u << 1,
+};
+
+/* ---- shim entry points (implemented in srtp_kernels.hip) --------------- */
+int   sgpu_init(void);                  /* 0, or ENODEV / ENOSYS */
+const char *sgpu_last_error(void);
+
+/* device session-context table: slots are allocated by the host */
+int   sgpu_table_reserve(uint32_t nsessions);      /* grow capacity */
+int   sgpu_setup_sessions(const struct sgpu_keyreq *req, const uint32_t *slot,
+			  uint32_t n);               /* KDF + key schedule */
+uint64_t sgpu_table_device_ptr(void);
+
+/* run one kernel class over jobs[0..njobs) of a device arena.  Every job
+ * of a launch shares (mode, nr, shift = (c_off/4)&3, direction); verdict is
+ * a device array (or NULL).  `stream` is a hipStream_t or NULL. */
+int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
+		     const struct sgpu_job *jobs, uint32_t njobs,
+		     uint8_t *verdict, uint32_t *save, int mode, int nr,
+		     int shift, int prot, void *stream);
+
+/* store 4 raw bytes (LE word vals[i]) at arena + offs[i], any alignment
+ * (restores tag bytes before a re-run) -- device arrays */
+int   sgpu_store_words(uint8_t *arena, const uint32_t *offs,
+		       const uint32_t *vals, uint32_t n, void *stream);
+
+/* device-resident header parse: for each packet i, reads the RTP (or RTCP)
+ * header at arena[pos[i]] bounded by end[i] and writes sgpu_hdr[i]. */
+struct sgpu_hdr {
+	uint32_t ssrc;
+	uint16_t seq;
+	uint16_t err_pos;   /* bytes consumed before an EBADMSG (0 if ok) */
+	uint32_t hdr_len;   /* full RTP header length (0xffffffff on EBADMSG) */
+};
+/* eix (RTCP, optional): 3 words per packet, the BE word at end-4-tl for
+ * tl = 0, 4, 10 (the E-bit/SRTCP-index word for each tag length). */
+int   sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,
+			 const uint32_t *end, struct sgpu_hdr *out,
+			 uint32_t *eix, uint32_t n, int rtcp, void *stream);
+
+/* kernel timing (HIP events recorded on the launch stream) */
+void  sgpu_prof_enable(int on);
+void  sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs);
+
+/* memory helpers (device / pinned host) */
+void *sgpu_malloc(size_t n);
+void  sgpu_free(void *p);
+void *sgpu_host_alloc(size_t n);
+void  sgpu_host_free(void *p);
+int   sgpu_memcpy_h2d(void *dst, const void *src, size_t n, void *stream);
+int   sgpu_memcpy_d2h(void *dst, const void *src, size_t n, void *stream);
+int   sgpu_memset(void *dst, int v, size_t n, void *stream);
+int   sgpu_stream_sync(void *stream);
+int   sgpu_device_sync(void);
+void *sgpu_stream_create(void);
+void  sgpu_stream_destroy(void *s);
+int   sgpu_set_device(int dev);
+int   sgpu_get_device(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,277 @@
+"""ctypes mirror of include/re_srtp.h + include/re_srtp_batch.h.
+
+Names, argument meaning and errno results follow the reference interface
+(/root/reference/include/re_srtp.h:8-30).  Errors from the C library are
+returned as errno integers exactly as the C functions return them.
+"""
+import ctypes
+import errno
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libre_srtp_amd.so")
+
+SRTP_AES_CM_128_HMAC_SHA1_32 = 0
+SRTP_AES_CM_128_HMAC_SHA1_80 = 1
+SRTP_AES_256_CM_HMAC_SHA1_32 = 2
+SRTP_AES_256_CM_HMAC_SHA1_80 = 3
+SRTP_AES_128_GCM = 4
+SRTP_AES_256_GCM = 5
+SUITES = range(6)
+SRTP_UNENCRYPTED_SRTCP = 1 << 1
+EAUTH = 217
+
+_KEY = {0: 16, 1: 16, 2: 32, 3: 32, 4: 16, 5: 32}
+_SALT = {0: 14, 1: 14, 2: 14, 3: 14, 4: 12, 5: 12}
+_TAG = {0: 4, 1: 10, 2: 4, 3: 10, 4: 16, 5: 16}
+
+
+def key_len(s):
+    return _KEY[s]
+
+
+def salt_len(s):
+    return _SALT[s]
+
+
+def tag_len(s):
+    return _TAG[s]
+
+
+class Mbuf(ctypes.Structure):
+    """struct mbuf (include/re_mbuf.h:43-48)"""
+    _fields_ = [("buf", ctypes.POINTER(ctypes.c_uint8)),
+                ("size", ctypes.c_size_t),
+                ("pos", ctypes.c_size_t),
+                ("end", ctypes.c_size_t)]
+
+
+class SrtpBatch(ctypes.Structure):
+    """struct srtp_batch (include/re_srtp_batch.h)"""
+    _fields_ = [("arena", ctypes.c_void_p),
+                ("arena_size", ctypes.c_size_t),
+                ("pos", ctypes.POINTER(ctypes.c_uint32)),
+                ("end", ctypes.POINTER(ctypes.c_uint32)),
+                ("cap", ctypes.POINTER(ctypes.c_uint32)),
+                ("err", ctypes.POINTER(ctypes.c_int32)),
+                ("sess", ctypes.POINTER(ctypes.c_uint32)),
+                ("n", ctypes.c_size_t),
+                ("stream", ctypes.c_void_p)]
+
+
+class StreamState(ctypes.Structure):
+    _fields_ = [("replay_rtp_bitmap", ctypes.c_uint64),
+                ("replay_rtp_lix", ctypes.c_uint64),
+                ("replay_rtcp_bitmap", ctypes.c_uint64),
+                ("replay_rtcp_lix", ctypes.c_uint64),
+                ("ssrc", ctypes.c_uint32),
+                ("roc", ctypes.c_uint32),
+                ("s_l", ctypes.c_uint16),
+                ("s_l_set", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8),
+                ("rtcp_index", ctypes.c_uint32)]
+
+
+EXPORTS = (
+    "srtp_alloc", "srtp_encrypt", "srtp_decrypt", "srtcp_encrypt",
+    "srtcp_decrypt", "srtp_suite_name",
+    "srtp_encrypt_mbufs", "srtp_decrypt_mbufs", "srtcp_encrypt_mbufs",
+    "srtcp_decrypt_mbufs", "srtp_encrypt_batch", "srtp_decrypt_batch",
+    "srtcp_encrypt_batch", "srtcp_decrypt_batch", "srtp_stream_export",
+    "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
+    "srtp_gpu_prof", "srtp_gpu_prof_read",
+    "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
+)
+
+_lib = None
+
+
+def load():
+    """Load the C-ABI library; raise (loudly) if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "re_amd: %s missing -- run `make -C re_amd` (or "
+            "__graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.srtp_alloc.argtypes = [ctypes.POINTER(vp), ctypes.c_int,
+                             ctypes.c_char_p, sz, ctypes.c_int]
+    for f in ("srtp_encrypt", "srtp_decrypt", "srtcp_encrypt",
+              "srtcp_decrypt"):
+        getattr(L, f).argtypes = [vp, ctypes.POINTER(Mbuf)]
+        getattr(L, f + "_mbufs").argtypes = [
+            vp, ctypes.POINTER(ctypes.POINTER(Mbuf)),
+            ctypes.POINTER(ctypes.c_int), sz]
+        getattr(L, f + "_batch").argtypes = [
+            ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatch)]
+    L.srtp_suite_name.restype = ctypes.c_char_p
+    L.srtp_suite_name.argtypes = [ctypes.c_int]
+    L.srtp_gpu_error.restype = ctypes.c_char_p
+    L.srtp_stream_export.argtypes = [vp, ctypes.c_uint32,
+                                     ctypes.POINTER(StreamState)]
+    L.srtp_stream_import.argtypes = [vp, ctypes.POINTER(StreamState)]
+    L.srtp_alloc_many.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_int,
+                                  ctypes.c_char_p, sz, ctypes.c_int]
+    L.srtp_gpu_prof.argtypes = [ctypes.c_int]
+    L.srtp_gpu_prof_read.argtypes = [ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    L.mbuf_alloc.restype = ctypes.POINTER(Mbuf)
+    L.mbuf_alloc.argtypes = [sz]
+    L.mbuf_resize.argtypes = [ctypes.POINTER(Mbuf), sz]
+    L.mbuf_write_mem.argtypes = [ctypes.POINTER(Mbuf), ctypes.c_char_p, sz]
+    L.mem_deref.restype = vp
+    L.mem_deref.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def lib():
+    return load()
+
+
+def suite_name(suite):
+    return lib().srtp_suite_name(suite).decode()
+
+
+class Srtp:
+    """Owning handle around `struct srtp *` (freed with mem_deref)."""
+
+    def __init__(self, suite, key, flags=0):
+        L = lib()
+        self.ptr = ctypes.c_void_p()
+        self.err = L.srtp_alloc(ctypes.byref(self.ptr), suite, key, len(key),
+                                flags)
+        self.suite = suite
+
+    @classmethod
+    def wrap(cls, ptr, suite):
+        o = cls.__new__(cls)
+        o.ptr = ctypes.c_void_p(ptr)
+        o.err = 0
+        o.suite = suite
+        return o
+
+    def close(self):
+        if self.ptr:
+            lib().mem_deref(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _op(self, name, mb):
+        return getattr(lib(), name)(self.ptr, mb)
+
+    def encrypt(self, mb):
+        return self._op("srtp_encrypt", mb)
+
+    def decrypt(self, mb):
+        return self._op("srtp_decrypt", mb)
+
+    def rtcp_encrypt(self, mb):
+        return self._op("srtcp_encrypt", mb)
+
+    def rtcp_decrypt(self, mb):
+        return self._op("srtcp_decrypt", mb)
+
+    def export(self, ssrc):
+        st = StreamState()
+        e = lib().srtp_stream_export(self.ptr, ssrc, ctypes.byref(st))
+        return e, st
+
+    def import_(self, st):
+        return lib().srtp_stream_import(self.ptr, ctypes.byref(st))
+
+
+def alloc_many(n, suite, keys, flags=0):
+    """srtp_alloc_many: n sessions in one GPU setup launch."""
+    arr = (ctypes.c_void_p * n)()
+    klen = key_len(suite) + salt_len(suite)
+    e = lib().srtp_alloc_many(arr, n, suite, keys, klen, flags)
+    if e:
+        return e, []
+    return 0, [Srtp.wrap(arr[i], suite) for i in range(n)]
+
+
+def new_mbuf(data, size, pos=0):
+    """mbuf with buf[0:len(data)] = data, bytes [len, size) zero."""
+    L = lib()
+    mb = L.mbuf_alloc(size)
+    ctypes.memset(mb.contents.buf, 0, mb.contents.size)
+    if data:
+        ctypes.memmove(mb.contents.buf, data, len(data))
+    mb.contents.pos = pos
+    mb.contents.end = len(data)
+    return mb
+
+
+def mbuf_bytes(mb, n=None):
+    m = mb.contents
+    return ctypes.string_at(m.buf, m.end if n is None else n)
+
+
+def free_mbuf(mb):
+    lib().mem_deref(ctypes.cast(mb, ctypes.c_void_p))
+
+
+_OPS = {"srtp_encrypt": "srtp_encrypt", "srtp_decrypt": "srtp_decrypt",
+        "srtcp_encrypt": "srtcp_encrypt", "srtcp_decrypt": "srtcp_decrypt"}
+
+
+def batch_run(ctx, opname, mbufs):
+    """srtp_*_mbufs over a list of mbuf pointers; returns (rc, errs)."""
+    n = len(mbufs)
+    arr = (ctypes.POINTER(Mbuf) * n)(*mbufs)
+    errs = (ctypes.c_int * n)()
+    rc = getattr(lib(), opname + "_mbufs")(ctx.ptr, arr, errs, n)
+    return rc, list(errs)
+
+
+def device_batch(opname, sessions, arena_ptr, arena_size, pos, end, cap,
+                 sess_idx=None, stream=None):
+    """srtp_*_batch on a device arena.  pos/end/cap: numpy uint32 arrays
+    (pos/end updated in place); returns (rc, err numpy int32)."""
+    import numpy as np
+    n = len(pos)
+    assert pos.dtype == np.uint32 and end.dtype == np.uint32
+    cap = np.ascontiguousarray(cap, dtype=np.uint32)
+    err = np.zeros(n, dtype=np.int32)
+    b = SrtpBatch()
+    b.arena = arena_ptr
+    b.arena_size = arena_size
+    b.pos = pos.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    b.end = end.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    b.cap = cap.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    b.err = err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    if sess_idx is not None:
+        sess_idx = np.ascontiguousarray(sess_idx, dtype=np.uint32)
+        b.sess = sess_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    b.n = n
+    b.stream = stream
+    sv = (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
+    rc = getattr(lib(), opname + "_batch")(sv, len(sessions), ctypes.byref(b))
+    return rc, err
+
+
+def prof_enable(on=True):
+    lib().srtp_gpu_prof(1 if on else 0)
+
+
+def prof_read():
+    """{slot: (ms, launches, jobs)} for kernel classes that ran.
+    slot = protect*16 + gcm*8 + aes256*4 + shift"""
+    ms = (ctypes.c_double * 32)()
+    la = (ctypes.c_uint64 * 32)()
+    jb = (ctypes.c_uint64 * 32)()
+    lib().srtp_gpu_prof_read(ms, la, jb)
+    return {k: (ms[k], la[k], jb[k]) for k in range(32) if la[k]}
+
+
+__all__ = ["errno"]

@@ -212,7 +212,15 @@ def main():
     T = float(tmax.item())
     verified = None
     if plain is not None:
-        verified = bool(torch.equal(arena, plain)) and tot_err == 0
+        # packet windows [pos, end) are restored by protect+unprotect; the
+        # bytes past end keep the tag (and the ROC written over it,
+        # srtp.c:342-344) exactly like the reference mbuf
+        slot = int(cap[0] - pos[0])
+        lens = torch.from_numpy((end - pos).astype(np.int64)).to(dev)
+        win = torch.arange(slot, device=dev)[None, :] < lens[:, None]
+        a2, p2 = arena.view(n, slot), plain.view(n, slot)
+        verified = bool(torch.equal(a2[win], p2[win])) and tot_err == 0
+        del win, a2, p2
 
     for ss in sess_sets:
         for s in ss[0] + ss[1]:

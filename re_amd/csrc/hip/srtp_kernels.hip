@@ -114,29 +114,134 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t gw, uint32_t data_be,
 	return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* kernel arguments and job sources                                    */
+
+struct KArgs {
+	uint8_t *arena;
+	uint64_t asz;
+	const struct sgpu_job *jobs;    /* general path */
+	uint32_t njobs;
+	const struct sgpu_comp *comps;
+	uint8_t *verdict;
+	uint32_t *save;
+	struct sgpu_compact c;          /* compact path */
+};
+
+/*
+ * Job of thread t.  General path: jobs[t], results at slot t.  Compact
+ * path: packet p = idx[base+t] (or base+t); the job is derived exactly as
+ * plan_rtp_enc / plan_rtp_dec (re_amd/csrc/host/srtp.c) build it, from the
+ * packet window, the parsed header and the 8-byte descriptor
+ * (srtp.c:215-277, 325-382, 383-424 of the reference).
+ */
+template <bool COMPACT, int MODE, bool PROT>
+__device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
+					struct sgpu_job &j, uint32_t &slot)
+{
+	if (!COMPACT) {
+		if (t >= a.njobs)
+			return false;
+		j = a.jobs[t];
+		slot = t;
+		return true;
+	}
+	const struct sgpu_compact &c = a.c;
+	if (t >= c.n)
+		return false;
+	const uint32_t p = c.idx ? c.idx[c.base + t] : c.base + t;
+	slot = p;
+	const uint64_t d = c.desc[p];
+	const uint32_t fl = (uint32_t)(d >> 48);
+	j.flags = SJ_SKIP;
+	j.comp = 0;
+	if (!(fl & SD_RUN))
+		return true;
+	uint8_t vd = 0;
+	if (c.undo) {
+		vd = a.verdict[p];
+		if (MODE == SGPU_MODE_GCM && !(vd & SV_CIPHERED))
+			return true;
+	}
+	const uint32_t comp = c.compmap[c.sess ? c.sess[p] : 0u];
+	const uint32_t off = c.pos[p];
+	const uint32_t L = c.end[p] - off;
+	const uint32_t *hw = (const uint32_t *)(c.hdr + p);
+	const uint32_t ssrc = hw[0], hl = hw[2];
+	const uint32_t ixhi = (uint32_t)(d >> 16);
+	j.off = off;
+	j.comp = comp;
+	j.ssrc = ssrc;
+	j.ixhi = ixhi;
+	j.ixlo = (uint32_t)(d & 0xffffu);
+	j.trailer = ixhi + ((fl & SD_ROC_P1) ? 1u : 0u) -
+		    ((fl & SD_ROC_M1) ? 1u : 0u);
+	j.t_off = 0;
+	j.c_off = hl;
+	if (MODE == SGPU_MODE_CTR) {
+		if (PROT) {
+			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_HMAC | SJ_TRAILER;
+			j.a_len = L;
+			j.c_len = L - hl;
+			j.tag_off = L;
+		}
+		else {
+			const uint32_t T = a.comps[comp].tag_len;
+			j.a_len = L - T;
+			j.tag_off = L - T;
+			j.c_len = L - T - hl;
+			if (c.undo)
+				j.flags = (vd & SV_CIPHERED) ? SJ_CIPHER : 0u;
+			else
+				j.flags = SJ_HMAC | SJ_TRAILER | SJ_ROC_AT_TAG |
+					  ((fl & SD_CIPHER) ?
+					   (SJ_CIPHER | SJ_CIPHER_IF_OK) : 0u);
+		}
+	}
+	else {
+		j.a_len = hl;
+		if (PROT) {
+			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_GCM;
+			j.c_len = L - hl;
+			j.tag_off = L;
+		}
+		else {
+			j.flags = c.undo ? (SJ_GCM | SJ_CIPHER | SJ_UNDO)
+					 : (SJ_GCM | SJ_CIPHER);
+			j.c_len = L - 16u - hl;
+			j.tag_off = L - 16u;
+		}
+	}
+	return true;
+}
+
 /*
  * Fused AES-CM + HMAC-SHA1, one packet per lane.
  *   SHIFT = (c_off / 4) & 3: the cipher region starts SHIFT words into a
  *   16-byte packet granule (3 for a 12-byte RTP header, 2 for SRTCP).
  */
-template <int NR, int SHIFT, bool PROT>
+template <int NR, int SHIFT, bool PROT, bool COMPACT>
 __global__ void __launch_bounds__(KBLOCK)
-k_ctr_hmac(uint8_t *__restrict__ arena, uint64_t asz,
-	   const struct sgpu_job *__restrict__ jobs, uint32_t njobs,
-	   const struct sgpu_comp *__restrict__ comps,
-	   uint8_t *__restrict__ verdict, uint32_t *__restrict__ save)
+k_ctr_hmac(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
 	tt_fill(smem, g_T0);
 	__syncthreads();
 
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= njobs)
+	uint8_t *const arena = a.arena;
+	const uint64_t asz = a.asz;
+	const struct sgpu_comp *__restrict__ comps = a.comps;
+	uint8_t *__restrict__ verdict = a.verdict;
+	uint32_t *__restrict__ save = a.save;
+	const bool undo = COMPACT && a.c.undo;
+	struct sgpu_job j;
+	uint32_t i;
+	if (!get_job<COMPACT, SGPU_MODE_CTR, PROT>(
+		    a, blockIdx.x * blockDim.x + threadIdx.x, j, i))
 		return;
 	const uint32_t lo = (threadIdx.x & 31u) * 4u;
-	const struct sgpu_job j = jobs[i];
 	if (j.flags & SJ_SKIP) {
-		if (verdict)
+		if (verdict && !undo)
 			verdict[i] = 0;
 		return;
 	}
@@ -373,6 +478,16 @@ k_ctr_hmac(uint8_t *__restrict__ arena, uint64_t asz,
 		}
 		vd &= (uint8_t)~SV_CIPHERED;
 	}
+	if (undo) {
+		/* compact undo: the word under the ROC back (srtp.c:342-344) */
+		uint8_t *tp = pkt + j.tag_off;
+		const uint32_t v = save[i];
+		tp[0] = (uint8_t)v; tp[1] = (uint8_t)(v >> 8);
+		tp[2] = (uint8_t)(v >> 16); tp[3] = (uint8_t)(v >> 24);
+		return;
+	}
+	if (COMPACT && !PROT && !(vd & SV_TAG_OK))
+		atomicAdd(a.c.nfail, 1u);
 	if (verdict)
 		verdict[i] = vd;
 }
@@ -396,13 +511,15 @@ __device__ __forceinline__ void aad_block(const uint8_t *pkt, uint64_t pasz,
 		w[q] = msg_word((p >> 2) + q, bswap32(d[q]), A, X);
 }
 
-template <int NR, bool PROT>
+template <int NR, bool PROT, bool COMPACT>
 __global__ void __launch_bounds__(KBLOCK)
-k_gcm(uint8_t *__restrict__ arena, uint64_t asz,
-      const struct sgpu_job *__restrict__ jobs, uint32_t njobs,
-      const struct sgpu_comp *__restrict__ comps,
-      uint8_t *__restrict__ verdict, uint32_t *__restrict__ save)
+k_gcm(const KArgs a)
 {
+	uint8_t *const arena = a.arena;
+	const uint64_t asz = a.asz;
+	const struct sgpu_comp *__restrict__ comps = a.comps;
+	uint8_t *__restrict__ verdict = a.verdict;
+	const bool undo = COMPACT && a.c.undo;
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES + 4096 + 64];
 	uint8_t *htab_lds = smem + TT_BYTES;                  /* 16 waves x 256 */
 	uint32_t *rem4 = (uint32_t *)(smem + TT_BYTES + 4096);
@@ -411,14 +528,13 @@ k_gcm(uint8_t *__restrict__ arena, uint64_t asz,
 		rem4[threadIdx.x] = c_rem4[threadIdx.x];
 	__syncthreads();
 
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 	const uint32_t lo = (threadIdx.x & 31u) * 4u;
-	const bool live = i < njobs;
 	struct sgpu_job j;
-	if (live)
-		j = jobs[i];
-	else
+	uint32_t i = 0;
+	const bool live = get_job<COMPACT, SGPU_MODE_GCM, PROT>(
+		a, blockIdx.x * blockDim.x + threadIdx.x, j, i);
+	if (!live)
 		j.flags = SJ_SKIP, j.comp = 0;
 	/* stage the GHASH table: per wave, in LDS if the wave's packets
 	 * share one context, else per-lane reads from global memory */
@@ -440,7 +556,7 @@ k_gcm(uint8_t *__restrict__ arena, uint64_t asz,
 	if (!live)
 		return;
 	if (j.flags & SJ_SKIP) {
-		if (verdict)
+		if (verdict && !undo)
 			verdict[i] = 0;
 		return;
 	}
@@ -497,7 +613,7 @@ k_gcm(uint8_t *__restrict__ arena, uint64_t asz,
 				}
 			}
 		}
-		if (verdict)
+		if (verdict && !undo)
 			verdict[i] = 0;
 		return;
 	}
@@ -583,6 +699,8 @@ k_gcm(uint8_t *__restrict__ arena, uint64_t asz,
 			diff |= tp[q] ^ (uint8_t)(t[q >> 2] >> (24 - 8 * (q & 3)));
 		if (diff == 0)
 			vd |= SV_TAG_OK;
+		if (COMPACT && !(vd & SV_TAG_OK))
+			atomicAdd(a.c.nfail, 1u);
 	}
 	if (verdict)
 		verdict[i] = vd;
@@ -1034,65 +1152,49 @@ extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs)
 	pthread_mutex_unlock(&g_prof_lock);
 }
 
-typedef void (*kfn_t)(uint8_t *, uint64_t, const struct sgpu_job *, uint32_t,
-		      const struct sgpu_comp *, uint8_t *, uint32_t *);
+typedef void (*kfn_t)(const KArgs);
 
+template <bool COMPACT>
 static kfn_t pick_ctr(int nr, int shift, int prot)
 {
 #define PICK(NR, S)                                                            \
 	if (nr == NR && shift == S)                                            \
-		return prot ? k_ctr_hmac<NR, S, true> : k_ctr_hmac<NR, S, false>;
+		return prot ? k_ctr_hmac<NR, S, true, COMPACT>                 \
+			    : k_ctr_hmac<NR, S, false, COMPACT>;
 	PICK(10, 0) PICK(10, 1) PICK(10, 2) PICK(10, 3)
 	PICK(14, 0) PICK(14, 1) PICK(14, 2) PICK(14, 3)
 #undef PICK
 	return NULL;
 }
 
+template <bool COMPACT>
 static kfn_t pick_gcm(int nr, int prot)
 {
 	if (nr == 10)
-		return prot ? k_gcm<10, true> : k_gcm<10, false>;
+		return prot ? k_gcm<10, true, COMPACT> : k_gcm<10, false, COMPACT>;
 	if (nr == 14)
-		return prot ? k_gcm<14, true> : k_gcm<14, false>;
+		return prot ? k_gcm<14, true, COMPACT> : k_gcm<14, false, COMPACT>;
 	return NULL;
 }
 
-/*
- * Launch one kernel over jobs[0..njobs).  The caller (host C) groups jobs
- * so that one launch shares (mode, key size, shift class, direction); the
- * class is passed in jobs via sgpu_run_class().
- */
-extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
-			      const struct sgpu_job *jobs, uint32_t njobs,
-			      uint8_t *verdict, uint32_t *save, int mode,
-			      int nr, int shift, int prot, void *stream)
+static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
+		  hipStream_t stream)
 {
-	if (!njobs)
-		return 0;
-	kfn_t f = mode == SGPU_MODE_GCM ? pick_gcm(nr, prot)
-					: pick_ctr(nr, shift, prot);
-	if (!f) {
-		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
-			 mode, nr);
-		return EINVAL;
-	}
 	struct prof_ev pe;
 	int prof = 0;
-	if (g_prof_on) {
+	if (g_prof_on && slot >= 0) {
 		prof = hipEventCreate(&pe.a) == hipSuccess &&
 		       hipEventCreate(&pe.b) == hipSuccess;
 		if (prof)
-			(void)hipEventRecord(pe.a, (hipStream_t)stream);
+			(void)hipEventRecord(pe.a, stream);
 	}
-	hipLaunchKernelGGL(f, dim3((njobs + KBLOCK - 1) / KBLOCK), dim3(KBLOCK),
-			   0, (hipStream_t)stream, arena, arena_size, jobs, njobs,
-			   (const struct sgpu_comp *)g_table, verdict, save);
+	hipLaunchKernelGGL(f, dim3((n + KBLOCK - 1) / KBLOCK), dim3(KBLOCK), 0,
+			   stream, a);
 	int e = herr(hipGetLastError(), "kernel launch");
 	if (prof) {
-		(void)hipEventRecord(pe.b, (hipStream_t)stream);
-		pe.slot = (prot ? 16 : 0) + (mode ? 8 : 0) + (nr == 14 ? 4 : 0) +
-			  (mode ? 0 : shift);
-		pe.jobs = njobs;
+		(void)hipEventRecord(pe.b, stream);
+		pe.slot = slot;
+		pe.jobs = n;
 		pthread_mutex_lock(&g_prof_lock);
 		if (g_npev == g_pev_cap) {
 			size_t nc = g_pev_cap ? 2 * g_pev_cap : 64;
@@ -1108,6 +1210,69 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		pthread_mutex_unlock(&g_prof_lock);
 	}
 	return e;
+}
+
+static int prof_slot(int mode, int nr, int shift, int prot)
+{
+	return (prot ? 16 : 0) + (mode ? 8 : 0) + (nr == 14 ? 4 : 0) +
+	       (mode ? 0 : shift);
+}
+
+/*
+ * Launch one kernel over jobs[0..njobs).  The caller (host C) groups jobs
+ * so that one launch shares (mode, key size, shift class, direction).
+ */
+extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
+			      const struct sgpu_job *jobs, uint32_t njobs,
+			      uint8_t *verdict, uint32_t *save, int mode,
+			      int nr, int shift, int prot, void *stream)
+{
+	if (!njobs)
+		return 0;
+	kfn_t f = mode == SGPU_MODE_GCM ? pick_gcm<false>(nr, prot)
+					: pick_ctr<false>(nr, shift, prot);
+	if (!f) {
+		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
+			 mode, nr);
+		return EINVAL;
+	}
+	KArgs a;
+	memset(&a, 0, sizeof(a));
+	a.arena = arena;
+	a.asz = arena_size;
+	a.jobs = jobs;
+	a.njobs = njobs;
+	a.comps = (const struct sgpu_comp *)g_table;
+	a.verdict = verdict;
+	a.save = save;
+	return launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
+		      (hipStream_t)stream);
+}
+
+extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
+				const struct sgpu_compact *c, int mode, int nr,
+				int shift, int prot, void *stream)
+{
+	if (!c->n)
+		return 0;
+	kfn_t f = mode == SGPU_MODE_GCM ? pick_gcm<true>(nr, prot)
+					: pick_ctr<true>(nr, shift, prot);
+	if (!f) {
+		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
+			 mode, nr);
+		return EINVAL;
+	}
+	KArgs a;
+	memset(&a, 0, sizeof(a));
+	a.arena = arena;
+	a.asz = arena_size;
+	a.comps = (const struct sgpu_comp *)g_table;
+	a.verdict = c->verdict;
+	a.save = c->save;
+	a.c = *c;
+	return launch(f, a, c->n,
+		      c->undo ? -1 : prof_slot(mode, nr, shift, prot),
+		      (hipStream_t)stream);
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,
@@ -1225,4 +1390,36 @@ extern "C" int sgpu_get_device(void)
 	int d = -1;
 	(void)hipGetDevice(&d);
 	return d;
+}
+
+extern "C" void *sgpu_event_create(void)
+{
+	hipEvent_t e = NULL;
+	if (herr(hipEventCreateWithFlags(&e, hipEventDisableTiming),
+		 "event create"))
+		return NULL;
+	return (void *)e;
+}
+
+extern "C" void sgpu_event_destroy(void *ev)
+{
+	if (ev)
+		(void)hipEventDestroy((hipEvent_t)ev);
+}
+
+extern "C" int sgpu_event_record(void *ev, void *stream)
+{
+	return herr(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream),
+		    "event record");
+}
+
+extern "C" int sgpu_event_sync(void *ev)
+{
+	return herr(hipEventSynchronize((hipEvent_t)ev), "event sync");
+}
+
+extern "C" int sgpu_stream_wait(void *stream, void *ev)
+{
+	return herr(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0),
+		    "stream wait");
 }

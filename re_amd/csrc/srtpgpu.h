@@ -112,6 +112,52 @@ int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		     uint8_t *verdict, uint32_t *save, int mode, int nr,
 		     int shift, int prot, void *stream);
 
+/*
+ * Compact RTP path.  The host's sequential pass emits one 8-byte
+ * descriptor per packet; the kernel derives the rest of the job from the
+ * packet window (pos/end), the header it parsed (sgpu_hdr) and the session
+ * context -- exactly the fields plan_rtp_enc/plan_rtp_dec would set.
+ *   bits  0..15  (uint16_t)ix
+ *   bits 16..47  (uint32_t)(ix >> 16)
+ *   bits 48..63  SD_* flags
+ */
+enum {
+	SD_RUN      = 1u << 0,  /* packet has a GPU job (else host-decided) */
+	SD_CIPHER   = 1u << 1,  /* apply the keystream (dec HMAC: if tag ok) */
+	SD_ROC_M1   = 1u << 2,  /* trailer ROC = ixhi - 1 (receiver v=roc+1) */
+	SD_ROC_P1   = 1u << 3,  /* trailer ROC = ixhi + 1 (receiver v=roc-1) */
+};
+
+static inline uint64_t sgpu_desc(uint64_t ix, uint32_t flags)
+{
+	return (ix & 0xffffull) | ((uint64_t)(uint32_t)(ix >> 16) << 16) |
+	       ((uint64_t)flags << 48);
+}
+
+struct sgpu_hdr;
+
+struct sgpu_compact {
+	const uint32_t *pos;            /* packet start in arena (device) */
+	const uint32_t *end;            /* packet end (device) */
+	const struct sgpu_hdr *hdr;     /* parsed headers (device) */
+	const uint64_t *desc;           /* descriptors (device) */
+	const uint32_t *sess;           /* per-packet session index or NULL */
+	const uint32_t *compmap;        /* session index -> sgpu_comp index */
+	const uint32_t *idx;            /* packet list of this class, or NULL:
+					   packets base .. base+n-1 */
+	uint32_t base;
+	uint32_t n;
+	uint8_t *verdict;               /* [packet] SV_* (device) */
+	uint32_t *save;                 /* [packet] tag word under the ROC */
+	uint32_t *nfail;                /* +1 per speculation miss (device) */
+	int undo;                       /* restore the pre-call bytes */
+};
+
+/* launch the compact kernel of class (mode, nr, shift, prot) */
+int   sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
+		       const struct sgpu_compact *c, int mode, int nr,
+		       int shift, int prot, void *stream);
+
 /* store 4 raw bytes (LE word vals[i]) at arena + offs[i], any alignment
  * (restores tag bytes before a re-run) -- device arrays */
 int   sgpu_store_words(uint8_t *arena, const uint32_t *offs,
@@ -119,7 +165,7 @@ int   sgpu_store_words(uint8_t *arena, const uint32_t *offs,
 
 /* device-resident header parse: for each packet i, reads the RTP (or RTCP)
  * header at arena[pos[i]] bounded by end[i] and writes sgpu_hdr[i]. */
-struct sgpu_hdr {
+struct sgpu_hdr {               /* 12 bytes */
 	uint32_t ssrc;
 	uint16_t seq;
 	uint16_t err_pos;   /* bytes consumed before an EBADMSG (0 if ok) */
@@ -148,6 +194,11 @@ int   sgpu_device_sync(void);
 void *sgpu_stream_create(void);
 void  sgpu_stream_destroy(void *s);
 int   sgpu_set_device(int dev);
+void *sgpu_event_create(void);
+void  sgpu_event_destroy(void *ev);
+int   sgpu_event_record(void *ev, void *stream);
+int   sgpu_event_sync(void *ev);
+int   sgpu_stream_wait(void *stream, void *ev);
 int   sgpu_get_device(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,275 @@
+"""GPU parity of the compact descriptor path (srtp_*_batch fast path).
+
+The fast path (re_amd/csrc/host/srtp.c run_fast) must give exactly the
+results of the general engine (RE_SRTP_GENERAL=1), which the golden
+replays pin to the reference, and of the oracle called one packet at a
+time: same errno, pos/end, bytes and stream state.  Batches are adversarial:
+CSRC/extension headers (mixed kernel classes), 9 SSRCs in one session
+(ENOSR), seq jumps past 32768 (ETIMEDOUT), ROC wraps, reordering,
+truncated packets (EBADMSG), short capacity (ENOMEM), replays (EALREADY)
+and forged packets (EAUTH -> speculation miss -> undo + exact fold), with
+tiny chunks so the host/GPU pipeline crosses many chunk boundaries.
+"""
+import errno
+import os
+
+import numpy as np
+import pytest
+
+import re_amd.srtp as P
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def rtp_packet(rng, seq, ssrc, cc=0, x=False, plen=None):
+    b = bytearray([0x80 | (0x10 if x else 0) | cc, 96,
+                   (seq >> 8) & 0xff, seq & 0xff])
+    b += int(rng.integers(0, 1 << 32)).to_bytes(4, "big")
+    b += ssrc.to_bytes(4, "big")
+    for _ in range(cc):
+        b += int(rng.integers(0, 1 << 32)).to_bytes(4, "big")
+    if x:
+        xl = int(rng.integers(0, 4))
+        b += b"\xbe\xde" + xl.to_bytes(2, "big")
+        b += rng.integers(0, 256, 4 * xl, dtype=np.uint8).tobytes()
+    if plen is None:
+        plen = int(rng.integers(0, 300))
+    b += rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+    return bytes(b)
+
+
+def make_traffic(rng, n, nsess, enosr=True):
+    """[(session, packet bytes)] with per-stream sequence evolution"""
+    streams = {}
+    out = []
+    for _ in range(n):
+        s = int(rng.integers(0, nsess))
+        k = int(rng.integers(0, 9 if (enosr and s == 0) else 2))
+        ssrc = 0x1000 * (s + 1) + k
+        seq = streams.get(ssrc, int(rng.integers(0, 65536)))
+        r = rng.random()
+        if r < 0.80:
+            seq = (seq + 1) & 0xffff
+        elif r < 0.88:
+            seq = (seq + int(rng.integers(2, 200))) & 0xffff
+        elif r < 0.95:
+            seq = (seq - int(rng.integers(1, 40))) & 0xffff
+        elif r < 0.98:
+            seq = (seq + int(rng.integers(32769, 40000))) & 0xffff
+        else:
+            seq = (seq + 65000) & 0xffff
+        streams[ssrc] = seq
+        cc = int(rng.integers(0, 4)) if rng.random() < 0.3 else 0
+        x = rng.random() < 0.2
+        pkt = rtp_packet(rng, seq, ssrc, cc, x)
+        if rng.random() < 0.03:
+            pkt = pkt[:int(rng.integers(0, len(pkt)))]
+        out.append((s, pkt))
+    return out
+
+
+def to_arena(pkts, short_cap=()):
+    """(arena, pos, end, cap, sess) with 4-aligned starts and tag room"""
+    sizes = [len(p) + 80 for _, p in pkts]
+    base, off = [], 0
+    for sz in sizes:
+        base.append(off)
+        off += (sz + 15) & ~15
+    arena = np.zeros(off, dtype=np.uint8)
+    pos = np.zeros(len(pkts), dtype=np.uint32)
+    end = np.zeros(len(pkts), dtype=np.uint32)
+    cap = np.zeros(len(pkts), dtype=np.uint32)
+    for i, (_, p) in enumerate(pkts):
+        st = base[i] + 4 * (i % 3)
+        arena[st:st + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        pos[i], end[i] = st, st + len(p)
+        cap[i] = end[i] + (2 if i in short_cap else 60)
+    sess = np.array([s for s, _ in pkts], dtype=np.uint32)
+    return arena, pos, end, cap, sess
+
+
+def run(torch, opname, sessions, arena, pos, end, cap, sess, general,
+        chunk=None):
+    env_old = {k: os.environ.get(k) for k in ("RE_SRTP_GENERAL",
+                                               "RE_SRTP_CHUNK")}
+    try:
+        if general:
+            os.environ["RE_SRTP_GENERAL"] = "1"
+        else:
+            os.environ.pop("RE_SRTP_GENERAL", None)
+        if chunk:
+            os.environ["RE_SRTP_CHUNK"] = str(chunk)
+        else:
+            os.environ.pop("RE_SRTP_CHUNK", None)
+        dev = torch.from_numpy(arena.copy()).cuda()
+        p, e = pos.copy(), end.copy()
+        torch.cuda.synchronize()
+        rc, err = P.device_batch(opname, sessions, dev.data_ptr(),
+                                 arena.nbytes, p, e, cap, sess)
+        assert rc == 0, (rc, P.lib().srtp_gpu_error())
+        return dev.cpu().numpy(), p, e, err
+    finally:
+        for k, v in env_old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def states(sessions, ssrcs):
+    out = []
+    for s in sessions:
+        for x in ssrcs:
+            e, st = s.export(x)
+            out.append((e,) if e else (st.roc, st.s_l, st.s_l_set,
+                                       st.replay_rtp_bitmap,
+                                       st.replay_rtp_lix))
+    return out
+
+
+def keys_for(suite, nsess):
+    klen = P.key_len(suite) + P.salt_len(suite)
+    return [bytes((7 * s + i) & 0xff for i in range(klen))
+            for s in range(nsess)]
+
+
+@pytest.mark.parametrize("suite", list(range(6)))
+def test_fast_equals_general_and_oracle(suite, torch_cuda):
+    torch = torch_cuda
+    rng = np.random.default_rng(100 + suite)
+    nsess, n = 3, 1500
+    keys = keys_for(suite, nsess)
+    pkts = make_traffic(rng, n, nsess)
+    ssrcs = sorted({int.from_bytes(p[8:12], "big") for _, p in pkts
+                    if len(p) >= 12})
+    short = set()
+    arena, pos, end, cap, sess = to_arena(pkts, short)
+
+    txa = [P.Srtp(suite, k) for k in keys]
+    txb = [P.Srtp(suite, k) for k in keys]
+    ra = run(torch, "srtp_encrypt", txa, arena, pos, end, cap, sess, False,
+             chunk=200)
+    rb = run(torch, "srtp_encrypt", txb, arena, pos, end, cap, sess, True)
+    assert (ra[3] == rb[3]).all() and (ra[1] == rb[1]).all() and \
+        (ra[2] == rb[2]).all()
+    assert (ra[0] == rb[0]).all()
+    assert states(txa, ssrcs) == states(txb, ssrcs)
+    errs = ra[3]
+    assert (errs == 0).sum() > n // 2
+    assert {int(e) for e in errs} >= {0}
+
+    # oracle, one call at a time, on the packets with enough capacity
+    be = O.OracleBackend()
+    octx = [be.alloc(suite, k, 0)[0] for k in keys]
+    for i, (s, p) in enumerate(pkts):
+        if i in short:
+            continue
+        e, po, en, _, buf = be.call(octx[s], "srtp_encrypt", len(p) + 64, 0,
+                                    len(p), p, len(p) + 16)
+        got = (int(errs[i]), int(ra[1][i] - pos[i]), int(ra[2][i] - pos[i]))
+        assert got == (e, po, en), (i, got, (e, po, en))
+        if e == 0:
+            assert ra[0][pos[i]:ra[2][i]].tobytes() == buf[:en], i
+    for c in octx:
+        be.free(c)
+
+    # receive: protected packets, plus replays and forgeries
+    prot = []
+    for i, (s, _) in enumerate(pkts):
+        if errs[i] == 0:
+            prot.append((s, ra[0][pos[i]:ra[2][i]].tobytes()))
+    rx_pkts = []
+    for k, (s, p) in enumerate(prot):
+        rx_pkts.append((s, p))
+        r = rng.random()
+        if r < 0.03:
+            rx_pkts.append(prot[int(rng.integers(0, k + 1))])
+        elif r < 0.05:
+            q = bytearray(p)
+            q[int(rng.integers(12, len(q)))] ^= 0x40
+            rx_pkts.append((s, bytes(q)))
+    arena2, pos2, end2, cap2, sess2 = to_arena(rx_pkts)
+    rxa = [P.Srtp(suite, k) for k in keys]
+    rxb = [P.Srtp(suite, k) for k in keys]
+    da = run(torch, "srtp_decrypt", rxa, arena2, pos2, end2, cap2, sess2,
+             False, chunk=128)
+    db = run(torch, "srtp_decrypt", rxb, arena2, pos2, end2, cap2, sess2,
+             True)
+    assert (da[3] == db[3]).all(), np.flatnonzero(da[3] != db[3])[:10]
+    assert (da[1] == db[1]).all() and (da[2] == db[2]).all()
+    assert (da[0] == db[0]).all()
+    assert states(rxa, ssrcs) == states(rxb, ssrcs)
+    codes = {int(e) for e in da[3]}
+    assert {0, P.EAUTH, errno.EALREADY} <= codes, codes
+
+    # and against the oracle receiver
+    octx = [be.alloc(suite, k, 0)[0] for k in keys]
+    for i, (s, p) in enumerate(rx_pkts):
+        e, po, en, _, buf = be.call(octx[s], "srtp_decrypt", len(p) + 64, 0,
+                                    len(p), p, len(p))
+        got = (int(da[3][i]), int(da[1][i] - pos2[i]),
+               int(da[2][i] - pos2[i]))
+        assert got == (e, po, en), (i, got, (e, po, en))
+        assert da[0][pos2[i]:pos2[i] + len(buf)].tobytes() == buf, i
+    for c in octx:
+        be.free(c)
+    for c in txa + txb + rxa + rxb:
+        c.close()
+
+
+def test_fast_all_forged_single_chunk(torch_cuda):
+    """every packet forged: one speculation miss per packet, one undo"""
+    torch = torch_cuda
+    suite = 1
+    key = keys_for(suite, 1)[0]
+    rng = np.random.default_rng(5)
+    pkts = [(0, rtp_packet(rng, (65530 + i) & 0xffff, 0x42, plen=200))
+            for i in range(300)]
+    arena, pos, end, cap, sess = to_arena(pkts)
+    tx = P.Srtp(suite, key)
+    enc = run(torch, "srtp_encrypt", [tx], arena, pos, end, cap, None, False)
+    assert not enc[3].any()
+    forged = []
+    for i in range(300):
+        q = bytearray(enc[0][pos[i]:enc[2][i]].tobytes())
+        q[-1] ^= 1
+        forged.append((0, bytes(q)))
+    a2, p2, e2, c2, _ = to_arena(forged)
+    rxa, rxb = P.Srtp(suite, key), P.Srtp(suite, key)
+    da = run(torch, "srtp_decrypt", [rxa], a2, p2, e2, c2, None, False)
+    db = run(torch, "srtp_decrypt", [rxb], a2, p2, e2, c2, None, True)
+    assert (da[3] == P.EAUTH).all()
+    for x, y in zip(da, db):
+        assert (x == y).all()
+    assert states([rxa], [0x42]) == states([rxb], [0x42])
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_fast_short_capacity(suite, torch_cuda):
+    """device arenas cannot grow: ENOMEM, identical in both engines"""
+    torch = torch_cuda
+    rng = np.random.default_rng(33 + suite)
+    keys = keys_for(suite, 2)
+    pkts = make_traffic(rng, 400, 2, enosr=False)
+    short = set(rng.choice(400, 40, replace=False).tolist())
+    arena, pos, end, cap, sess = to_arena(pkts, short)
+    ssrcs = sorted({int.from_bytes(p[8:12], "big") for _, p in pkts
+                    if len(p) >= 12})
+    txa = [P.Srtp(suite, k) for k in keys]
+    txb = [P.Srtp(suite, k) for k in keys]
+    ra = run(torch, "srtp_encrypt", txa, arena, pos, end, cap, sess, False,
+             chunk=64)
+    rb = run(torch, "srtp_encrypt", txb, arena, pos, end, cap, sess, True)
+    assert errno.ENOMEM in {int(e) for e in ra[3]}
+    for x, y in zip(ra, rb):
+        assert (x == y).all()
+    assert states(txa, ssrcs) == states(txb, ssrcs)

@@ -975,6 +975,179 @@ __global__ void k_parse(const uint8_t *__restrict__ arena,
 	out[i] = h;
 }
 
+/* ------------------------------------------------------------------ */
+/* Device-side planning of a single-stream RTP batch (srtpgpu.h).      */
+
+#define PLAN_BLOCK 256
+
+/* sgpu_desc() (srtpgpu.h) on the device */
+__device__ __forceinline__ uint64_t d_desc(uint64_t ix, uint32_t flags)
+{
+	return (ix & 0xffffull) | ((uint64_t)(uint32_t)(ix >> 16) << 16) |
+	       ((uint64_t)flags << 48);
+}
+
+/* srtp_get_index (misc.c:22-41), including the int wrap of roc +- 1 */
+__device__ __forceinline__ int32_t plan_v(uint32_t roc, uint32_t s_l,
+					  uint32_t seq)
+{
+	if (s_l < 32768)
+		return ((int)seq - (int)s_l > 32768) ? (int32_t)(roc - 1)
+						     : (int32_t)roc;
+	return ((int)s_l - 32768 > (int)seq) ? (int32_t)(roc + 1)
+					     : (int32_t)roc;
+}
+
+/* speculated s_l seen by packet i: the previous packet's seq */
+__device__ __forceinline__ uint32_t plan_sb(const struct sgpu_plan_in &in,
+					    const struct sgpu_hdr *hdr,
+					    uint32_t i)
+{
+	if (i == 0)
+		return in.fresh ? hdr[0].seq : in.s_l;
+	return hdr[i - 1].seq;
+}
+
+/* ROC rollover seen by a packet (srtp.c:208-213, 318-321) */
+__device__ __forceinline__ bool plan_wrap(uint32_t seq, uint32_t sb)
+{
+	return (int)seq - (int)sb <= -32768;
+}
+
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_plan_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
+	     const uint32_t *pos, const uint32_t *end, uint32_t *bcnt,
+	     struct sgpu_plan_out *out)
+{
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	bool wrap = false;
+	uint32_t f = 0;
+	if (i < in.n) {
+		const struct sgpu_hdr h = hdr[i];
+		const uint32_t hl0 = hdr[0].hdr_len;
+		const uint32_t ssrc0 = in.ssrc_any ? hdr[0].ssrc : in.ssrc;
+		const uint32_t seq = h.seq, sb = plan_sb(in, hdr, i);
+		if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (((h.hdr_len ^ hl0) >> 2) & 3u)
+			f |= SPF_CLASS;
+		if (h.ssrc != ssrc0)
+			f |= SPF_SSRC;
+		if (!in.prot && h.hdr_len != 0xffffffffu &&
+		    end[i] - pos[i] - h.hdr_len < in.tag)
+			f |= SPF_PARSE;
+		if (!in.prot && (int)seq - (int)sb > 32768)
+			f |= SPF_TIMEOUT;
+		wrap = plan_wrap(seq, sb);
+		/* the next packet sees s_l = seq only if this one left it so */
+		if (i + 1 < in.n && !wrap && seq < sb)
+			f |= SPF_ORDER;
+		if (i == 0) {
+			out->ssrc0 = h.ssrc;
+			out->hl0 = h.hdr_len;
+		}
+		if (f)
+			atomicOr(&out->fail, f);
+	}
+	const int c = __syncthreads_count(wrap);
+	if (threadIdx.x == 0)
+		bcnt[blockIdx.x] = (uint32_t)c;
+}
+
+/* exclusive scan of the per-block wrap counts (one workgroup) */
+__global__ void __launch_bounds__(1024)
+k_plan_scan(uint32_t *bcnt, uint32_t nb, struct sgpu_plan_out *out)
+{
+	__shared__ uint32_t part[1024];
+	const uint32_t per = (nb + 1023u) / 1024u;
+	const uint32_t a = threadIdx.x * per;
+	uint32_t sum = 0;
+	for (uint32_t k = a; k < a + per && k < nb; k++)
+		sum += bcnt[k];
+	part[threadIdx.x] = sum;
+	__syncthreads();
+	for (uint32_t d = 1; d < 1024; d <<= 1) {
+		uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+		__syncthreads();
+		part[threadIdx.x] += v;
+		__syncthreads();
+	}
+	uint32_t run = part[threadIdx.x] - sum;
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
+		const uint32_t v = bcnt[k];
+		bcnt[k] = run;
+		run += v;
+	}
+	if (threadIdx.x == 1023)
+		out->wraps = part[1023];
+}
+
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_plan_desc(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
+	    const uint32_t *bpre, uint64_t *desc, struct sgpu_plan_out *out)
+{
+	__shared__ uint32_t wsum[PLAN_BLOCK / 64];
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	uint32_t seq = 0, sb = 0;
+	bool wrap = false;
+	if (i < in.n) {
+		seq = hdr[i].seq;
+		sb = plan_sb(in, hdr, i);
+		wrap = plan_wrap(seq, sb);
+	}
+	const uint64_t m = __ballot(wrap);
+	if (lane == 0)
+		wsum[wv] = (uint32_t)__popcll(m);
+	__syncthreads();
+	uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+	for (uint32_t k = 0; k < wv; k++)
+		pre += wsum[k];
+	if (i >= in.n)
+		return;
+	/* ROC after this packet's own rollover */
+	const uint32_t roc = in.roc + bpre[blockIdx.x] + pre + (wrap ? 1u : 0u);
+	uint64_t ix;
+	uint32_t fl = SD_RUN | SD_CIPHER;
+	if (in.prot) {
+		ix = 65536ull * roc + seq;              /* srtp.c:215 */
+	}
+	else {
+		const int32_t v = plan_v(roc, wrap ? 0u : sb, seq);
+		ix = seq + (uint64_t)(int64_t)v * 65536ull;
+		if ((uint32_t)v != roc)
+			fl |= (uint32_t)v + 1u == roc ? SD_ROC_P1 : SD_ROC_M1;
+		/* replay: every packet must be new (replay.c:32-62) */
+		bool ok;
+		if (i == 0) {
+			if (ix > in.lix)
+				ok = true;
+			else {
+				const uint64_t d = in.lix - ix;
+				ok = d < 64 && !(in.bitmap & (1ull << d));
+			}
+		}
+		else {
+			const uint32_t pseq = hdr[i - 1].seq;
+			const uint32_t psb = plan_sb(in, hdr, i - 1);
+			const bool pw = plan_wrap(pseq, psb);
+			const uint32_t proc = roc - (wrap ? 1u : 0u);
+			const int32_t pv = plan_v(proc, pw ? 0u : psb, pseq);
+			const uint64_t pix = pseq +
+					     (uint64_t)(int64_t)pv * 65536ull;
+			ok = ix > pix;
+		}
+		if (!ok)
+			atomicOr(&out->fail, (uint32_t)SPF_REPLAY);
+	}
+	desc[i] = d_desc(ix, fl);
+	const uint32_t t0 = in.n > SGPU_PLAN_TAIL ? in.n - SGPU_PLAN_TAIL : 0u;
+	if (i >= t0)
+		out->tail_ix[i - t0] = ix;
+	if (i + 1 == in.n)
+		out->s_l_last = wrap ? seq : (seq > sb ? seq : sb);
+}
+
 /* ================================================================== */
 /* C-ABI shim                                                          */
 
@@ -1422,4 +1595,26 @@ extern "C" int sgpu_stream_wait(void *stream, void *ev)
 {
 	return herr(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0),
 		    "stream wait");
+}
+
+extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
+			     const struct sgpu_hdr *hdr, const uint32_t *pos,
+			     const uint32_t *end, uint64_t *desc,
+			     uint32_t *scratch, struct sgpu_plan_out *out,
+			     void *stream)
+{
+	hipStream_t st = (hipStream_t)stream;
+	const uint32_t nb = (in->n + PLAN_BLOCK - 1) / PLAN_BLOCK;
+	if (!in->n)
+		return EINVAL;
+	int e = herr(hipMemsetAsync(out, 0, sizeof(*out), st), "plan memset");
+	if (e)
+		return e;
+	hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(PLAN_BLOCK), 0, st,
+			   *in, hdr, pos, end, scratch, out);
+	hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, scratch,
+			   nb, out);
+	hipLaunchKernelGGL(k_plan_desc, dim3(nb), dim3(PLAN_BLOCK), 0, st,
+			   *in, hdr, (const uint32_t *)scratch, desc, out);
+	return herr(hipGetLastError(), "plan launch");
 }

@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include "re_mem.h"
 #include "re_mbuf.h"
 #include "re_srtp.h"
@@ -985,6 +986,7 @@ struct ws {
 	struct pool dsc;        /* descriptors | class lists */
 	struct pool vs;         /* verdict | save | nfail */
 	struct pool cm;         /* session -> comp index */
+	struct pool pl;         /* device planner: out | scratch */
 	void **ev;              /* per-chunk parse events */
 	size_t nev;
 	struct ulog *ulog;      /* stream-state undo log */
@@ -1673,19 +1675,30 @@ struct fscan {
 	int log;
 	int mode;
 	uint32_t tag_len;
-	/* one-entry stream cache */
+	int nomem;
+	/* current stream, its state held in `cur` (flushed on a switch) */
 	struct srtp *ls;
 	uint32_t lssrc;
 	struct srtp_stream *lst;
-	int nomem;
+	struct srtp_stream cur;
 };
 
+static inline void fs_flush(struct fscan *F)
+{
+	if (F->lst)
+		*F->lst = F->cur;
+}
+
+/* the stream of (s, ssrc) as F->cur; NULL with *err on ENOSR/ENOMEM */
 static inline struct srtp_stream *fs_get(struct fscan *F, struct srtp *s,
 					 uint32_t ssrc, int *err)
 {
 	struct srtp_stream *st;
 	if (s == F->ls && ssrc == F->lssrc && F->lst)
-		return F->lst;
+		return &F->cur;
+	fs_flush(F);
+	F->lst = NULL;
+	F->ls = NULL;
 	*err = fs_stream(F->w, s, ssrc, F->epoch, F->log, &st);
 	if (*err) {
 		if (*err == ENOMEM)
@@ -1695,7 +1708,8 @@ static inline struct srtp_stream *fs_get(struct fscan *F, struct srtp *s,
 	F->ls = s;
 	F->lssrc = ssrc;
 	F->lst = st;
-	return st;
+	F->cur = *st;
+	return &F->cur;
 }
 
 static inline void fs_none(struct fscan *F, size_t i, int err, uint32_t pos)
@@ -1711,43 +1725,49 @@ static void scan_enc(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 	const uint32_t grow_by = F->mode == SGPU_MODE_GCM ? 16u : F->tag_len;
 	const uint32_t need = F->mode == SGPU_MODE_GCM ? 16u
 			      : (F->tag_len > 4 ? F->tag_len : 4u);
+	const struct sgpu_hdr *__restrict hd = F->hd;
+	uint64_t *__restrict desc = F->desc;
+	uint32_t *__restrict pos = F->pos, *__restrict endv = F->end;
+	const uint32_t *__restrict cap = F->cap;
+	int32_t *__restrict errv = F->err;
+	const uint32_t *__restrict sidx = F->sidx;
 	size_t i;
 	for (i = a; i < b; i++) {
-		struct srtp *s = F->sessv[F->sidx ? F->sidx[i] : 0];
-		const struct sgpu_hdr *h = &F->hd[i];
-		const uint32_t start = F->pos[i], end = F->end[i];
+		struct srtp *s = F->sessv[sidx ? sidx[i] : 0];
+		const struct sgpu_hdr h = hd[i];
+		const uint32_t start = pos[i], end = endv[i];
 		struct srtp_stream *st;
-		uint16_t seq = h->seq;
+		const uint16_t seq = h.seq;
 		int err = 0;
-		if (h->hdr_len == UINT32_MAX) {
-			fs_none(F, i, EBADMSG, start + h->err_pos);
+		if (h.hdr_len == UINT32_MAX) {
+			fs_none(F, i, EBADMSG, start + h.err_pos);
 			continue;
 		}
-		st = fs_get(F, s, h->ssrc, &err);
+		st = fs_get(F, s, h.ssrc, &err);
 		if (!st) {
-			fs_none(F, i, err, start + h->hdr_len);
+			fs_none(F, i, err, start + h.hdr_len);
 			continue;
 		}
 		if (!st->s_l_set) {
 			st->s_l = seq;
 			st->s_l_set = 1;
 		}
-		if ((uint64_t)end + need > F->cap[i]) {
-			fs_none(F, i, ENOMEM, start + h->hdr_len);
+		if ((uint64_t)end + need > cap[i]) {
+			fs_none(F, i, ENOMEM, start + h.hdr_len);
 			continue;
 		}
 		if ((int)seq - (int)st->s_l <= -32768) {
 			st->roc++;
 			st->s_l = 0;
 		}
-		F->desc[i] = sgpu_desc(65536ULL * st->roc + seq,
-				       SD_RUN | SD_CIPHER);
+		desc[i] = sgpu_desc(65536ULL * st->roc + seq, SD_RUN | SD_CIPHER);
 		if (seq > st->s_l)
 			st->s_l = seq;
-		F->err[i] = 0;
-		F->end[i] = end + grow_by;
-		cnt[(h->hdr_len >> 2) & 3]++;
+		errv[i] = 0;
+		endv[i] = end + grow_by;
+		cnt[(h.hdr_len >> 2) & 3]++;
 	}
+	fs_flush(F);
 }
 
 /* srtp_decrypt (srtp.c:288-432) over packets [a, b), speculating that
@@ -1756,23 +1776,28 @@ static void scan_dec(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 {
 	const int hmac = F->mode == SGPU_MODE_CTR;
 	const uint32_t T = hmac ? F->tag_len : 16u;
+	const struct sgpu_hdr *__restrict hd = F->hd;
+	uint64_t *__restrict desc = F->desc;
+	uint32_t *__restrict pos = F->pos, *__restrict endv = F->end;
+	int32_t *__restrict errv = F->err;
+	const uint32_t *__restrict sidx = F->sidx;
 	size_t i;
 	for (i = a; i < b; i++) {
-		struct srtp *s = F->sessv[F->sidx ? F->sidx[i] : 0];
-		const struct sgpu_hdr *h = &F->hd[i];
-		const uint32_t start = F->pos[i], end = F->end[i];
+		struct srtp *s = F->sessv[sidx ? sidx[i] : 0];
+		const struct sgpu_hdr h = hd[i];
+		const uint32_t start = pos[i], end = endv[i];
 		struct srtp_stream *st;
-		uint16_t seq = h->seq;
+		const uint16_t seq = h.seq;
 		uint32_t pld, fl = SD_RUN;
 		int32_t v;
 		uint64_t ix;
 		int diff, err = 0;
-		if (h->hdr_len == UINT32_MAX) {
-			fs_none(F, i, EBADMSG, start + h->err_pos);
+		if (h.hdr_len == UINT32_MAX) {
+			fs_none(F, i, EBADMSG, start + h.err_pos);
 			continue;
 		}
-		pld = start + h->hdr_len;
-		st = fs_get(F, s, h->ssrc, &err);
+		pld = start + h.hdr_len;
+		st = fs_get(F, s, h.ssrc, &err);
 		if (!st) {
 			fs_none(F, i, err, pld);
 			continue;
@@ -1804,47 +1829,61 @@ static void scan_dec(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 			fs_none(F, i, EBADMSG, pld);
 			continue;
 		}
-		F->end[i] = end - T;
-		if (hmac) {
-			struct replay rp = st->replay_rtp;
-			const int rp_ok = replay_check(&rp, ix);
-			st->replay_rtp = rp;
-			if (!rp_ok) {
-				F->desc[i] = sgpu_desc(ix, fl);
-				F->err[i] = EALREADY;
-				F->pos[i] = pld;
-				cnt[(h->hdr_len >> 2) & 3]++;
-				continue;
-			}
-			fl |= SD_CIPHER;
+		endv[i] = end - T;
+		/* replay (replay.c:32-62), checked after a verified MAC
+		 * (srtp.c:367) or tag (srtp.c:421) -- speculated verified */
+		if (!replay_check(&st->replay_rtp, ix)) {
+			desc[i] = sgpu_desc(ix, hmac ? fl : fl | SD_CIPHER);
+			errv[i] = EALREADY;
+			pos[i] = pld;
+			cnt[hmac ? (h.hdr_len >> 2) & 3 : 0]++;
+			continue;
 		}
-		else {
-			fl |= SD_CIPHER;
-			if (!replay_check(&st->replay_rtp, ix)) {
-				F->desc[i] = sgpu_desc(ix, fl);
-				F->err[i] = EALREADY;
-				F->pos[i] = pld;
-				cnt[0]++;
-				continue;
-			}
-		}
-		F->desc[i] = sgpu_desc(ix, fl);
+		desc[i] = sgpu_desc(ix, fl | SD_CIPHER);
 		if (seq > st->s_l)
 			st->s_l = seq;
-		F->err[i] = 0;
-		cnt[hmac ? (h->hdr_len >> 2) & 3 : 0]++;
+		errv[i] = 0;
+		cnt[hmac ? (h.hdr_len >> 2) & 3 : 0]++;
 	}
+	fs_flush(F);
 }
 
 struct flaunch {
 	uint32_t base, n, shift, has_idx;
 };
 
+static double now_ms(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 static size_t fast_chunk(void)
 {
 	const char *e = getenv("RE_SRTP_CHUNK");
 	long v = e ? atol(e) : 0;
 	return v >= 64 ? (size_t)v : (size_t)1 << 18;
+}
+
+/* replay state after the planned batch: the last <= 65 indices suffice
+ * (every index is new and increasing, so older bits have shifted out) */
+static struct replay plan_replay(const struct replay *r0,
+				 const struct sgpu_plan_out *o, size_t n)
+{
+	struct replay r = *r0;
+	size_t k, m = n < SGPU_PLAN_TAIL ? n : SGPU_PLAN_TAIL;
+	if (n > SGPU_PLAN_TAIL) {
+		r.lix = o->tail_ix[0];
+		r.bitmap = 1;
+		k = 1;
+	}
+	else {
+		k = 0;
+	}
+	for (; k < m; k++)
+		(void)replay_check(&r, o->tail_ix[k]);
+	return r;
 }
 
 /*
@@ -1858,6 +1897,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	const size_t n = b->n, CH = fast_chunk();
 	const size_t nch = (n + CH - 1) / CH;
 	const struct comp *c0 = &sessv[0]->rtp;
+	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
 	struct fscan F;
 	struct flaunch *fl = NULL;
 	size_t nfl = 0, i, k;
@@ -1869,7 +1909,13 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	uint32_t *save_d, *nfail_d, nfail = 0;
 	void *stream, *entry_ev = NULL;
 	struct ws *w;
-	int err = 0;
+	int err = 0, parsed = 0, planned = 0;
+	/* planned path: stream state before the call (undo) */
+	struct srtp *ps = sessv[0];
+	unsigned ps_n = ps->nstreams;
+	struct srtp_stream ps_old;
+	const int trace = getenv("RE_SRTP_TRACE") != NULL;
+	double t0 = trace ? now_ms() : 0, t1 = 0, t2 = 0, tscan = 0, twait = 0;
 
 	if (n == 0)
 		return -1;
@@ -1898,6 +1944,9 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		err = pool_reserve(w, &w->vs, n * 5 + 64);
 	if (!err)
 		err = pool_reserve(w, &w->cm, nsess * 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out) +
+				   (n / 256 + 8) * 4);
 	if (err)
 		return err;
 	if (w->nev < nch) {
@@ -1912,7 +1961,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			w->nev++;
 		}
 	}
-	fl = malloc(4 * nch * sizeof(*fl));
+	fl = malloc(4 * nch * sizeof(*fl) + 4 * sizeof(*fl));
 	if (!fl)
 		return ENOMEM;
 
@@ -1929,8 +1978,6 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	for (k = 0; k < nsess; k++)
 		cm_h[k] = sessv[k]->rtp.dev;
 
-	/* 1. parse stream: staged windows up, headers parsed, back down,
-	 *    chunk by chunk (ordered after the caller's prior work) */
 	entry_ev = w->ev[0];
 	if (b->stream) {
 		err = sgpu_event_record(entry_ev, stream);
@@ -1942,8 +1989,117 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->pstream);
 	if (!err && !prot)
 		err = sgpu_memset(nfail_d, 0, 4, w->pstream);
+	if (err)
+		goto out;
+
+	/* 0. one stream: plan on the device (speculative scan, verified) */
+	if (nsess == 1 && ps->nstreams <= 1 && !getenv("RE_SRTP_NOPLAN")) {
+		struct sgpu_plan_in in;
+		struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
+		struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
+		uint32_t *scr = (uint32_t *)(w->pl.d + sizeof(*po));
+		const struct srtp_stream *st0 =
+			ps->nstreams ? &ps->streams[0] : NULL;
+		const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
+				      (T > 4 ? T : 4u)) : 0u;
+		int capok = 1;
+
+		memset(&in, 0, sizeof(in));
+		in.n = (uint32_t)n;
+		in.prot = (uint32_t)prot;
+		in.fresh = !st0 || !st0->s_l_set;
+		in.ssrc_any = !st0;
+		in.ssrc = st0 ? st0->ssrc : 0;
+		in.roc = st0 ? st0->roc : 0;
+		in.s_l = st0 ? st0->s_l : 0;
+		in.lix = st0 ? st0->replay_rtp.lix : 0;
+		in.bitmap = st0 ? st0->replay_rtp.bitmap : 0;
+		in.tag = T;
+		memcpy(up_h, b->pos, n * 4);
+		memcpy(up_h + n, b->end, n * 4);
+		err = sgpu_memcpy_h2d(up_d, up_h, n * 8, w->pstream);
+		if (!err)
+			err = sgpu_parse_headers(b->arena, up_d, up_d + n, hd_d,
+						 NULL, (uint32_t)n, 0,
+						 w->pstream);
+		if (!err)
+			err = sgpu_plan_rtp(&in, hd_d, up_d, up_d + n, desc_d,
+					    scr, po_d, w->pstream);
+		if (!err)
+			err = sgpu_memcpy_d2h(po, po_d, sizeof(*po),
+					      w->pstream);
+		if (err)
+			goto out;
+		/* device arenas cannot grow (cap_short) */
+		if (prot)
+			for (i = 0; i < n; i++)
+				capok &= (uint64_t)b->end[i] + need <= b->cap[i];
+		err = sgpu_stream_sync(w->pstream);
+		if (err)
+			goto out;
+		parsed = 1;
+		if (trace)
+			fprintf(stderr, "re_srtp plan %s n=%zu: fail 0x%x "
+				"wraps %u cap %d (%.3f ms)\n", prot ? "enc" :
+				"dec", n, po->fail, po->wraps, capok,
+				now_ms() - t0);
+		if (!po->fail && capok) {
+			struct srtp_stream *st;
+			if (!prot && st0)
+				ps_old = *st0;
+			if (!st0) {
+				memset(&ps->streams[0], 0, sizeof(ps->streams[0]));
+				ps->streams[0].ssrc = po->ssrc0;
+				ps->nstreams = 1;
+			}
+			st = &ps->streams[0];
+			st->s_l_set = 1;
+			st->roc += po->wraps;
+			st->s_l = (uint16_t)po->s_l_last;
+			if (!prot)
+				st->replay_rtp = plan_replay(&st->replay_rtp, po,
+							     n);
+			fl[nfl++] = (struct flaunch){0, (uint32_t)n,
+						     (po->hl0 >> 2) & 3u, 0};
+			planned = 1;
+			/* pstream work is complete (synchronised above) */
+			{
+				struct sgpu_compact C = {
+					up_d, up_d + n, hd_d, desc_d, NULL,
+					(const uint32_t *)w->cm.d, NULL, 0,
+					(uint32_t)n, vd_d, save_d, nfail_d, 0};
+				err = sgpu_run_compact(b->arena,
+						       b->arena_size, &C,
+						       c0->mode, (int)c0->nr,
+						       (int)fl[0].shift, prot,
+						       stream);
+			}
+			if (err)
+				goto out;
+			/* per-packet results, while the GPU runs */
+			for (i = 0; i < n; i++) {
+				b->end[i] = prot ? b->end[i] + T : b->end[i] - T;
+				b->err[i] = 0;
+			}
+			if (trace)
+				t1 = t2 = now_ms();
+			goto finish;
+		}
+		/* not plannable: headers down for the host scan */
+		err = sgpu_memcpy_d2h(w->hd.h, hd_d, n * sizeof(*hd_d),
+				      w->pstream);
+		if (err)
+			goto out;
+	}
+
+	/* 1. parse stream: staged windows up, headers parsed, back down,
+	 *    chunk by chunk (ordered after the caller's prior work) */
 	for (k = 0; k < nch && !err; k++) {
 		const size_t a = k * CH, e = a + CH < n ? a + CH : n;
+		if (parsed) {
+			err = sgpu_event_record(w->ev[k], w->pstream);
+			continue;
+		}
 		memcpy(up_h + a, b->pos + a, (e - a) * 4);
 		memcpy(up_h + n + a, b->end + a, (e - a) * 4);
 		err = sgpu_memcpy_h2d(up_d + a, up_h + a, (e - a) * 4,
@@ -1971,8 +2127,17 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	}
 	if (err)
 		goto out;
+	if (parsed && b->sess) {
+		memcpy(up_h + 2 * n, b->sess, n * 4);
+		err = sgpu_memcpy_h2d(up_d + 2 * n, up_h + 2 * n, n * 4,
+				      stream);
+		if (err)
+			goto out;
+	}
 
 	/* 2. sequential scan per chunk, crypto launched behind it */
+	if (trace)
+		t1 = now_ms();
 	memset(&F, 0, sizeof(F));
 	F.w = w;
 	F.sessv = sessv;
@@ -1991,13 +2156,20 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	for (k = 0; k < nch && !err; k++) {
 		const size_t a = k * CH, e = a + CH < n ? a + CH : n;
 		uint32_t cnt[4] = {0, 0, 0, 0}, nz = 0, sh = 0, q;
+		double ta = trace ? now_ms() : 0, tb = 0;
 		err = sgpu_event_sync(w->ev[k]);
 		if (err)
 			break;
+		if (trace)
+			tb = now_ms();
 		if (prot)
 			scan_enc(&F, a, e, cnt);
 		else
 			scan_dec(&F, a, e, cnt);
+		if (trace) {
+			twait += tb - ta;
+			tscan += now_ms() - tb;
+		}
 		if (F.nomem) {
 			err = ENOMEM;
 			break;
@@ -2048,10 +2220,20 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 					       (int)fl[q].shift, prot, stream);
 		}
 	}
+	if (trace)
+		t2 = now_ms();
+ finish:
 	if (!err && !prot)
 		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
+	if (trace)
+		fprintf(stderr, "re_srtp fast %s n=%zu%s: stage %.3f ms, "
+			"parse-wait %.3f, scan %.3f, launch %.3f, tail %.3f, "
+			"total %.3f\n", prot ? "enc" : "dec", n,
+			planned ? " (device-planned)" : "", t1 - t0, twait,
+			tscan, t2 - t1 - twait - tscan, now_ms() - t2,
+			now_ms() - t0);
 	if (err)
 		goto out;
 	if (nfail) {
@@ -2071,6 +2253,11 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			err = sgpu_stream_sync(stream);
 		if (err)
 			goto out;
+		if (planned) {
+			if (ps_n)
+				ps->streams[0] = ps_old;
+			ps->nstreams = ps_n;
+		}
 		ulog_undo(w);
 		memcpy(b->pos, up_h, n * 4);
 		memcpy(b->end, up_h + n, n * 4);

@@ -158,6 +158,53 @@ int   sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		       const struct sgpu_compact *c, int mode, int nr,
 		       int shift, int prot, void *stream);
 
+/*
+ * Device-side planning of a single-stream RTP batch (the sequential state
+ * machine of srtp.c:203-213/279-280 and 310-321/426-427, misc.c:22-41,
+ * replay.c:32-62) as a speculative parallel scan: packet i is assumed to
+ * see s_l = seq[i-1]; ROC wraps are prefix-summed; every assumption is
+ * verified on the device.  out->fail != 0 means "plan on the host".
+ */
+struct sgpu_plan_in {
+	uint32_t n;
+	uint32_t prot;          /* 1 srtp_encrypt, 0 srtp_decrypt */
+	uint32_t fresh;         /* s_l not set yet (first RTP packet) */
+	uint32_t ssrc;          /* existing stream's SSRC (!fresh) */
+	uint32_t roc;
+	uint32_t s_l;
+	uint64_t lix;           /* replay_rtp */
+	uint64_t bitmap;
+	uint32_t tag;           /* bytes the tag adds / removes */
+	uint32_t ssrc_any;      /* no stream yet: take packet 0's SSRC */
+};
+
+enum {
+	SPF_PARSE   = 1u << 0,  /* EBADMSG / short packet */
+	SPF_SSRC    = 1u << 1,  /* more than one SSRC */
+	SPF_CLASS   = 1u << 2,  /* header lengths of different shift class */
+	SPF_ORDER   = 1u << 3,  /* s_l speculation broken (reordering) */
+	SPF_TIMEOUT = 1u << 4,  /* ETIMEDOUT */
+	SPF_REPLAY  = 1u << 5,  /* index not strictly increasing */
+	SPF_SIZE    = 1u << 6,  /* packet too long for 32-bit offsets */
+};
+
+#define SGPU_PLAN_TAIL 65
+struct sgpu_plan_out {
+	uint32_t fail;          /* SPF_* */
+	uint32_t wraps;         /* ROC increments over the batch */
+	uint32_t ssrc0;
+	uint32_t hl0;           /* header length of packet 0 */
+	uint32_t s_l_last;      /* s_l after the last packet */
+	uint32_t pad;
+	uint64_t tail_ix[SGPU_PLAN_TAIL]; /* ix of the last min(n,65) packets */
+};
+
+/* plan n packets (hdr/pos/end device arrays) into desc (device); scratch
+ * holds >= n/256 + 2 words; out is a device pointer */
+int   sgpu_plan_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
+		    const uint32_t *pos, const uint32_t *end, uint64_t *desc,
+		    uint32_t *scratch, struct sgpu_plan_out *out, void *stream);
+
 /* store 4 raw bytes (LE word vals[i]) at arena + offs[i], any alignment
  * (restores tag bytes before a re-run) -- device arrays */
 int   sgpu_store_words(uint8_t *arena, const uint32_t *offs,

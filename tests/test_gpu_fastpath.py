@@ -273,3 +273,75 @@ def test_fast_short_capacity(suite, torch_cuda):
     for x, y in zip(ra, rb):
         assert (x == y).all()
     assert states(txa, ssrcs) == states(txb, ssrcs)
+
+
+def seq_batch(rng, seqs, ssrc=0x5151, plen=160, csrc_at=()):
+    return [(0, rtp_packet(rng, s & 0xffff, ssrc, cc=1 if i in csrc_at else 0,
+                           plen=plen)) for i, s in enumerate(seqs)]
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_device_planner_and_its_fallbacks(suite, torch_cuda):
+    """Single-stream batches take the device planner; every broken
+    speculation (reorder, replay, ETIMEDOUT, mixed header classes, second
+    SSRC) must fall back with identical results.  Compared against the
+    host-planned fast path (RE_SRTP_NOPLAN) and the general engine, with
+    state carried across consecutive batches."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77 + suite)
+    key = keys_for(suite, 1)[0]
+    base = list(range(65000, 65000 + 3000))            # ROC wrap inside
+    cases = {
+        "inorder": (base, ()),
+        "reorder": (base[:700] + [base[701], base[700]] + base[702:], ()),
+        "classes": (base, (5, 900)),
+        "jump": (base[:1000] + [base[999] + 40000] + base[1000:], ()),
+        "dup": (base[:1500] + [base[1200]] + base[1500:], ()),
+    }
+    for name, (seqs, csrc_at) in cases.items():
+        pkts = seq_batch(rng, seqs, csrc_at=csrc_at)
+        if name == "dup":
+            pkts[1500] = pkts[1200]
+        arena, pos, end, cap, _ = to_arena(pkts)
+        half = len(pkts) // 2
+        parts = [(0, half), (half, len(pkts))]
+        res = {}
+        for mode in ("plan", "noplan", "general"):
+            tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
+            outs = []
+            for a, b in parts:
+                os.environ.pop("RE_SRTP_NOPLAN", None)
+                if mode == "noplan":
+                    os.environ["RE_SRTP_NOPLAN"] = "1"
+                sl = slice(a, b)
+                enc = run(torch, "srtp_encrypt", [tx], arena, pos[sl],
+                          end[sl], cap[sl], None, mode == "general")
+                os.environ.pop("RE_SRTP_NOPLAN", None)
+                outs.append(enc)
+            # receive what was sent (protected windows), same split
+            prot = []
+            for (a, b), enc in zip(parts, outs):
+                for j in range(b - a):
+                    i = a + j
+                    if enc[3][j] == 0:
+                        prot.append((0, enc[0][pos[i]:enc[2][j]].tobytes()))
+            a2, p2, e2, c2, _ = to_arena(prot)
+            h = len(prot) // 2
+            douts = []
+            for a, b in ((0, h), (h, len(prot))):
+                if mode == "noplan":
+                    os.environ["RE_SRTP_NOPLAN"] = "1"
+                sl = slice(a, b)
+                douts.append(run(torch, "srtp_decrypt", [rx], a2, p2[sl],
+                                 e2[sl], c2[sl], None, mode == "general"))
+                os.environ.pop("RE_SRTP_NOPLAN", None)
+            res[mode] = (outs, douts, states([tx], [0x5151]),
+                         states([rx], [0x5151]))
+            tx.close()
+            rx.close()
+        for mode in ("noplan", "general"):
+            A, B = res["plan"], res[mode]
+            for x, y in zip(A[0] + A[1], B[0] + B[1]):
+                for u, v in zip(x, y):
+                    assert (u == v).all(), (name, mode)
+            assert A[2] == B[2] and A[3] == B[3], (name, mode)

@@ -1,0 +1,19 @@
+/*
+ * ctr10.hip -- AES-128-CM + HMAC-SHA1 kernel instantiations (see k_ctr.h).
+ */
+#include "k_ctr.h"
+
+kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot)
+{
+#define PICK(C, U, S)                                                          \
+	if (compact == C && uni == U && shift == S)                            \
+		return prot ? k_ctr_hmac<10, S, true, C, U>                    \
+			    : k_ctr_hmac<10, S, false, C, U>;
+#define PICK4(C, U) PICK(C, U, 0) PICK(C, U, 1) PICK(C, U, 2) PICK(C, U, 3)
+	PICK4(false, false)
+	PICK4(true, false)
+	PICK4(true, true)
+#undef PICK4
+#undef PICK
+	return NULL;
+}

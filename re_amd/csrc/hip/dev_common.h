@@ -36,6 +36,23 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x)
 	return __builtin_amdgcn_perm(x, x, 0x00010203u);
 }
 
+/* gfx950 v_bitop3_b32: bit = TT[(a << 2) | (b << 1) | c] */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+/* SHA-1 Ch(b,c,d) = b ? c : d, Maj(b,c,d) (FIPS 180-4 4.1.1) */
+__device__ __forceinline__ uint32_t sha_ch(uint32_t b, uint32_t c, uint32_t d)
+{
+	return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+}
+
+__device__ __forceinline__ uint32_t sha_maj(uint32_t b, uint32_t c, uint32_t d)
+{
+	return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
+}
+
 /* LDS T-table address of byte k of x for this lane (laneoff = (lane&31)*4) */
 #define TT_ADDR(x, k, laneoff) \
 	__builtin_amdgcn_perm((x), (laneoff), 0x0C0C0000u | ((4u + (k)) << 8))
@@ -86,10 +103,10 @@ __device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
 		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo) + 128);
 		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
 		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
-		s0 = a0 ^ b1 ^ rot16(c2 ^ d3 ^ k[0]);
-		s1 = a1 ^ b2 ^ rot16(c3 ^ d0 ^ k[1]);
-		s2 = a2 ^ b3 ^ rot16(c0 ^ d1 ^ k[2]);
-		s3 = a3 ^ b0 ^ rot16(c1 ^ d2 ^ k[3]);
+		s0 = xor3(a0, b1, rot16(xor3(c2, d3, k[0])));
+		s1 = xor3(a1, b2, rot16(xor3(c3, d0, k[1])));
+		s2 = xor3(a2, b3, rot16(xor3(c0, d1, k[2])));
+		s3 = xor3(a3, b0, rot16(xor3(c1, d2, k[3])));
 	}
 	{
 		const uint32_t *k = rk + 4 * NR;
@@ -110,18 +127,20 @@ __device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
 		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo));
 		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
 		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
-		s0 = __builtin_amdgcn_perm(a0, b1, 0x0C0C0105u) ^
-		     __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu) ^ k[0];
-		s1 = __builtin_amdgcn_perm(a1, b2, 0x0C0C0105u) ^
-		     __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu) ^ k[1];
-		s2 = __builtin_amdgcn_perm(a2, b3, 0x0C0C0105u) ^
-		     __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu) ^ k[2];
-		s3 = __builtin_amdgcn_perm(a3, b0, 0x0C0C0105u) ^
-		     __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu) ^ k[3];
+		s0 = xor3(__builtin_amdgcn_perm(a0, b1, 0x0C0C0105u),
+			  __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu), k[0]);
+		s1 = xor3(__builtin_amdgcn_perm(a1, b2, 0x0C0C0105u),
+			  __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu), k[1]);
+		s2 = xor3(__builtin_amdgcn_perm(a2, b3, 0x0C0C0105u),
+			  __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu), k[2]);
+		s3 = xor3(__builtin_amdgcn_perm(a3, b0, 0x0C0C0105u),
+			  __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu), k[3]);
 	}
 }
 
 /* ---- SHA-1 compression, W[] holds the 16 big-endian message words ---- */
+/* Round = alignbit + bitop3 + 2 x add3 + alignbit; schedule = bitop3 (xor3)
+ * + xor + alignbit (FIPS 180-4 6.1.2, rolling 16-word W). */
 __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16])
 {
 	uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
@@ -131,8 +150,8 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16])
 		if ((i) < 16) {                                              \
 			wi = w[(i) & 15];                                    \
 		} else {                                                     \
-			wi = rotl32(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ \
-				    w[((i) + 2) & 15] ^ w[(i) & 15], 1);     \
+			wi = rotl32(xor3(w[((i) + 13) & 15], w[((i) + 8) & 15], \
+					 w[((i) + 2) & 15]) ^ w[(i) & 15], 1); \
 			w[(i) & 15] = wi;                                    \
 		}                                                            \
 		uint32_t t = rotl32(a, 5) + (f) + e + (K) + wi;              \
@@ -140,16 +159,16 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16])
 	} while (0)
 #pragma unroll
 	for (int i = 0; i < 20; i++)
-		SHA_ROUND(i, (d ^ (b & (c ^ d))), 0x5a827999u);
+		SHA_ROUND(i, sha_ch(b, c, d), 0x5a827999u);
 #pragma unroll
 	for (int i = 20; i < 40; i++)
-		SHA_ROUND(i, (b ^ c ^ d), 0x6ed9eba1u);
+		SHA_ROUND(i, xor3(b, c, d), 0x6ed9eba1u);
 #pragma unroll
 	for (int i = 40; i < 60; i++)
-		SHA_ROUND(i, ((b & c) | (d & (b | c))), 0x8f1bbcdcu);
+		SHA_ROUND(i, sha_maj(b, c, d), 0x8f1bbcdcu);
 #pragma unroll
 	for (int i = 60; i < 80; i++)
-		SHA_ROUND(i, (b ^ c ^ d), 0xca62c1d6u);
+		SHA_ROUND(i, xor3(b, c, d), 0xca62c1d6u);
 #undef SHA_ROUND
 	h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }

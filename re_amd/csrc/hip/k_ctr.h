@@ -1,0 +1,322 @@
+/*
+ * k_ctr.h -- fused AES-CM + HMAC-SHA1 kernel template (SRTP/SRTCP with the
+ * AES_CM_* suites).  Instantiated by ctr10.hip (AES-128) and ctr14.hip
+ * (AES-256).
+ */
+#pragma once
+#include "kern_common.h"
+
+/*
+ * Fused AES-CM + HMAC-SHA1, one packet per lane.
+ *   SHIFT = (c_off / 4) & 3: the cipher region starts SHIFT words into a
+ *   16-byte packet granule (3 for a 12-byte RTP header, 2 for SRTCP).
+ *   UNI: every packet of the launch uses one session context, so round
+ *   keys and HMAC midstates live in SGPRs (fewer VGPRs, more waves).
+ * Chunks wholly inside both the cipher region and the MAC input run a
+ * branch-free steady-state body; the header / tail chunks take the
+ * general byte-exact path.
+ */
+template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>
+__global__ void __launch_bounds__(CTR_BLOCK)
+__attribute__((amdgpu_waves_per_eu(UNI ? 4 : 1, 8)))
+k_ctr_hmac(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
+	tt_fill(smem, a.t0);
+	__syncthreads();
+
+	uint8_t *const arena = a.arena;
+	const uint64_t asz = a.asz;
+	uint8_t *__restrict__ verdict = a.verdict;
+	uint32_t *__restrict__ save = a.save;
+	const bool undo = COMPACT && a.c.undo;
+	struct sgpu_job j;
+	uint32_t i;
+	if (!get_job<COMPACT, SGPU_MODE_CTR, PROT>(
+		    a, blockIdx.x * blockDim.x + threadIdx.x, j, i))
+		return;
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	if (j.flags & SJ_SKIP) {
+		if (verdict && !undo)
+			verdict[i] = 0;
+		return;
+	}
+	const uint32_t ci = UNI ? __builtin_amdgcn_readfirstlane(j.comp)
+				: j.comp;
+	const struct sgpu_comp *cp = a.comps + ci;
+
+	uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+	for (int k = 0; k < NR + 1; k++) {
+		uint4 v = *(const uint4 *)&cp->rk[4 * k];
+		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
+		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
+	}
+	if (UNI) {
+#pragma unroll
+		for (int k = 0; k < 4 * (NR + 1); k++)
+			rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
+	}
+
+	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
+	const bool do_hmac = (j.flags & SJ_HMAC) != 0;
+	const bool trail = (j.flags & SJ_TRAILER) != 0;
+	const bool cipher_if_ok = !PROT && (j.flags & SJ_CIPHER_IF_OK);
+	const uint32_t c_off = j.c_off, c_end = j.c_off + j.c_len;
+	const uint32_t A = do_hmac ? j.a_len : 0;
+	const uint32_t data_end = max(c_end, A);
+	uint8_t *pkt = arena + j.off;
+	const uint64_t pasz = asz - j.off;   /* bytes addressable from pkt */
+
+	/* srtp_iv_calc (misc.c:76-87): k_s ^ (0, ssrc, ix>>16, ix<<16) */
+	uint32_t iv[4];
+	{
+		uint4 ks = *(const uint4 *)cp->k_s;
+		iv[0] = ks.x;
+		iv[1] = ks.y ^ bswap32(j.ssrc);
+		iv[2] = ks.z ^ bswap32(j.ixhi);
+		iv[3] = (ks.w ^ (bswap32(j.ixlo) >> 16)) & 0xffffu;
+	}
+
+	uint32_t h[5];
+	if (do_hmac) {
+		h[0] = cp->ipad[0]; h[1] = cp->ipad[1]; h[2] = cp->ipad[2];
+		h[3] = cp->ipad[3]; h[4] = cp->ipad[4];
+	}
+	const uint64_t X = trail ? ((uint64_t)j.trailer << 32 | 0x80000000u)
+				 : 0x8000000000000000ull;
+	const uint32_t tl = trail ? 4u : 0u;
+	const uint32_t nb = do_hmac ? (A + tl + 9u + 63u) / 64u : 0u;
+	const uint64_t bitlen = (uint64_t)(64u + A + tl) * 8u;
+	const uint32_t nck = do_cipher ? (c_end + 63u) / 64u : 0u;
+	const uint32_t nchunk = max(nb, nck);
+	const int32_t cw4 = (int32_t)(c_off >> 4);   /* (c_off/4) >> 2 */
+	const bool store_ct = do_cipher && (PROT || cipher_if_ok ||
+					    !do_hmac);
+	/* chunks [kf0, kf1) lie wholly inside the cipher region and the MAC
+	 * input: steady-state body */
+	uint32_t kf0 = nchunk, kf1 = nchunk;
+	if (do_cipher && do_hmac) {
+		kf0 = min((c_off + 63u) / 64u, nchunk);
+		kf1 = max(min(c_end, A) / 64u, kf0);
+	}
+
+	uint32_t carry[4] = {0, 0, 0, 0};
+
+	/* general chunk: any mix of header, cipher, MAC and padding */
+	auto chunk_general = [&](uint32_t k) {
+		const uint32_t c0 = 64u * k;
+		uint32_t d[16], w[16];
+#pragma unroll
+		for (int g = 0; g < 4; g++) {
+			uint4 v = make_uint4(0, 0, 0, 0);
+			if (c0 + 16u * g < data_end)
+				v = ld16(pkt, pasz, c0 + 16u * g);
+			d[4 * g] = v.x; d[4 * g + 1] = v.y;
+			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+		}
+		const bool mac = do_hmac && k < nb;
+		/* unprotect: the MAC covers the received ciphertext */
+		if (!PROT && mac) {
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				w[jj] = msg_word(16u * k + jj, bswap32(d[jj]), A,
+						 X);
+			if (k + 1 == nb) {
+				w[14] = (uint32_t)(bitlen >> 32);
+				w[15] = (uint32_t)bitlen;
+			}
+			sha1_compress(h, w);
+		}
+		const bool need_ks = do_cipher && (c0 + 64u > c_off) &&
+				     (c0 < c_end);
+		if (need_ks) {
+			uint32_t mask[16];
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++) {
+				const uint32_t bpos = c0 + 4u * jj;
+				const uint32_t nbytes =
+					(bpos >= c_off && bpos < c_end) ?
+					min(c_end - bpos, 4u) : 0u;
+				mask[jj] = nbytes >= 4 ? 0xffffffffu :
+					   ((1u << (8 * nbytes)) - 1u);
+			}
+			ks_xor<NR, SHIFT, true>(smem, lo, rk, iv,
+						(int32_t)(4 * k) - cw4, carry, d,
+						mask);
+			if (store_ct) {
+#pragma unroll
+				for (int jj = 0; jj < 16; jj++) {
+					const uint32_t bpos = c0 + 4u * jj;
+					if (bpos >= c_off && bpos < c_end) {
+						const uint32_t nbytes =
+							min(c_end - bpos, 4u);
+						if (nbytes == 4)
+							*(uint32_t *)(pkt + bpos) =
+								d[jj];
+						else
+							st_partial(pkt + bpos,
+								   d[jj], nbytes);
+					}
+				}
+			}
+		}
+		/* protect: the MAC covers the ciphertext just produced */
+		if (PROT && mac) {
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				w[jj] = msg_word(16u * k + jj, bswap32(d[jj]), A,
+						 X);
+			if (k + 1 == nb) {
+				w[14] = (uint32_t)(bitlen >> 32);
+				w[15] = (uint32_t)bitlen;
+			}
+			sha1_compress(h, w);
+		}
+	};
+
+	uint32_t k = 0;
+	for (; k < kf0; k++)
+		chunk_general(k);
+	for (; k < kf1; k++) {
+		const uint32_t c0 = 64u * k;
+		uint32_t d[16], w[16];
+#pragma unroll
+		for (int g = 0; g < 4; g++) {
+			const uint4 v = *(const uint4 *)(pkt + c0 + 16u * g);
+			d[4 * g] = v.x; d[4 * g + 1] = v.y;
+			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+		}
+		if (!PROT) {
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				w[jj] = bswap32(d[jj]);
+			sha1_compress(h, w);
+			/* reload the chunk (L1/L2 hit) rather than keep 16
+			 * VGPRs live across the compression */
+			asm volatile("" ::: "memory");
+#pragma unroll
+			for (int g = 0; g < 4; g++) {
+				const uint4 v = *(const uint4 *)(pkt + c0 + 16u * g);
+				d[4 * g] = v.x; d[4 * g + 1] = v.y;
+				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+			}
+		}
+		ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+					 (int32_t)(4 * k) - cw4, carry, d, NULL);
+		if (store_ct) {
+#pragma unroll
+			for (int g = 0; g < 4; g++)
+				*(uint4 *)(pkt + c0 + 16u * g) =
+					make_uint4(d[4 * g], d[4 * g + 1],
+						   d[4 * g + 2], d[4 * g + 3]);
+		}
+		if (PROT) {
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				w[jj] = bswap32(d[jj]);
+			sha1_compress(h, w);
+		}
+	}
+	for (; k < nchunk; k++)
+		chunk_general(k);
+
+	uint8_t vd = 0;
+	if (do_hmac) {
+		/* outer hash: opad midstate + 20-byte inner digest */
+		uint32_t w[16];
+		w[0] = h[0]; w[1] = h[1]; w[2] = h[2]; w[3] = h[3]; w[4] = h[4];
+		w[5] = 0x80000000u;
+#pragma unroll
+		for (int q = 6; q < 15; q++)
+			w[q] = 0;
+		w[15] = (64u + 20u) * 8u;
+		h[0] = cp->opad[0]; h[1] = cp->opad[1]; h[2] = cp->opad[2];
+		h[3] = cp->opad[3]; h[4] = cp->opad[4];
+		sha1_compress(h, w);
+
+		const uint32_t tag_len = cp->tag_len;
+		uint8_t *tp = pkt + j.tag_off;
+		if (PROT) {
+			for (uint32_t q = 0; q < tag_len; q++)
+				tp[q] = (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
+		}
+		else {
+			uint32_t diff = 0;
+			for (uint32_t q = 0; q < tag_len; q++)
+				diff |= tp[q] ^ (uint8_t)(h[q >> 2] >>
+							  (24 - 8 * (q & 3)));
+			vd = diff == 0 ? SV_TAG_OK : 0;
+			if (j.flags & SJ_ROC_AT_TAG) {
+				/* the reference writes the ROC over the tag
+				 * before comparing (srtp.c:342-344); keep the
+				 * original bytes for a possible re-run */
+				if (save)
+					save[i] = (uint32_t)tp[0] |
+						  (uint32_t)tp[1] << 8 |
+						  (uint32_t)tp[2] << 16 |
+						  (uint32_t)tp[3] << 24;
+				st_be32(tp, j.trailer);
+			}
+		}
+	}
+	if (PROT && (j.flags & SJ_STORE_TRAIL))
+		st_be32(pkt + j.t_off, j.trailer);
+
+	if (store_ct && !PROT)
+		vd |= SV_CIPHERED;
+
+	/* unprotect with decrypt-if-authentic: the plaintext was written
+	 * speculatively during the single pass; a forged packet is restored
+	 * by re-applying the keystream (rare path) */
+	if (cipher_if_ok && !(vd & SV_TAG_OK)) {
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+			carry[q] = 0;
+		for (uint32_t kk = 0; kk < nck; kk++) {
+			const uint32_t c0 = 64u * kk;
+			if (!(c0 + 64u > c_off && c0 < c_end))
+				continue;
+			uint32_t ksw[16], mask[16];
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++) {
+				ksw[jj] = 0;
+				mask[jj] = 0xffffffffu;
+			}
+			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+						 (int32_t)(4 * kk) - cw4, carry,
+						 ksw, mask);
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++) {
+				const uint32_t bpos = c0 + 4u * jj;
+				if (bpos >= c_off && bpos < c_end) {
+					uint32_t nbytes = min(c_end - bpos, 4u);
+					if (nbytes == 4) {
+						uint32_t *p = (uint32_t *)(pkt + bpos);
+						*p = *p ^ ksw[jj];
+					}
+					else {
+						uint32_t v = 0;
+						for (uint32_t q = 0; q < nbytes; q++)
+							v |= (uint32_t)pkt[bpos + q] << (8 * q);
+						st_partial(pkt + bpos, v ^ ksw[jj], nbytes);
+					}
+				}
+			}
+		}
+		vd &= (uint8_t)~SV_CIPHERED;
+	}
+	if (undo) {
+		/* compact undo: the word under the ROC back (srtp.c:342-344) */
+		uint8_t *tp = pkt + j.tag_off;
+		const uint32_t v = save[i];
+		tp[0] = (uint8_t)v; tp[1] = (uint8_t)(v >> 8);
+		tp[2] = (uint8_t)(v >> 16); tp[3] = (uint8_t)(v >> 24);
+		return;
+	}
+	if (COMPACT && !PROT && !(vd & SV_TAG_OK))
+		atomicAdd(a.c.nfail, 1u);
+	if (verdict)
+		verdict[i] = vd;
+}
+

@@ -1,0 +1,233 @@
+/*
+ * kern_common.h -- shared device code of the SRTP crypto kernels: arena
+ * access, CTR blocks, the SHA-1 message word of the MAC input, kernel
+ * arguments and the two job sources (general sgpu_job / compact
+ * descriptor).  Included by ctr10.hip, ctr14.hip and gcm.hip (one
+ * translation unit per kernel family, built in parallel).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include "../srtpgpu.h"
+#include "dev_common.h"
+
+#define KBLOCK 256
+#define CTR_BLOCK 512      /* 8 waves share one 64 KiB T-table image */
+
+/* ------------------------------------------------------------------ */
+/* memory helpers: packet starts are 4-byte aligned (host-checked)     */
+
+__device__ __forceinline__ uint4 ld16(const uint8_t *arena, uint64_t asz,
+				      uint64_t a)
+{
+	if (a + 16 <= asz)
+		return *(const uint4 *)(arena + a);
+	uint4 r = make_uint4(0, 0, 0, 0);
+	if (a + 4 <= asz)  r.x = *(const uint32_t *)(arena + a);
+	if (a + 8 <= asz)  r.y = *(const uint32_t *)(arena + a + 4);
+	if (a + 12 <= asz) r.z = *(const uint32_t *)(arena + a + 8);
+	return r;
+}
+
+/* store the low `n` bytes (1..3) of LE word v at p */
+__device__ __forceinline__ void st_partial(uint8_t *p, uint32_t v, uint32_t n)
+{
+	if (n >= 2) {
+		*(uint16_t *)p = (uint16_t)v;
+		if (n == 3)
+			p[2] = (uint8_t)(v >> 16);
+	}
+	else if (n == 1) {
+		p[0] = (uint8_t)v;
+	}
+}
+
+/* big-endian 32-bit word to 4 byte stores (arbitrary alignment) */
+__device__ __forceinline__ void st_be32(uint8_t *p, uint32_t v)
+{
+	p[0] = (uint8_t)(v >> 24);
+	p[1] = (uint8_t)(v >> 16);
+	p[2] = (uint8_t)(v >> 8);
+	p[3] = (uint8_t)v;
+}
+
+/* ------------------------------------------------------------------ */
+/* CTR keystream block b (IV + b, 128-bit big-endian add, OpenSSL
+ * CRYPTO_ctr128_encrypt semantics) */
+template <int NR>
+__device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
+					  const uint32_t *rk, const uint32_t iv[4],
+					  int32_t b, uint32_t ks[4])
+{
+	uint64_t c = ((uint64_t)bswap32(iv[2]) << 32 | bswap32(iv[3])) +
+		     (uint64_t)(int64_t)b;
+	uint32_t s0 = iv[0], s1 = iv[1];
+	uint32_t s2 = bswap32((uint32_t)(c >> 32));
+	uint32_t s3 = bswap32((uint32_t)c);
+	aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
+	ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
+}
+
+/* the SHA-1 input word at global word index gw of the HMAC message
+ * M = data[0,A) ‖ (trailer?) ‖ 0x80 ‖ 0* ‖ len64 -- for non-fast chunks */
+__device__ __forceinline__ uint32_t msg_word(uint32_t gw, uint32_t data_be,
+					     uint32_t A, uint64_t X)
+{
+	uint32_t aw = A >> 2, u = A & 3;
+	if (gw < aw)
+		return data_be;
+	if (gw == aw)
+		return (u ? (data_be & (0xFFFFFFFFu << (32 - 8 * u))) : 0u) |
+		       (uint32_t)(X >> (32 + 8 * u));
+	if (gw == aw + 1)
+		return (uint32_t)(X >> (8 * u));
+	return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* kernel arguments and job sources                                    */
+
+struct KArgs {
+	const uint32_t *t0;             /* AES T0 table (device, 1 KiB) */
+	uint8_t *arena;
+	uint64_t asz;
+	const struct sgpu_job *jobs;    /* general path */
+	uint32_t njobs;
+	const struct sgpu_comp *comps;
+	uint8_t *verdict;
+	uint32_t *save;
+	struct sgpu_compact c;          /* compact path */
+};
+
+/*
+ * Job of thread t.  General path: jobs[t], results at slot t.  Compact
+ * path: packet p = idx[base+t] (or base+t); the job is derived exactly as
+ * plan_rtp_enc / plan_rtp_dec (re_amd/csrc/host/srtp.c) build it, from the
+ * packet window, the parsed header and the 8-byte descriptor
+ * (srtp.c:215-277, 325-382, 383-424 of the reference).
+ */
+template <bool COMPACT, int MODE, bool PROT>
+__device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
+					struct sgpu_job &j, uint32_t &slot)
+{
+	if (!COMPACT) {
+		if (t >= a.njobs)
+			return false;
+		j = a.jobs[t];
+		slot = t;
+		return true;
+	}
+	const struct sgpu_compact &c = a.c;
+	if (t >= c.n)
+		return false;
+	const uint32_t p = c.idx ? c.idx[c.base + t] : c.base + t;
+	slot = p;
+	const uint64_t d = c.desc[p];
+	const uint32_t fl = (uint32_t)(d >> 48);
+	j.flags = SJ_SKIP;
+	j.comp = 0;
+	if (!(fl & SD_RUN))
+		return true;
+	uint8_t vd = 0;
+	if (c.undo) {
+		vd = a.verdict[p];
+		if (MODE == SGPU_MODE_GCM && !(vd & SV_CIPHERED))
+			return true;
+	}
+	const uint32_t comp = c.compmap[c.sess ? c.sess[p] : 0u];
+	const uint32_t off = c.pos[p];
+	const uint32_t L = c.end[p] - off;
+	const uint32_t *hw = (const uint32_t *)(c.hdr + p);
+	const uint32_t ssrc = hw[0], hl = hw[2];
+	const uint32_t ixhi = (uint32_t)(d >> 16);
+	j.off = off;
+	j.comp = comp;
+	j.ssrc = ssrc;
+	j.ixhi = ixhi;
+	j.ixlo = (uint32_t)(d & 0xffffu);
+	j.trailer = ixhi + ((fl & SD_ROC_P1) ? 1u : 0u) -
+		    ((fl & SD_ROC_M1) ? 1u : 0u);
+	j.t_off = 0;
+	j.c_off = hl;
+	if (MODE == SGPU_MODE_CTR) {
+		if (PROT) {
+			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_HMAC | SJ_TRAILER;
+			j.a_len = L;
+			j.c_len = L - hl;
+			j.tag_off = L;
+		}
+		else {
+			const uint32_t T = a.comps[comp].tag_len;
+			j.a_len = L - T;
+			j.tag_off = L - T;
+			j.c_len = L - T - hl;
+			if (c.undo)
+				j.flags = (vd & SV_CIPHERED) ? SJ_CIPHER : 0u;
+			else
+				j.flags = SJ_HMAC | SJ_TRAILER | SJ_ROC_AT_TAG |
+					  ((fl & SD_CIPHER) ?
+					   (SJ_CIPHER | SJ_CIPHER_IF_OK) : 0u);
+		}
+	}
+	else {
+		j.a_len = hl;
+		if (PROT) {
+			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_GCM;
+			j.c_len = L - hl;
+			j.tag_off = L;
+		}
+		else {
+			j.flags = c.undo ? (SJ_GCM | SJ_CIPHER | SJ_UNDO)
+					 : (SJ_GCM | SJ_CIPHER);
+			j.c_len = L - 16u - hl;
+			j.tag_off = L - 16u;
+		}
+	}
+	return true;
+}
+
+/*
+ * XOR the keystream into the 16 words d[] of chunk k as each AES block is
+ * produced (no 16-word keystream buffer).  Word jj of the chunk takes
+ * keystream word jj - SHIFT of block blk0 = 4k - cw4; the first SHIFT words
+ * take the tail of the previous chunk's last block (carry).  mask[]: per
+ * word byte mask of the cipher region (all ones in the steady state).
+ */
+template <int NR, int SHIFT, bool MASKED>
+__device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
+				       const uint32_t *rk, const uint32_t iv[4],
+				       int32_t blk0, uint32_t carry[4],
+				       uint32_t d[16], const uint32_t *mask)
+{
+#pragma unroll
+	for (int q = 0; q < SHIFT; q++)
+		d[q] ^= MASKED ? (carry[4 - SHIFT + q] & mask[q])
+			       : carry[4 - SHIFT + q];
+#pragma unroll
+	for (int m = 0; m < 4; m++) {
+		uint32_t B[4];
+		ctr_block<NR>(smem, lo, rk, iv, blk0 + m, B);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const int jj = SHIFT + 4 * m + q;
+			if (jj < 16)
+				d[jj] ^= MASKED ? (B[q] & mask[jj]) : B[q];
+			else
+				carry[q] = B[q];
+		}
+		if (m == 3 && SHIFT == 0) {
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				carry[q] = B[q];
+		}
+	}
+}
+
+
+typedef void (*kfn_t)(const KArgs);
+
+/* kernel pickers, one per translation unit */
+kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);
+kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
+kfn_t sgpu_pick_gcm(bool compact, int nr, int prot);

@@ -1,6 +1,7 @@
 /*
- * srtp_kernels.hip -- MI355X (gfx950) kernels for SRTP/SRTCP protect and
- * unprotect, plus the thin C-ABI shim declared in ../srtpgpu.h.
+ * srtp_kernels.hip -- MI355X (gfx950) session setup, header parse and
+ * device planner kernels, plus the thin C-ABI shim declared in ../srtpgpu.h.
+ * The crypto kernels live in ctr10.hip, ctr14.hip and gcm.hip.
  *
  * Work decomposition: ONE PACKET PER LANE.  SHA-1 is a serial chain of
  * 80-round compressions per packet (20 of them for a 1200-B RTP packet), so
@@ -29,682 +30,11 @@
 #include <stdio.h>
 #include <string.h>
 #include "../srtpgpu.h"
-#include "dev_common.h"
+#include "kern_common.h"
 
-#define KBLOCK 256
 
 __device__ uint32_t g_T0[256];          /* T0 table (source of LDS image) */
 __device__ uint8_t g_sbox[256];
-
-/* OpenSSL gcm_gmult_4bit rem_4bit (values << 16 into the top word) */
-__constant__ uint32_t c_rem4[16] = {
-	0x0000u << 16, 0x1C20u << 16, 0x3840u << 16, 0x2460u << 16,
-	0x7080u << 16, 0x6CA0u << 16, 0x48C0u << 16, 0x54E0u << 16,
-	0xE100u << 16, 0xFD20u << 16, 0xD940u << 16, 0xC560u << 16,
-	0x9180u << 16, 0x8DA0u << 16, 0xA9C0u << 16, 0xB5E0u << 16,
-};
-
-/* ------------------------------------------------------------------ */
-/* memory helpers: packet starts are 4-byte aligned (host-checked)     */
-
-__device__ __forceinline__ uint4 ld16(const uint8_t *arena, uint64_t asz,
-				      uint64_t a)
-{
-	if (a + 16 <= asz)
-		return *(const uint4 *)(arena + a);
-	uint4 r = make_uint4(0, 0, 0, 0);
-	if (a + 4 <= asz)  r.x = *(const uint32_t *)(arena + a);
-	if (a + 8 <= asz)  r.y = *(const uint32_t *)(arena + a + 4);
-	if (a + 12 <= asz) r.z = *(const uint32_t *)(arena + a + 8);
-	return r;
-}
-
-/* store the low `n` bytes (1..3) of LE word v at p */
-__device__ __forceinline__ void st_partial(uint8_t *p, uint32_t v, uint32_t n)
-{
-	if (n >= 2) {
-		*(uint16_t *)p = (uint16_t)v;
-		if (n == 3)
-			p[2] = (uint8_t)(v >> 16);
-	}
-	else if (n == 1) {
-		p[0] = (uint8_t)v;
-	}
-}
-
-/* big-endian 32-bit word to 4 byte stores (arbitrary alignment) */
-__device__ __forceinline__ void st_be32(uint8_t *p, uint32_t v)
-{
-	p[0] = (uint8_t)(v >> 24);
-	p[1] = (uint8_t)(v >> 16);
-	p[2] = (uint8_t)(v >> 8);
-	p[3] = (uint8_t)v;
-}
-
-/* ------------------------------------------------------------------ */
-/* CTR keystream block b (IV + b, 128-bit big-endian add, OpenSSL
- * CRYPTO_ctr128_encrypt semantics) */
-template <int NR>
-__device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
-					  const uint32_t *rk, const uint32_t iv[4],
-					  int32_t b, uint32_t ks[4])
-{
-	uint64_t c = ((uint64_t)bswap32(iv[2]) << 32 | bswap32(iv[3])) +
-		     (uint64_t)(int64_t)b;
-	uint32_t s0 = iv[0], s1 = iv[1];
-	uint32_t s2 = bswap32((uint32_t)(c >> 32));
-	uint32_t s3 = bswap32((uint32_t)c);
-	aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
-	ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
-}
-
-/* the SHA-1 input word at global word index gw of the HMAC message
- * M = data[0,A) ‖ (trailer?) ‖ 0x80 ‖ 0* ‖ len64 -- for non-fast chunks */
-__device__ __forceinline__ uint32_t msg_word(uint32_t gw, uint32_t data_be,
-					     uint32_t A, uint64_t X)
-{
-	uint32_t aw = A >> 2, u = A & 3;
-	if (gw < aw)
-		return data_be;
-	if (gw == aw)
-		return (u ? (data_be & (0xFFFFFFFFu << (32 - 8 * u))) : 0u) |
-		       (uint32_t)(X >> (32 + 8 * u));
-	if (gw == aw + 1)
-		return (uint32_t)(X >> (8 * u));
-	return 0;
-}
-
-/* ------------------------------------------------------------------ */
-/* kernel arguments and job sources                                    */
-
-struct KArgs {
-	uint8_t *arena;
-	uint64_t asz;
-	const struct sgpu_job *jobs;    /* general path */
-	uint32_t njobs;
-	const struct sgpu_comp *comps;
-	uint8_t *verdict;
-	uint32_t *save;
-	struct sgpu_compact c;          /* compact path */
-};
-
-/*
- * Job of thread t.  General path: jobs[t], results at slot t.  Compact
- * path: packet p = idx[base+t] (or base+t); the job is derived exactly as
- * plan_rtp_enc / plan_rtp_dec (re_amd/csrc/host/srtp.c) build it, from the
- * packet window, the parsed header and the 8-byte descriptor
- * (srtp.c:215-277, 325-382, 383-424 of the reference).
- */
-template <bool COMPACT, int MODE, bool PROT>
-__device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
-					struct sgpu_job &j, uint32_t &slot)
-{
-	if (!COMPACT) {
-		if (t >= a.njobs)
-			return false;
-		j = a.jobs[t];
-		slot = t;
-		return true;
-	}
-	const struct sgpu_compact &c = a.c;
-	if (t >= c.n)
-		return false;
-	const uint32_t p = c.idx ? c.idx[c.base + t] : c.base + t;
-	slot = p;
-	const uint64_t d = c.desc[p];
-	const uint32_t fl = (uint32_t)(d >> 48);
-	j.flags = SJ_SKIP;
-	j.comp = 0;
-	if (!(fl & SD_RUN))
-		return true;
-	uint8_t vd = 0;
-	if (c.undo) {
-		vd = a.verdict[p];
-		if (MODE == SGPU_MODE_GCM && !(vd & SV_CIPHERED))
-			return true;
-	}
-	const uint32_t comp = c.compmap[c.sess ? c.sess[p] : 0u];
-	const uint32_t off = c.pos[p];
-	const uint32_t L = c.end[p] - off;
-	const uint32_t *hw = (const uint32_t *)(c.hdr + p);
-	const uint32_t ssrc = hw[0], hl = hw[2];
-	const uint32_t ixhi = (uint32_t)(d >> 16);
-	j.off = off;
-	j.comp = comp;
-	j.ssrc = ssrc;
-	j.ixhi = ixhi;
-	j.ixlo = (uint32_t)(d & 0xffffu);
-	j.trailer = ixhi + ((fl & SD_ROC_P1) ? 1u : 0u) -
-		    ((fl & SD_ROC_M1) ? 1u : 0u);
-	j.t_off = 0;
-	j.c_off = hl;
-	if (MODE == SGPU_MODE_CTR) {
-		if (PROT) {
-			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_HMAC | SJ_TRAILER;
-			j.a_len = L;
-			j.c_len = L - hl;
-			j.tag_off = L;
-		}
-		else {
-			const uint32_t T = a.comps[comp].tag_len;
-			j.a_len = L - T;
-			j.tag_off = L - T;
-			j.c_len = L - T - hl;
-			if (c.undo)
-				j.flags = (vd & SV_CIPHERED) ? SJ_CIPHER : 0u;
-			else
-				j.flags = SJ_HMAC | SJ_TRAILER | SJ_ROC_AT_TAG |
-					  ((fl & SD_CIPHER) ?
-					   (SJ_CIPHER | SJ_CIPHER_IF_OK) : 0u);
-		}
-	}
-	else {
-		j.a_len = hl;
-		if (PROT) {
-			j.flags = SJ_PROTECT | SJ_CIPHER | SJ_GCM;
-			j.c_len = L - hl;
-			j.tag_off = L;
-		}
-		else {
-			j.flags = c.undo ? (SJ_GCM | SJ_CIPHER | SJ_UNDO)
-					 : (SJ_GCM | SJ_CIPHER);
-			j.c_len = L - 16u - hl;
-			j.tag_off = L - 16u;
-		}
-	}
-	return true;
-}
-
-/*
- * Fused AES-CM + HMAC-SHA1, one packet per lane.
- *   SHIFT = (c_off / 4) & 3: the cipher region starts SHIFT words into a
- *   16-byte packet granule (3 for a 12-byte RTP header, 2 for SRTCP).
- */
-template <int NR, int SHIFT, bool PROT, bool COMPACT>
-__global__ void __launch_bounds__(KBLOCK)
-k_ctr_hmac(const KArgs a)
-{
-	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
-	tt_fill(smem, g_T0);
-	__syncthreads();
-
-	uint8_t *const arena = a.arena;
-	const uint64_t asz = a.asz;
-	const struct sgpu_comp *__restrict__ comps = a.comps;
-	uint8_t *__restrict__ verdict = a.verdict;
-	uint32_t *__restrict__ save = a.save;
-	const bool undo = COMPACT && a.c.undo;
-	struct sgpu_job j;
-	uint32_t i;
-	if (!get_job<COMPACT, SGPU_MODE_CTR, PROT>(
-		    a, blockIdx.x * blockDim.x + threadIdx.x, j, i))
-		return;
-	const uint32_t lo = (threadIdx.x & 31u) * 4u;
-	if (j.flags & SJ_SKIP) {
-		if (verdict && !undo)
-			verdict[i] = 0;
-		return;
-	}
-	const struct sgpu_comp *cp = comps + j.comp;
-
-	uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-	for (int k = 0; k < NR + 1; k++) {
-		uint4 v = *(const uint4 *)&cp->rk[4 * k];
-		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
-		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
-	}
-
-	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
-	const bool do_hmac = (j.flags & SJ_HMAC) != 0;
-	const bool trail = (j.flags & SJ_TRAILER) != 0;
-	const bool cipher_if_ok = !PROT && (j.flags & SJ_CIPHER_IF_OK);
-	const uint32_t c_off = j.c_off, c_end = j.c_off + j.c_len;
-	const uint32_t A = do_hmac ? j.a_len : 0;
-	const uint32_t data_end = max(c_end, A);
-	uint8_t *pkt = arena + j.off;
-	const uint64_t pasz = asz - j.off;   /* bytes addressable from pkt */
-
-	/* srtp_iv_calc (misc.c:76-87): k_s ^ (0, ssrc, ix>>16, ix<<16) */
-	uint32_t iv[4];
-	{
-		uint4 ks = *(const uint4 *)cp->k_s;
-		iv[0] = ks.x;
-		iv[1] = ks.y ^ bswap32(j.ssrc);
-		iv[2] = ks.z ^ bswap32(j.ixhi);
-		iv[3] = (ks.w ^ (bswap32(j.ixlo) >> 16)) & 0xffffu;
-	}
-
-	uint32_t h[5];
-	if (do_hmac) {
-		h[0] = cp->ipad[0]; h[1] = cp->ipad[1]; h[2] = cp->ipad[2];
-		h[3] = cp->ipad[3]; h[4] = cp->ipad[4];
-	}
-	const uint64_t X = trail ? ((uint64_t)j.trailer << 32 | 0x80000000u)
-				 : 0x8000000000000000ull;
-	const uint32_t tl = trail ? 4u : 0u;
-	const uint32_t nb = do_hmac ? (A + tl + 9u + 63u) / 64u : 0u;
-	const uint64_t bitlen = (uint64_t)(64u + A + tl) * 8u;
-	const uint32_t nck = do_cipher ? (c_end + 63u) / 64u : 0u;
-	const uint32_t nchunk = max(nb, nck);
-	const int32_t cw4 = (int32_t)(c_off >> 4);   /* (c_off/4) >> 2 */
-	const bool store_ct = do_cipher && (PROT || cipher_if_ok ||
-					    !do_hmac);
-
-	uint32_t carry[4] = {0, 0, 0, 0};
-
-	for (uint32_t k = 0; k < nchunk; k++) {
-		const uint32_t c0 = 64u * k;
-		uint32_t d[16];
-		/* ---- load ---- */
-#pragma unroll
-		for (int g = 0; g < 4; g++) {
-			uint4 v = make_uint4(0, 0, 0, 0);
-			if (c0 + 16u * g < data_end)
-				v = ld16(pkt, pasz, c0 + 16u * g);
-			d[4 * g] = v.x; d[4 * g + 1] = v.y;
-			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
-		}
-		/* ---- keystream ---- */
-		uint32_t ksw[16];
-		const bool need_ks = do_cipher && (c0 + 64u > c_off) &&
-				     (c0 < c_end);
-		if (need_ks) {
-			uint32_t B[4][4];
-#pragma unroll
-			for (int m = 0; m < 4; m++)
-				ctr_block<NR>(smem, lo, rk, iv,
-					      (int32_t)(4 * k) - cw4 + m, B[m]);
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				if (SHIFT == 0)
-					ksw[jj] = B[jj >> 2][jj & 3];
-				else if (jj < SHIFT)
-					ksw[jj] = carry[jj + 4 - SHIFT];
-				else
-					ksw[jj] = B[(jj - SHIFT) >> 2][(jj - SHIFT) & 3];
-			}
-#pragma unroll
-			for (int q = 0; q < 4; q++)
-				carry[q] = B[3][q];
-		}
-		else {
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				ksw[jj] = 0;
-		}
-
-		const bool fast = (c0 + 64u <= data_end) &&
-				  (!do_cipher || (c0 >= c_off && c0 + 64u <= c_end)) &&
-				  (!do_hmac || c0 + 64u <= A);
-		uint32_t w[16];
-		if (fast) {
-			uint32_t o[16];
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				o[jj] = d[jj] ^ ksw[jj];
-			if (store_ct) {
-#pragma unroll
-				for (int g = 0; g < 4; g++)
-					*(uint4 *)(pkt + c0 + 16u * g) =
-						make_uint4(o[4 * g], o[4 * g + 1],
-							   o[4 * g + 2], o[4 * g + 3]);
-			}
-			/* MAC input is always the ciphertext */
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				w[jj] = bswap32(PROT ? o[jj] : d[jj]);
-		}
-		else {
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				const uint32_t bpos = c0 + 4u * jj;
-				uint32_t o = d[jj];
-				if (do_cipher && bpos >= c_off && bpos < c_end) {
-					uint32_t nbytes = min(c_end - bpos, 4u);
-					uint32_t m = nbytes == 4 ? 0xffffffffu
-						   : ((1u << (8 * nbytes)) - 1u);
-					o = d[jj] ^ (ksw[jj] & m);
-					if (store_ct) {
-						if (nbytes == 4)
-							*(uint32_t *)(pkt + bpos) = o;
-						else
-							st_partial(pkt + bpos, o, nbytes);
-					}
-				}
-				w[jj] = msg_word(16u * k + jj,
-						 bswap32(PROT ? o : d[jj]), A, X);
-			}
-			if (k + 1 == nb) {
-				w[14] = (uint32_t)(bitlen >> 32);
-				w[15] = (uint32_t)bitlen;
-			}
-		}
-		if (do_hmac && k < nb)
-			sha1_compress(h, w);
-	}
-
-	uint8_t vd = 0;
-	if (do_hmac) {
-		/* outer hash: opad midstate + 20-byte inner digest */
-		uint32_t w[16];
-		w[0] = h[0]; w[1] = h[1]; w[2] = h[2]; w[3] = h[3]; w[4] = h[4];
-		w[5] = 0x80000000u;
-#pragma unroll
-		for (int q = 6; q < 15; q++)
-			w[q] = 0;
-		w[15] = (64u + 20u) * 8u;
-		h[0] = cp->opad[0]; h[1] = cp->opad[1]; h[2] = cp->opad[2];
-		h[3] = cp->opad[3]; h[4] = cp->opad[4];
-		sha1_compress(h, w);
-
-		const uint32_t tag_len = cp->tag_len;
-		uint8_t *tp = pkt + j.tag_off;
-		if (PROT) {
-			for (uint32_t q = 0; q < tag_len; q++)
-				tp[q] = (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
-		}
-		else {
-			uint32_t diff = 0;
-			for (uint32_t q = 0; q < tag_len; q++)
-				diff |= tp[q] ^ (uint8_t)(h[q >> 2] >>
-							  (24 - 8 * (q & 3)));
-			vd = diff == 0 ? SV_TAG_OK : 0;
-			if (j.flags & SJ_ROC_AT_TAG) {
-				/* the reference writes the ROC over the tag
-				 * before comparing (srtp.c:342-344); keep the
-				 * original bytes for a possible re-run */
-				if (save)
-					save[i] = (uint32_t)tp[0] |
-						  (uint32_t)tp[1] << 8 |
-						  (uint32_t)tp[2] << 16 |
-						  (uint32_t)tp[3] << 24;
-				st_be32(tp, j.trailer);
-			}
-		}
-	}
-	if (PROT && (j.flags & SJ_STORE_TRAIL))
-		st_be32(pkt + j.t_off, j.trailer);
-
-	if (store_ct && !PROT)
-		vd |= SV_CIPHERED;
-
-	/* unprotect with decrypt-if-authentic: the plaintext was written
-	 * speculatively during the single pass; a forged packet is restored
-	 * by re-applying the keystream (rare path) */
-	if (cipher_if_ok && !(vd & SV_TAG_OK)) {
-#pragma unroll
-		for (int q = 0; q < 4; q++)
-			carry[q] = 0;
-		for (uint32_t k = 0; k < nck; k++) {
-			const uint32_t c0 = 64u * k;
-			if (!(c0 + 64u > c_off && c0 < c_end))
-				continue;
-			uint32_t B[4][4];
-#pragma unroll
-			for (int m = 0; m < 4; m++)
-				ctr_block<NR>(smem, lo, rk, iv,
-					      (int32_t)(4 * k) - cw4 + m, B[m]);
-			uint32_t ksw[16];
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				if (SHIFT == 0)
-					ksw[jj] = B[jj >> 2][jj & 3];
-				else if (jj < SHIFT)
-					ksw[jj] = carry[jj + 4 - SHIFT];
-				else
-					ksw[jj] = B[(jj - SHIFT) >> 2][(jj - SHIFT) & 3];
-			}
-#pragma unroll
-			for (int q = 0; q < 4; q++)
-				carry[q] = B[3][q];
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				const uint32_t bpos = c0 + 4u * jj;
-				if (bpos >= c_off && bpos < c_end) {
-					uint32_t nbytes = min(c_end - bpos, 4u);
-					if (nbytes == 4) {
-						uint32_t *p = (uint32_t *)(pkt + bpos);
-						*p = *p ^ ksw[jj];
-					}
-					else {
-						uint32_t v = 0;
-						for (uint32_t q = 0; q < nbytes; q++)
-							v |= (uint32_t)pkt[bpos + q] << (8 * q);
-						st_partial(pkt + bpos, v ^ ksw[jj], nbytes);
-					}
-				}
-			}
-		}
-		vd &= (uint8_t)~SV_CIPHERED;
-	}
-	if (undo) {
-		/* compact undo: the word under the ROC back (srtp.c:342-344) */
-		uint8_t *tp = pkt + j.tag_off;
-		const uint32_t v = save[i];
-		tp[0] = (uint8_t)v; tp[1] = (uint8_t)(v >> 8);
-		tp[2] = (uint8_t)(v >> 16); tp[3] = (uint8_t)(v >> 24);
-		return;
-	}
-	if (COMPACT && !PROT && !(vd & SV_TAG_OK))
-		atomicAdd(a.c.nfail, 1u);
-	if (verdict)
-		verdict[i] = vd;
-}
-
-/* ------------------------------------------------------------------ */
-/* AES-GCM, one packet per lane.                                        */
-
-/* bytes [p, p+16) of the GCM AAD stream  AAD = pkt[0,A) ‖ trailer? ,
- * as 4 big-endian words, zero padded */
-__device__ __forceinline__ void aad_block(const uint8_t *pkt, uint64_t pasz,
-					  uint32_t p, uint32_t A, bool trail,
-					  uint32_t trailer, uint32_t w[4])
-{
-	uint4 v = make_uint4(0, 0, 0, 0);
-	if (p < A)
-		v = ld16(pkt, pasz, p);
-	uint32_t d[4] = {v.x, v.y, v.z, v.w};
-	const uint64_t X = trail ? ((uint64_t)trailer << 32) : 0ull;
-#pragma unroll
-	for (int q = 0; q < 4; q++)
-		w[q] = msg_word((p >> 2) + q, bswap32(d[q]), A, X);
-}
-
-template <int NR, bool PROT, bool COMPACT>
-__global__ void __launch_bounds__(KBLOCK)
-k_gcm(const KArgs a)
-{
-	uint8_t *const arena = a.arena;
-	const uint64_t asz = a.asz;
-	const struct sgpu_comp *__restrict__ comps = a.comps;
-	uint8_t *__restrict__ verdict = a.verdict;
-	const bool undo = COMPACT && a.c.undo;
-	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES + 4096 + 64];
-	uint8_t *htab_lds = smem + TT_BYTES;                  /* 16 waves x 256 */
-	uint32_t *rem4 = (uint32_t *)(smem + TT_BYTES + 4096);
-	tt_fill(smem, g_T0);
-	if (threadIdx.x < 16)
-		rem4[threadIdx.x] = c_rem4[threadIdx.x];
-	__syncthreads();
-
-	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-	const uint32_t lo = (threadIdx.x & 31u) * 4u;
-	struct sgpu_job j;
-	uint32_t i = 0;
-	const bool live = get_job<COMPACT, SGPU_MODE_GCM, PROT>(
-		a, blockIdx.x * blockDim.x + threadIdx.x, j, i);
-	if (!live)
-		j.flags = SJ_SKIP, j.comp = 0;
-	/* stage the GHASH table: per wave, in LDS if the wave's packets
-	 * share one context, else per-lane reads from global memory */
-	uint32_t c_first = __builtin_amdgcn_readfirstlane(j.comp);
-	const bool uniform = __all(j.comp == c_first || (j.flags & SJ_SKIP));
-	const uint8_t *tab;
-	if (uniform) {
-		uint8_t *wt = htab_lds + wv * 256u;
-		if (lane < 16)
-			*(uint4 *)(wt + lane * 16) =
-				*(const uint4 *)comps[c_first].htab[lane];
-		__builtin_amdgcn_wave_barrier();
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		tab = wt;
-	}
-	else {
-		tab = (const uint8_t *)comps[j.comp].htab;
-	}
-	if (!live)
-		return;
-	if (j.flags & SJ_SKIP) {
-		if (verdict && !undo)
-			verdict[i] = 0;
-		return;
-	}
-	const struct sgpu_comp *cp = comps + j.comp;
-	uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-	for (int k = 0; k < NR + 1; k++) {
-		uint4 v = *(const uint4 *)&cp->rk[4 * k];
-		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
-		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
-	}
-	uint8_t *pkt = arena + j.off;
-	const uint64_t pasz = asz - j.off;
-
-	/* srtp_iv_calc_gcm (misc.c:93-105); J0 = IV ‖ 0^31 ‖ 1 */
-	uint32_t iv[3];
-	{
-		uint4 ks = *(const uint4 *)cp->k_s;
-		uint32_t ixhi = j.ixhi, ixlo = j.ixlo;
-		/* BE16 words: w1=ssrc>>16 w2=ssrc w3=ix>>32 w4=ix>>16 w5=ix */
-		uint32_t be0 = (j.ssrc >> 16) & 0xffffu;            /* bytes 2,3 */
-		uint32_t be1 = ((j.ssrc & 0xffffu) << 16) | (ixhi >> 16);
-		uint32_t be2 = ((ixhi & 0xffffu) << 16) | (ixlo & 0xffffu);
-		iv[0] = ks.x ^ bswap32(be0);
-		iv[1] = ks.y ^ bswap32(be1);
-		iv[2] = ks.z ^ bswap32(be2);
-	}
-
-	const bool trail = (j.flags & SJ_TRAILER) != 0;
-	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
-	if (j.flags & SJ_UNDO) {
-		/* re-apply the GCM keystream (restores a speculatively
-		 * decrypted payload before a re-run) */
-		const uint32_t nb = (j.c_len + 15u) / 16u;
-		for (uint32_t b = 0; b < nb; b++) {
-			const uint32_t p = j.c_off + 16u * b;
-			uint32_t s0 = iv[0], s1 = iv[1], s2 = iv[2];
-			uint32_t s3 = bswap32(b + 2u);
-			aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
-			uint32_t ks[4] = {s0, s1, s2, s3};
-			const uint32_t rem = j.c_off + j.c_len - p;
-			for (int q = 0; q < 4; q++) {
-				uint32_t bp = 4u * q;
-				uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
-				if (nbytes == 4) {
-					uint32_t *w = (uint32_t *)(pkt + p + bp);
-					*w = *w ^ ks[q];
-				}
-				else if (nbytes) {
-					uint32_t v = 0;
-					for (uint32_t z = 0; z < nbytes; z++)
-						v |= (uint32_t)pkt[p + bp + z] << (8 * z);
-					st_partial(pkt + p + bp, v ^ ks[q], nbytes);
-				}
-			}
-		}
-		if (verdict && !undo)
-			verdict[i] = 0;
-		return;
-	}
-	const uint32_t A = j.a_len;
-	const uint32_t aad_total = A + (trail ? 4u : 0u);
-	const uint32_t c_off = j.c_off, c_len = do_cipher ? j.c_len : 0u;
-	const uint32_t c_end = c_off + c_len;
-
-	uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-	/* GHASH over AAD */
-	for (uint32_t p = 0; p < aad_total; p += 16) {
-		uint32_t w[4];
-		aad_block(pkt, pasz, p, A, trail, j.trailer, w);
-		/* msg_word adds the SHA 0x80 marker only when X has it; for
-		 * GCM X carries no marker, zero padding is implied */
-		x0 ^= w[0]; x1 ^= w[1]; x2 ^= w[2]; x3 ^= w[3];
-		ghash_mul(x0, x1, x2, x3, tab, rem4);
-	}
-	/* CTR + GHASH over the cipher region, in 16-B payload blocks */
-	const uint32_t nblk = (c_len + 15u) / 16u;
-	for (uint32_t b = 0; b < nblk; b++) {
-		const uint32_t p = c_off + 16u * b;
-		uint4 v = ld16(pkt, pasz, p);
-		uint32_t d[4] = {v.x, v.y, v.z, v.w};
-		uint32_t s0 = iv[0], s1 = iv[1], s2 = iv[2];
-		uint32_t s3 = bswap32(b + 2u);          /* inc32(J0) + b */
-		aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
-		uint32_t ks[4] = {s0, s1, s2, s3};
-		uint32_t o[4], ct[4];
-		const uint32_t rem = c_end - p;
-		if (rem >= 16) {
-#pragma unroll
-			for (int q = 0; q < 4; q++) {
-				o[q] = d[q] ^ ks[q];
-				ct[q] = PROT ? o[q] : d[q];
-			}
-			*(uint4 *)(pkt + p) = make_uint4(o[0], o[1], o[2], o[3]);
-		}
-		else {
-#pragma unroll
-			for (int q = 0; q < 4; q++) {
-				uint32_t bp = 4u * q;
-				uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
-				uint32_t m = nbytes >= 4 ? 0xffffffffu
-					   : ((1u << (8 * nbytes)) - 1u);
-				o[q] = (d[q] ^ ks[q]) & m;
-				ct[q] = PROT ? o[q] : (d[q] & m);
-				if (nbytes == 4)
-					*(uint32_t *)(pkt + p + bp) = o[q];
-				else if (nbytes)
-					st_partial(pkt + p + bp, o[q], nbytes);
-			}
-		}
-		x0 ^= bswap32(ct[0]); x1 ^= bswap32(ct[1]);
-		x2 ^= bswap32(ct[2]); x3 ^= bswap32(ct[3]);
-		ghash_mul(x0, x1, x2, x3, tab, rem4);
-	}
-	/* length block: bitlen(AAD) ‖ bitlen(C) */
-	{
-		uint64_t al = (uint64_t)aad_total * 8u, cl = (uint64_t)c_len * 8u;
-		x0 ^= (uint32_t)(al >> 32); x1 ^= (uint32_t)al;
-		x2 ^= (uint32_t)(cl >> 32); x3 ^= (uint32_t)cl;
-		ghash_mul(x0, x1, x2, x3, tab, rem4);
-	}
-	/* tag = GHASH ^ E(K, J0) */
-	uint32_t s0 = iv[0], s1 = iv[1], s2 = iv[2], s3 = bswap32(1u);
-	aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
-	uint32_t t[4] = {x0 ^ bswap32(s0), x1 ^ bswap32(s1), x2 ^ bswap32(s2),
-			 x3 ^ bswap32(s3)};
-	uint8_t *tp = pkt + j.tag_off;
-	uint8_t vd = do_cipher ? SV_CIPHERED : 0;
-	if (PROT) {
-#pragma unroll
-		for (int q = 0; q < 4; q++)
-			st_be32(tp + 4 * q, t[q]);
-		if (j.flags & SJ_STORE_TRAIL)
-			st_be32(pkt + j.t_off, j.trailer);
-	}
-	else {
-		uint32_t diff = 0;
-#pragma unroll
-		for (int q = 0; q < 16; q++)
-			diff |= tp[q] ^ (uint8_t)(t[q >> 2] >> (24 - 8 * (q & 3)));
-		if (diff == 0)
-			vd |= SV_TAG_OK;
-		if (COMPACT && !(vd & SV_TAG_OK))
-			atomicAdd(a.c.nfail, 1u);
-	}
-	if (verdict)
-		verdict[i] = vd;
-}
 
 /* ------------------------------------------------------------------ */
 /* Session setup: KDF + key schedule + HMAC midstates + GHASH table.   */
@@ -1159,6 +489,8 @@ static struct sgpu_keyreq *g_req_dev;
 static uint32_t *g_slot_dev;
 static uint32_t g_req_cap;
 
+static const uint32_t *g_T0_dev;
+
 static int herr(hipError_t e, const char *what)
 {
 	if (e == hipSuccess)
@@ -1213,6 +545,9 @@ extern "C" int sgpu_init(void)
 	int e = herr(hipMemcpyToSymbol(HIP_SYMBOL(g_sbox), sbox, 256), "sbox");
 	if (!e)
 		e = herr(hipMemcpyToSymbol(HIP_SYMBOL(g_T0), T0, 1024), "T0");
+	if (!e)
+		e = herr(hipGetSymbolAddress((void **)&g_T0_dev, HIP_SYMBOL(g_T0)),
+			 "T0 address");
 	if (e)
 		return e;
 	g_inited = 1;
@@ -1325,33 +660,8 @@ extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs)
 	pthread_mutex_unlock(&g_prof_lock);
 }
 
-typedef void (*kfn_t)(const KArgs);
-
-template <bool COMPACT>
-static kfn_t pick_ctr(int nr, int shift, int prot)
-{
-#define PICK(NR, S)                                                            \
-	if (nr == NR && shift == S)                                            \
-		return prot ? k_ctr_hmac<NR, S, true, COMPACT>                 \
-			    : k_ctr_hmac<NR, S, false, COMPACT>;
-	PICK(10, 0) PICK(10, 1) PICK(10, 2) PICK(10, 3)
-	PICK(14, 0) PICK(14, 1) PICK(14, 2) PICK(14, 3)
-#undef PICK
-	return NULL;
-}
-
-template <bool COMPACT>
-static kfn_t pick_gcm(int nr, int prot)
-{
-	if (nr == 10)
-		return prot ? k_gcm<10, true, COMPACT> : k_gcm<10, false, COMPACT>;
-	if (nr == 14)
-		return prot ? k_gcm<14, true, COMPACT> : k_gcm<14, false, COMPACT>;
-	return NULL;
-}
-
 static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
-		  hipStream_t stream)
+		  hipStream_t stream, uint32_t block = KBLOCK)
 {
 	struct prof_ev pe;
 	int prof = 0;
@@ -1361,7 +671,7 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		if (prof)
 			(void)hipEventRecord(pe.a, stream);
 	}
-	hipLaunchKernelGGL(f, dim3((n + KBLOCK - 1) / KBLOCK), dim3(KBLOCK), 0,
+	hipLaunchKernelGGL(f, dim3((n + block - 1) / block), dim3(block), 0,
 			   stream, a);
 	int e = herr(hipGetLastError(), "kernel launch");
 	if (prof) {
@@ -1402,8 +712,9 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 {
 	if (!njobs)
 		return 0;
-	kfn_t f = mode == SGPU_MODE_GCM ? pick_gcm<false>(nr, prot)
-					: pick_ctr<false>(nr, shift, prot);
+	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(false, nr, prot)
+		  : nr == 10 ? sgpu_pick_ctr10(false, false, shift, prot)
+			     : sgpu_pick_ctr14(false, false, shift, prot);
 	if (!f) {
 		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
 			 mode, nr);
@@ -1416,10 +727,12 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	a.jobs = jobs;
 	a.njobs = njobs;
 	a.comps = (const struct sgpu_comp *)g_table;
+	a.t0 = g_T0_dev;
 	a.verdict = verdict;
 	a.save = save;
 	return launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
-		      (hipStream_t)stream);
+		      (hipStream_t)stream,
+		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK);
 }
 
 extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
@@ -1428,8 +741,9 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 {
 	if (!c->n)
 		return 0;
-	kfn_t f = mode == SGPU_MODE_GCM ? pick_gcm<true>(nr, prot)
-					: pick_ctr<true>(nr, shift, prot);
+	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(true, nr, prot)
+		  : nr == 10 ? sgpu_pick_ctr10(true, c->uniform != 0, shift, prot)
+			     : sgpu_pick_ctr14(true, c->uniform != 0, shift, prot);
 	if (!f) {
 		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
 			 mode, nr);
@@ -1440,12 +754,14 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 	a.arena = arena;
 	a.asz = arena_size;
 	a.comps = (const struct sgpu_comp *)g_table;
+	a.t0 = g_T0_dev;
 	a.verdict = c->verdict;
 	a.save = c->save;
 	a.c = *c;
 	return launch(f, a, c->n,
 		      c->undo ? -1 : prof_slot(mode, nr, shift, prot),
-		      (hipStream_t)stream);
+		      (hipStream_t)stream,
+		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK);
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,

@@ -2067,7 +2067,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				struct sgpu_compact C = {
 					up_d, up_d + n, hd_d, desc_d, NULL,
 					(const uint32_t *)w->cm.d, NULL, 0,
-					(uint32_t)n, vd_d, save_d, nfail_d, 0};
+					(uint32_t)n, vd_d, save_d, nfail_d, 0, 1};
 				err = sgpu_run_compact(b->arena,
 						       b->arena_size, &C,
 						       c0->mode, (int)c0->nr,
@@ -2214,7 +2214,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				b->sess ? up_d + 2 * n : NULL,
 				(const uint32_t *)w->cm.d,
 				fl[q].has_idx ? idx_d : NULL, fl[q].base,
-				fl[q].n, vd_d, save_d, nfail_d, 0};
+				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[q].shift, prot, stream);
@@ -2244,7 +2244,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				b->sess ? up_d + 2 * n : NULL,
 				(const uint32_t *)w->cm.d,
 				fl[k].has_idx ? idx_d : NULL, fl[k].base,
-				fl[k].n, vd_d, save_d, nfail_d, 1};
+				fl[k].n, vd_d, save_d, nfail_d, 1, nsess == 1};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[k].shift, prot, stream);

@@ -151,6 +151,7 @@ struct sgpu_compact {
 	uint32_t *save;                 /* [packet] tag word under the ROC */
 	uint32_t *nfail;                /* +1 per speculation miss (device) */
 	int undo;                       /* restore the pre-call bytes */
+	int uniform;                    /* every packet: one session context */
 };
 
 /* launch the compact kernel of class (mode, nr, shift, prot) */

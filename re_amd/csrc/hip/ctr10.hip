@@ -17,3 +17,8 @@ kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot)
 #undef PICK
 	return NULL;
 }
+
+unsigned sgpu_ctr_block(bool uni, int prot)
+{
+	return ctr_block(prot != 0, uni);
+}

@@ -7,6 +7,23 @@
 #include "kern_common.h"
 
 /*
+ * Occupancy.  The 64 KiB T-table image allows one LDS image per block and
+ * two blocks per CU.  Single-key protect fits 128 VGPRs: 512-thread
+ * blocks, 2 per CU = 4 waves/SIMD.  Single-key unprotect keeps ciphertext
+ * and MAC schedule live together (~150 VGPRs): one 768-thread block per
+ * CU = 3 waves/SIMD.  Per-lane keys: 512-thread blocks, 2 waves/SIMD.
+ */
+__host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
+{
+	return !uni ? 1 : (prot ? 4 : 3);
+}
+
+__host__ __device__ constexpr unsigned ctr_block(bool prot, bool uni)
+{
+	return (uni && !prot) ? 768u : 512u;
+}
+
+/*
  * Fused AES-CM + HMAC-SHA1, one packet per lane.
  *   SHIFT = (c_off / 4) & 3: the cipher region starts SHIFT words into a
  *   16-byte packet granule (3 for a 12-byte RTP header, 2 for SRTCP).
@@ -17,8 +34,9 @@
  * general byte-exact path.
  */
 template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>
-__global__ void __launch_bounds__(CTR_BLOCK)
-__attribute__((amdgpu_waves_per_eu(UNI ? 4 : 1, 8)))
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, ctr_block(PROT, UNI))))
+__attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
 k_ctr_hmac(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
@@ -188,22 +206,28 @@ k_ctr_hmac(const KArgs a)
 			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
 		}
 		if (!PROT) {
+			/* keystream first (hides the chunk load), then the MAC
+			 * over the received ciphertext, then decrypt */
+			uint32_t ks[16];
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				ks[jj] = 0;
+			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+						 (int32_t)(4 * k) - cw4, carry, ks,
+						 NULL);
 #pragma unroll
 			for (int jj = 0; jj < 16; jj++)
 				w[jj] = bswap32(d[jj]);
 			sha1_compress(h, w);
-			/* reload the chunk (L1/L2 hit) rather than keep 16
-			 * VGPRs live across the compression */
-			asm volatile("" ::: "memory");
 #pragma unroll
-			for (int g = 0; g < 4; g++) {
-				const uint4 v = *(const uint4 *)(pkt + c0 + 16u * g);
-				d[4 * g] = v.x; d[4 * g + 1] = v.y;
-				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
-			}
+			for (int jj = 0; jj < 16; jj++)
+				d[jj] ^= ks[jj];
 		}
-		ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
-					 (int32_t)(4 * k) - cw4, carry, d, NULL);
+		else {
+			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+						 (int32_t)(4 * k) - cw4, carry, d,
+						 NULL);
+		}
 		if (store_ct) {
 #pragma unroll
 			for (int g = 0; g < 4; g++)

@@ -14,6 +14,7 @@
 
 #define KBLOCK 256
 #define CTR_BLOCK 512      /* 8 waves share one 64 KiB T-table image */
+#define CTR_BLOCK_MAX 768  /* single-key unprotect: 12 waves, 1 block/CU */
 
 /* ------------------------------------------------------------------ */
 /* memory helpers: packet starts are 4-byte aligned (host-checked)     */
@@ -228,6 +229,7 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 typedef void (*kfn_t)(const KArgs);
 
 /* kernel pickers, one per translation unit */
+unsigned sgpu_ctr_block(bool uni, int prot);
 kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_gcm(bool compact, int nr, int prot);

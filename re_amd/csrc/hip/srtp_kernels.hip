@@ -761,7 +761,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 	return launch(f, a, c->n,
 		      c->undo ? -1 : prof_slot(mode, nr, shift, prot),
 		      (hipStream_t)stream,
-		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK);
+		      mode == SGPU_MODE_GCM ? KBLOCK
+					    : sgpu_ctr_block(c->uniform != 0, prot));
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,

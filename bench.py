@@ -166,17 +166,21 @@ def main():
                                              W.SSRC_BASE, True)) == 0
         return tx, rx
 
+    # per-call descriptor arrays (the API updates pos/end in place)
+    p, e = np.empty_like(pos), np.empty_like(end)
+    err_e = np.zeros(n, dtype=np.int32)
+    err_d = np.zeros(n, dtype=np.int32)
+
     def step(tx, rx):
-        p, e = pos.copy(), end.copy()
-        rc, err = P.device_batch("srtp_encrypt", tx, arena.data_ptr(),
-                                 arena.numel(), p, e, cap, sess, sptr)
+        np.copyto(p, pos)
+        np.copyto(e, end)
+        rc, _ = P.device_batch("srtp_encrypt", tx, arena.data_ptr(),
+                               arena.numel(), p, e, cap, sess, sptr, err_e)
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
-        bad = int((err != 0).sum())
-        rc, err = P.device_batch("srtp_decrypt", rx, arena.data_ptr(),
-                                 arena.numel(), p, e, cap, sess, sptr)
+        rc, _ = P.device_batch("srtp_decrypt", rx, arena.data_ptr(),
+                               arena.numel(), p, e, cap, sess, sptr, err_d)
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
-        bad += int((err != 0).sum())
-        return bad
+        return np.count_nonzero(err_e) + np.count_nonzero(err_d)
 
     # ---- warmup (untimed) ----
     for _ in range(args.warmup):

@@ -73,6 +73,80 @@ __device__ __forceinline__ void tt_fill(uint8_t *smem, const uint32_t *T0g)
 	}
 }
 
+/* one middle round r (1 <= r < NR) on (s0..s3); k = rk + 4r (rot16'd) */
+__device__ __forceinline__ void aes_round(const uint8_t *smem, uint32_t lo,
+					  const uint32_t *k, uint32_t &s0,
+					  uint32_t &s1, uint32_t &s2,
+					  uint32_t &s3)
+{
+	uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
+	uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo) + 128);
+	uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
+	uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
+	uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
+	uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo) + 128);
+	uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
+	uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
+	uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
+	uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo) + 128);
+	uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
+	uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
+	uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
+	uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo) + 128);
+	uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
+	uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
+	s0 = xor3(a0, b1, rot16(xor3(c2, d3, k[0])));
+	s1 = xor3(a1, b2, rot16(xor3(c3, d0, k[1])));
+	s2 = xor3(a2, b3, rot16(xor3(c0, d1, k[2])));
+	s3 = xor3(a3, b0, rot16(xor3(c1, d2, k[3])));
+}
+
+/* final round (SubBytes, ShiftRows, AddRoundKey; k plain) */
+__device__ __forceinline__ void aes_final(const uint8_t *smem, uint32_t lo,
+					  const uint32_t *k, uint32_t &s0,
+					  uint32_t &s1, uint32_t &s2,
+					  uint32_t &s3)
+{
+	/* S[x] = byte1 of T0[x] = byte2 of T0[x] = byte3 of T1[x] */
+	uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
+	uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo));
+	uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
+	uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
+	uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
+	uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo));
+	uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
+	uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
+	uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
+	uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo));
+	uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
+	uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
+	uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
+	uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo));
+	uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
+	uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
+	s0 = xor3(__builtin_amdgcn_perm(a0, b1, 0x0C0C0105u),
+		  __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu), k[0]);
+	s1 = xor3(__builtin_amdgcn_perm(a1, b2, 0x0C0C0105u),
+		  __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu), k[1]);
+	s2 = xor3(__builtin_amdgcn_perm(a2, b3, 0x0C0C0105u),
+		  __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu), k[2]);
+	s3 = xor3(__builtin_amdgcn_perm(a3, b0, 0x0C0C0105u),
+		  __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu), k[3]);
+}
+
+/* rounds FIRST .. NR on a state that has been through rounds 0..FIRST-1 */
+template <int NR, int FIRST>
+__device__ __forceinline__ void aes_rounds(const uint8_t *smem, uint32_t lo,
+					   const uint32_t *rk, uint32_t &s0,
+					   uint32_t &s1, uint32_t &s2,
+					   uint32_t &s3)
+{
+#pragma unroll
+	for (int r = FIRST; r < NR; r++)
+		aes_round(smem, lo, rk + 4 * r, s0, s1, s2, s3);
+	aes_final(smem, lo, rk + 4 * NR, s0, s1, s2, s3);
+}
+
 /*
  * One AES block encryption.  rk: 4*(NR+1) words; words 4..4*NR-1 (rounds
  * 1..NR-1) are rot16'd, round 0 and NR are plain.
@@ -84,58 +158,7 @@ __device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
 					  uint32_t &s3)
 {
 	s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
-#pragma unroll
-	for (int r = 1; r < NR; r++) {
-		const uint32_t *k = rk + 4 * r;
-		uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
-		uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo) + 128);
-		uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
-		uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
-		uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
-		uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo) + 128);
-		uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
-		uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
-		uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
-		uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo) + 128);
-		uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
-		uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
-		uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
-		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo) + 128);
-		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
-		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
-		s0 = xor3(a0, b1, rot16(xor3(c2, d3, k[0])));
-		s1 = xor3(a1, b2, rot16(xor3(c3, d0, k[1])));
-		s2 = xor3(a2, b3, rot16(xor3(c0, d1, k[2])));
-		s3 = xor3(a3, b0, rot16(xor3(c1, d2, k[3])));
-	}
-	{
-		const uint32_t *k = rk + 4 * NR;
-		/* S[x] = byte1 of T0[x] = byte2 of T0[x] = byte3 of T1[x] */
-		uint32_t a0 = lds_u32(smem, TT_ADDR(s0, 0, lo));
-		uint32_t b1 = lds_u32(smem, TT_ADDR(s1, 1, lo));
-		uint32_t c2 = lds_u32(smem, TT_ADDR(s2, 2, lo));
-		uint32_t d3 = lds_u32(smem, TT_ADDR(s3, 3, lo) + 128);
-		uint32_t a1 = lds_u32(smem, TT_ADDR(s1, 0, lo));
-		uint32_t b2 = lds_u32(smem, TT_ADDR(s2, 1, lo));
-		uint32_t c3 = lds_u32(smem, TT_ADDR(s3, 2, lo));
-		uint32_t d0 = lds_u32(smem, TT_ADDR(s0, 3, lo) + 128);
-		uint32_t a2 = lds_u32(smem, TT_ADDR(s2, 0, lo));
-		uint32_t b3 = lds_u32(smem, TT_ADDR(s3, 1, lo));
-		uint32_t c0 = lds_u32(smem, TT_ADDR(s0, 2, lo));
-		uint32_t d1 = lds_u32(smem, TT_ADDR(s1, 3, lo) + 128);
-		uint32_t a3 = lds_u32(smem, TT_ADDR(s3, 0, lo));
-		uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo));
-		uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
-		uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
-		s0 = xor3(__builtin_amdgcn_perm(a0, b1, 0x0C0C0105u),
-			  __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu), k[0]);
-		s1 = xor3(__builtin_amdgcn_perm(a1, b2, 0x0C0C0105u),
-			  __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu), k[1]);
-		s2 = xor3(__builtin_amdgcn_perm(a2, b3, 0x0C0C0105u),
-			  __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu), k[2]);
-		s3 = xor3(__builtin_amdgcn_perm(a3, b0, 0x0C0C0105u),
-			  __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu), k[3]);
-	}
+	aes_rounds<NR, 1>(smem, lo, rk, s0, s1, s2, s3);
 }
 
 /* ---- SHA-1 compression, W[] holds the 16 big-endian message words ---- */

@@ -96,6 +96,10 @@ k_ctr_hmac(const KArgs a)
 		iv[3] = (ks.w ^ (bswap32(j.ixlo) >> 16)) & 0xffffu;
 	}
 
+	/* compact launches never carry packets of 1 MiB or more (host) */
+	CtrKs<NR, COMPACT> C;
+	C.init(smem, lo, rk, iv);
+
 	uint32_t h[5];
 	if (do_hmac) {
 		h[0] = cp->ipad[0]; h[1] = cp->ipad[1]; h[2] = cp->ipad[2];
@@ -159,7 +163,7 @@ k_ctr_hmac(const KArgs a)
 				mask[jj] = nbytes >= 4 ? 0xffffffffu :
 					   ((1u << (8 * nbytes)) - 1u);
 			}
-			ks_xor<NR, SHIFT, true>(smem, lo, rk, iv,
+			ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
 						(int32_t)(4 * k) - cw4, carry, d,
 						mask);
 			if (store_ct) {
@@ -212,7 +216,7 @@ k_ctr_hmac(const KArgs a)
 #pragma unroll
 			for (int jj = 0; jj < 16; jj++)
 				ks[jj] = 0;
-			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
 						 (int32_t)(4 * k) - cw4, carry, ks,
 						 NULL);
 #pragma unroll
@@ -224,7 +228,7 @@ k_ctr_hmac(const KArgs a)
 				d[jj] ^= ks[jj];
 		}
 		else {
-			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
 						 (int32_t)(4 * k) - cw4, carry, d,
 						 NULL);
 		}
@@ -307,7 +311,7 @@ k_ctr_hmac(const KArgs a)
 				ksw[jj] = 0;
 				mask[jj] = 0xffffffffu;
 			}
-			ks_xor<NR, SHIFT, false>(smem, lo, rk, iv,
+			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
 						 (int32_t)(4 * kk) - cw4, carry,
 						 ksw, mask);
 #pragma unroll

@@ -70,6 +70,95 @@ __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
 	ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
 }
 
+/*
+ * AES-CTR keystream of one packet with counter-mode caching.  SRTP IVs
+ * have bytes 14..15 zero (srtp_iv_calc, misc.c:76-87; the GCM/KDF paths do
+ * not use this), so while the block index b < 65536 (payload < 1 MiB) only
+ * bytes 14..15 of the counter block change: after round 0 only t3's bytes
+ * 2..3 vary, round 1 has two varying lookups (columns 2..3 are constant)
+ * and round 2 has eight.  Those constants are computed once per packet.
+ * CACHED = false is the plain counter (any packet size).
+ */
+template <int NR, bool CACHED>
+struct CtrKs {
+	uint32_t t0, t1, t2, t3c;       /* IV ^ rk[0..3] (t3c: bytes 14,15 = rk) */
+	uint32_t A0, P0, A1, P1;        /* round 1: s0 = A0^rot16(P0^T1[t3.b3]) */
+	uint32_t R0, C1a, C1b, C2, C3a, C3b; /* round 2 constants */
+
+	__device__ __forceinline__ void init(const uint8_t *smem, uint32_t lo,
+					     const uint32_t *rk,
+					     const uint32_t iv[4])
+	{
+		t0 = iv[0] ^ rk[0];
+		t1 = iv[1] ^ rk[1];
+		t2 = iv[2] ^ rk[2];
+		t3c = iv[3] ^ rk[3];
+		if (!CACHED)
+			return;
+		const uint32_t *k1 = rk + 4, *k2 = rk + 8;
+		A0 = lds_u32(smem, TT_ADDR(t0, 0, lo)) ^
+		     lds_u32(smem, TT_ADDR(t1, 1, lo) + 128);
+		P0 = lds_u32(smem, TT_ADDR(t2, 2, lo)) ^ k1[0];
+		A1 = lds_u32(smem, TT_ADDR(t1, 0, lo)) ^
+		     lds_u32(smem, TT_ADDR(t2, 1, lo) + 128);
+		P1 = lds_u32(smem, TT_ADDR(t0, 3, lo) + 128) ^ k1[1];
+		/* round-1 columns 2 and 3 read t3 bytes 0..1 only: constant */
+		const uint32_t S2 = xor3(lds_u32(smem, TT_ADDR(t2, 0, lo)),
+					 lds_u32(smem, TT_ADDR(t3c, 1, lo) + 128),
+					 rot16(xor3(lds_u32(smem, TT_ADDR(t0, 2, lo)),
+						    lds_u32(smem, TT_ADDR(t1, 3, lo) + 128),
+						    k1[2])));
+		const uint32_t S3 = xor3(lds_u32(smem, TT_ADDR(t3c, 0, lo)),
+					 lds_u32(smem, TT_ADDR(t0, 1, lo) + 128),
+					 rot16(xor3(lds_u32(smem, TT_ADDR(t1, 2, lo)),
+						    lds_u32(smem, TT_ADDR(t2, 3, lo) + 128),
+						    k1[3])));
+		R0 = rot16(xor3(lds_u32(smem, TT_ADDR(S2, 2, lo)),
+				lds_u32(smem, TT_ADDR(S3, 3, lo) + 128), k2[0]));
+		C1a = lds_u32(smem, TT_ADDR(S2, 1, lo) + 128);
+		C1b = lds_u32(smem, TT_ADDR(S3, 2, lo)) ^ k2[1];
+		C2 = lds_u32(smem, TT_ADDR(S2, 0, lo)) ^
+		     lds_u32(smem, TT_ADDR(S3, 1, lo) + 128);
+		C3a = lds_u32(smem, TT_ADDR(S3, 0, lo));
+		C3b = lds_u32(smem, TT_ADDR(S2, 3, lo) + 128) ^ k2[3];
+	}
+
+	/* keystream block b.  CACHED: exact for 0 <= b < 65536 (the host
+	 * sends packets of 1 MiB or more to the plain general kernels);
+	 * b < 0 only ever lands in masked words. */
+	__device__ __forceinline__ void block(const uint8_t *smem, uint32_t lo,
+					      const uint32_t *rk, int32_t b,
+					      uint32_t ks[4]) const
+	{
+		if (!CACHED) {
+			const uint32_t iv[4] = {t0 ^ rk[0], t1 ^ rk[1],
+						t2 ^ rk[2], t3c ^ rk[3]};
+			ctr_block<NR>(smem, lo, rk, iv, b, ks);
+			return;
+		}
+		const uint32_t t3 = t3c ^ bswap32((uint32_t)b);
+		/* round 1: two varying lookups */
+		const uint32_t s0 = A0 ^ rot16(P0 ^ lds_u32(smem,
+					TT_ADDR(t3, 3, lo) + 128));
+		const uint32_t s1 = A1 ^ rot16(P1 ^ lds_u32(smem,
+					TT_ADDR(t3, 2, lo)));
+		/* round 2: eight varying lookups */
+		const uint32_t *k2 = rk + 8;
+		uint32_t r0 = xor3(lds_u32(smem, TT_ADDR(s0, 0, lo)),
+				   lds_u32(smem, TT_ADDR(s1, 1, lo) + 128), R0);
+		uint32_t r1 = xor3(lds_u32(smem, TT_ADDR(s1, 0, lo)), C1a,
+				   rot16(C1b ^ lds_u32(smem,
+					TT_ADDR(s0, 3, lo) + 128)));
+		uint32_t r2 = C2 ^ rot16(xor3(lds_u32(smem, TT_ADDR(s0, 2, lo)),
+					      lds_u32(smem, TT_ADDR(s1, 3, lo) + 128),
+					      k2[2]));
+		uint32_t r3 = xor3(C3a, lds_u32(smem, TT_ADDR(s0, 1, lo) + 128),
+				   rot16(lds_u32(smem, TT_ADDR(s1, 2, lo)) ^ C3b));
+		aes_rounds<NR, 3>(smem, lo, rk, r0, r1, r2, r3);
+		ks[0] = r0; ks[1] = r1; ks[2] = r2; ks[3] = r3;
+	}
+};
+
 /* the SHA-1 input word at global word index gw of the HMAC message
  * M = data[0,A) ‖ (trailer?) ‖ 0x80 ‖ 0* ‖ len64 -- for non-fast chunks */
 __device__ __forceinline__ uint32_t msg_word(uint32_t gw, uint32_t data_be,
@@ -195,9 +284,10 @@ __device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
  * take the tail of the previous chunk's last block (carry).  mask[]: per
  * word byte mask of the cipher region (all ones in the steady state).
  */
-template <int NR, int SHIFT, bool MASKED>
+template <int NR, int SHIFT, bool MASKED, bool CACHED>
 __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
-				       const uint32_t *rk, const uint32_t iv[4],
+				       const uint32_t *rk,
+				       const CtrKs<NR, CACHED> &C,
 				       int32_t blk0, uint32_t carry[4],
 				       uint32_t d[16], const uint32_t *mask)
 {
@@ -208,7 +298,7 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 #pragma unroll
 	for (int m = 0; m < 4; m++) {
 		uint32_t B[4];
-		ctr_block<NR>(smem, lo, rk, iv, blk0 + m, B);
+		C.block(smem, lo, rk, blk0 + m, B);
 #pragma unroll
 		for (int q = 0; q < 4; q++) {
 			const int jj = SHIFT + 4 * m + q;
@@ -224,7 +314,6 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 		}
 	}
 }
-
 
 typedef void (*kfn_t)(const KArgs);
 

@@ -2270,11 +2270,13 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	return err;
 }
 
+#define FAST_MAX_PKT ((1u << 20) - 64u)
+
 static int run_batch(int op, struct srtp **sessv, size_t nsess,
 		     struct srtp_batch *b)
 {
 	size_t i;
-	int r;
+	int r, big = 0;
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && sessv && nsess && b &&
 	    b->arena && b->pos && b->end && b->cap && b->err &&
 	    b->n <= UINT32_MAX / 4 && b->arena_size <= UINT32_MAX &&
@@ -2286,12 +2288,17 @@ static int run_batch(int op, struct srtp **sessv, size_t nsess,
 			for (i = 0; i < b->n; i++)
 				if (b->sess[i] >= nsess)
 					return EINVAL;
-		for (i = 0; i < b->n; i++)
+		for (i = 0; i < b->n; i++) {
 			if ((b->pos[i] & 3) || b->end[i] > b->cap[i] ||
 			    b->cap[i] > b->arena_size ||
 			    b->pos[i] > b->end[i])
 				return EINVAL;
-		r = run_fast(op, sessv, nsess, b);
+			/* the compact kernels cache the CTR counter block
+			 * for payloads under 1 MiB (kern_common.h CtrKs) */
+			if (b->end[i] - b->pos[i] >= FAST_MAX_PKT)
+				big = 1;
+		}
+		r = big ? -1 : run_fast(op, sessv, nsess, b);
 		if (r >= 0)
 			return r;
 	}

@@ -235,14 +235,17 @@ def batch_run(ctx, opname, mbufs):
 
 
 def device_batch(opname, sessions, arena_ptr, arena_size, pos, end, cap,
-                 sess_idx=None, stream=None):
+                 sess_idx=None, stream=None, err=None):
     """srtp_*_batch on a device arena.  pos/end/cap: numpy uint32 arrays
-    (pos/end updated in place); returns (rc, err numpy int32)."""
+    (pos/end updated in place); err: optional int32 output array.
+    Returns (rc, err numpy int32)."""
     import numpy as np
     n = len(pos)
     assert pos.dtype == np.uint32 and end.dtype == np.uint32
     cap = np.ascontiguousarray(cap, dtype=np.uint32)
-    err = np.zeros(n, dtype=np.int32)
+    if err is None:
+        err = np.zeros(n, dtype=np.int32)
+    assert err.dtype == np.int32 and len(err) == n
     b = SrtpBatch()
     b.arena = arena_ptr
     b.arena_size = arena_size

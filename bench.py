@@ -115,6 +115,9 @@ def main():
                     help="override packets per GPU (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--host-arrays", action="store_true",
+                    help="srtp_*_batch with host pos/end/err arrays instead "
+                         "of the device-resident srtp_*_batch_dev")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary to attach (profiles/*.json)")
     args = ap.parse_args()
@@ -166,12 +169,36 @@ def main():
                                              W.SSRC_BASE, True)) == 0
         return tx, rx
 
-    # per-call descriptor arrays (the API updates pos/end in place)
-    p, e = np.empty_like(pos), np.empty_like(end)
-    err_e = np.zeros(n, dtype=np.int32)
-    err_d = np.zeros(n, dtype=np.int32)
+    # per-call descriptor arrays (the API updates pos/end in place).
+    # Default: srtp_*_batch_dev -- windows and results resident in HBM like
+    # the packets; --host-arrays: srtp_*_batch with host windows.
+    use_dev = (not args.host_arrays) and nsess == 1
+    if use_dev:
+        i32 = lambda a: torch.from_numpy(
+            np.asarray(a, dtype=np.uint32).view(np.int32)).to(dev)
+        pos_d, end_d, cap_d = i32(pos), i32(end), i32(cap)
+        p_d, e_d = torch.empty_like(pos_d), torch.empty_like(end_d)
+        err_ed = torch.zeros(n, dtype=torch.int32, device=dev)
+        err_dd = torch.zeros(n, dtype=torch.int32, device=dev)
+        nbad = torch.zeros((), dtype=torch.int64, device=dev)
+    else:
+        p, e = np.empty_like(pos), np.empty_like(end)
+        err_e = np.zeros(n, dtype=np.int32)
+        err_d = np.zeros(n, dtype=np.int32)
 
     def step(tx, rx):
+        if use_dev:
+            p_d.copy_(pos_d)
+            e_d.copy_(end_d)
+            for opname, ss, er in (("srtp_encrypt", tx, err_ed),
+                                   ("srtp_decrypt", rx, err_dd)):
+                rc = P.device_batch_dev(opname, ss, arena.data_ptr(),
+                                        arena.numel(), p_d.data_ptr(),
+                                        e_d.data_ptr(), cap_d.data_ptr(),
+                                        er.data_ptr(), n, None, sptr)
+                assert rc == 0, (rc, P.lib().srtp_gpu_error())
+                nbad.add_(torch.count_nonzero(er))
+            return 0
         np.copyto(p, pos)
         np.copyto(e, end)
         rc, _ = P.device_batch("srtp_encrypt", tx, arena.data_ptr(),
@@ -206,6 +233,8 @@ def main():
     prof = P.prof_read()
     P.prof_enable(False)
     elapsed = t1 - t0
+    if use_dev:
+        errors += int(nbad.item())
     counters = torch.tensor([n * args.steps, rtp_bytes * args.steps, errors],
                             dtype=torch.float64, device=dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -282,7 +311,8 @@ def main():
         "config": {"workload": "config%d: %s" % (cfg_id, cfg["name"]),
                    "packets_per_gpu": n, "pkt_len": cfg["length"] or
                    "200/1400", "suite": P.suite_name(suite),
-                   "sessions": nsess, "parallelism": "shard%d" % world},
+                   "sessions": nsess, "parallelism": "shard%d" % world,
+                   "api": "srtp_*_batch_dev" if use_dev else "srtp_*_batch"},
         "hbm_frac_e2e": round(tot_pkts / world * (4 * L + 2 * tag) /
                               (T / 1) / 1e9 / HBM_PEAK_GBS, 4),
         "errors": int(tot_err),

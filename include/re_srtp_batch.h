@@ -64,6 +64,35 @@ int srtcp_decrypt_batch(struct srtp **sessv, size_t nsess,
 			struct srtp_batch *b);
 
 /**
+ * Fully device-resident batch: like struct srtp_batch, but the per-packet
+ * windows and results (pos, end, cap, err, sess) are device arrays too, so
+ * a GPU-resident pipeline never moves per-packet data through the host.
+ * Same per-packet semantics.  Single-stream RTP batches are planned on the
+ * device (O(1) host work); other batches are staged through the host
+ * engine transparently.
+ */
+struct srtp_batch_dev {
+	uint8_t *arena;
+	size_t arena_size;
+	uint32_t *pos;          /* device, in/out */
+	uint32_t *end;          /* device, in/out */
+	const uint32_t *cap;    /* device */
+	int32_t *err;           /* device, out */
+	const uint32_t *sess;   /* device or NULL */
+	size_t n;
+	void *stream;
+};
+
+int srtp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			   struct srtp_batch_dev *b);
+int srtp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			   struct srtp_batch_dev *b);
+int srtcp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			    struct srtp_batch_dev *b);
+int srtcp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			    struct srtp_batch_dev *b);
+
+/**
  * Stream state export/import (checkpoint/resume and multi-GPU hand-off:
  * lets a second context continue an SSRC exactly where another left it).
  * Layout follows struct srtp_stream (src/srtp/srtp.h:29-38).

@@ -42,6 +42,8 @@ k_gcm(const KArgs a)
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES + 4096 + 64];
 	uint8_t *htab_lds = smem + TT_BYTES;                  /* 16 waves x 256 */
 	uint32_t *rem4 = (uint32_t *)(smem + TT_BYTES + 4096);
+	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
+		return;
 	tt_fill(smem, a.t0);
 	if (threadIdx.x < 16)
 		rem4[threadIdx.x] = c_rem4[threadIdx.x];

@@ -40,6 +40,8 @@ __attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
 k_ctr_hmac(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
+	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
+		return;
 	tt_fill(smem, a.t0);
 	__syncthreads();
 

@@ -211,6 +211,8 @@ __device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
 	const struct sgpu_compact &c = a.c;
 	if (t >= c.n)
 		return false;
+	if (c.guard && *c.guard)        /* the device plan was rejected */
+		return false;
 	const uint32_t p = c.idx ? c.idx[c.base + t] : c.base + t;
 	slot = p;
 	const uint64_t d = c.desc[p];

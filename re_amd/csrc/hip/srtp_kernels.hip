@@ -235,7 +235,7 @@ __global__ void k_setup(const struct sgpu_keyreq *__restrict__ req,
 /* rtp_hdr_decode (src/rtp/rtp.c:88-137), including the position at
  * which each EBADMSG is raised.  get_rtcp_ssrc (srtcp.c:19-28).        */
 
-__global__ void k_parse(const uint8_t *__restrict__ arena,
+__global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 			const uint32_t *__restrict__ pos,
 			const uint32_t *__restrict__ end,
 			struct sgpu_hdr *__restrict__ out,
@@ -245,7 +245,8 @@ __global__ void k_parse(const uint8_t *__restrict__ arena,
 	if (i >= n)
 		return;
 	const uint32_t p = pos[i], e = end[i];
-	const uint32_t left = e > p ? e - p : 0;
+	/* a window outside the arena is never read (the planner rejects it) */
+	const uint32_t left = (e > p && e <= asz) ? e - p : 0;
 	const uint8_t *b = arena + p;
 	struct sgpu_hdr h;
 	h.ssrc = 0; h.seq = 0; h.err_pos = 0; h.hdr_len = 0xffffffffu;
@@ -346,8 +347,8 @@ __device__ __forceinline__ bool plan_wrap(uint32_t seq, uint32_t sb)
 
 __global__ void __launch_bounds__(PLAN_BLOCK)
 k_plan_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
-	     const uint32_t *pos, const uint32_t *end, uint32_t *bcnt,
-	     struct sgpu_plan_out *out)
+	     const uint32_t *pos, const uint32_t *end, const uint32_t *cap,
+	     uint64_t asz, uint32_t *bcnt, struct sgpu_plan_out *out)
 {
 	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
 	bool wrap = false;
@@ -368,6 +369,14 @@ k_plan_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 			f |= SPF_PARSE;
 		if (!in.prot && (int)seq - (int)sb > 32768)
 			f |= SPF_TIMEOUT;
+		if (end[i] - pos[i] >= (1u << 20) - 64u)
+			f |= SPF_SIZE;
+		if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
+		    (cap && (end[i] > cap[i] || cap[i] > asz)))
+			f |= SPF_BAD;
+		if (in.prot && cap &&
+		    (uint64_t)end[i] + in.need > (uint64_t)cap[i])
+			f |= SPF_CAP;
 		wrap = plan_wrap(seq, sb);
 		/* the next packet sees s_l = seq only if this one left it so */
 		if (i + 1 < in.n && !wrap && seq < sb)
@@ -765,16 +774,16 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 					    : sgpu_ctr_block(c->uniform != 0, prot));
 }
 
-extern "C" int sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,
-				  const uint32_t *end, struct sgpu_hdr *out,
-				  uint32_t *eix, uint32_t n, int rtcp,
-				  void *stream)
+extern "C" int sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,
+				  const uint32_t *pos, const uint32_t *end,
+				  struct sgpu_hdr *out, uint32_t *eix, uint32_t n,
+				  int rtcp, void *stream)
 {
 	if (!n)
 		return 0;
 	hipLaunchKernelGGL(k_parse, dim3((n + 255) / 256), dim3(256), 0,
-			   (hipStream_t)stream, arena, pos, end, out, eix, n,
-			   rtcp);
+			   (hipStream_t)stream, arena, arena_size, pos, end, out,
+			   eix, n, rtcp);
 	return herr(hipGetLastError(), "k_parse launch");
 }
 
@@ -914,9 +923,18 @@ extern "C" int sgpu_stream_wait(void *stream, void *ev)
 		    "stream wait");
 }
 
+/* per-class launch guards, once every planning block has finished */
+__global__ void k_plan_final(struct sgpu_plan_out *out)
+{
+	if (threadIdx.x < 4)
+		out->skip[threadIdx.x] =
+			out->fail || (((out->hl0 >> 2) & 3u) != threadIdx.x);
+}
+
 extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
 			     const struct sgpu_hdr *hdr, const uint32_t *pos,
-			     const uint32_t *end, uint64_t *desc,
+			     const uint32_t *end, const uint32_t *cap,
+			     uint64_t arena_size, uint64_t *desc,
 			     uint32_t *scratch, struct sgpu_plan_out *out,
 			     void *stream)
 {
@@ -928,10 +946,43 @@ extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
 	if (e)
 		return e;
 	hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(PLAN_BLOCK), 0, st,
-			   *in, hdr, pos, end, scratch, out);
+			   *in, hdr, pos, end, cap, arena_size, scratch, out);
 	hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, scratch,
 			   nb, out);
 	hipLaunchKernelGGL(k_plan_desc, dim3(nb), dim3(PLAN_BLOCK), 0, st,
 			   *in, hdr, (const uint32_t *)scratch, desc, out);
+	hipLaunchKernelGGL(k_plan_final, dim3(1), dim3(64), 0, st, out);
 	return herr(hipGetLastError(), "plan launch");
+}
+
+__global__ void __launch_bounds__(256)
+k_plan_results(const uint32_t *__restrict__ guard,
+	       const uint32_t *__restrict__ end0, uint32_t *__restrict__ end,
+	       int32_t *__restrict__ err, uint32_t n, int32_t delta)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n || *guard)
+		return;
+	end[i] = end0[i] + (uint32_t)delta;
+	err[i] = 0;
+}
+
+extern "C" int sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
+				 uint32_t *end, int32_t *err, uint32_t n,
+				 int32_t delta, void *stream)
+{
+	if (!n)
+		return 0;
+	hipLaunchKernelGGL(k_plan_results, dim3((n + 255) / 256), dim3(256), 0,
+			   (hipStream_t)stream, guard, end0, end, err, n, delta);
+	return herr(hipGetLastError(), "results launch");
+}
+
+extern "C" int sgpu_memcpy_d2d(void *dst, const void *src, size_t n,
+			       void *stream)
+{
+	if (!n)
+		return 0;
+	return herr(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice,
+				   (hipStream_t)stream), "d2d");
 }

@@ -987,6 +987,7 @@ struct ws {
 	struct pool vs;         /* verdict | save | nfail */
 	struct pool cm;         /* session -> comp index */
 	struct pool pl;         /* device planner: out | scratch */
+	struct pool es;         /* device API: original ends */
 	void **ev;              /* per-chunk parse events */
 	size_t nev;
 	struct ulog *ulog;      /* stream-state undo log */
@@ -1460,7 +1461,8 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 	eix_h = (uint32_t *)(w->hdr.h + 8 * n + n * sizeof(struct sgpu_hdr));
 	err = sgpu_memcpy_h2d(w->hdr.d, w->hdr.h, 8 * n, stream);
 	if (!err)
-		err = sgpu_parse_headers(b->arena, (const uint32_t *)w->hdr.d,
+		err = sgpu_parse_headers(b->arena, b->arena_size,
+					 (const uint32_t *)w->hdr.d,
 					 (const uint32_t *)w->hdr.d + n,
 					 (struct sgpu_hdr *)(w->hdr.d + 8 * n),
 					 rtcp && op == OP_RTCP_DEC ?
@@ -1601,6 +1603,7 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
  */
 
 static uint32_t g_epoch;
+static __thread int t_noplan;   /* fallback of a rejected device plan */
 
 static int ulog_push(struct ws *w, struct srtp *s, struct srtp_stream *st)
 {
@@ -1886,6 +1889,53 @@ static struct replay plan_replay(const struct replay *r0,
 	return r;
 }
 
+/* planner input from the session's (single) stream */
+static void plan_in(struct sgpu_plan_in *in, const struct srtp *s,
+		    uint32_t n, int prot, uint32_t T, uint32_t need)
+{
+	const struct srtp_stream *st0 = s->nstreams ? &s->streams[0] : NULL;
+	memset(in, 0, sizeof(*in));
+	in->n = n;
+	in->prot = (uint32_t)prot;
+	in->fresh = !st0 || !st0->s_l_set;
+	in->ssrc_any = !st0;
+	in->ssrc = st0 ? st0->ssrc : 0;
+	in->roc = st0 ? st0->roc : 0;
+	in->s_l = st0 ? st0->s_l : 0;
+	in->lix = st0 ? st0->replay_rtp.lix : 0;
+	in->bitmap = st0 ? st0->replay_rtp.bitmap : 0;
+	in->tag = T;
+	in->need = need;
+}
+
+/* stream state after an accepted device plan (old state kept for undo) */
+static void plan_apply(struct srtp *s, const struct sgpu_plan_out *po,
+		       int prot, size_t n, struct srtp_stream *old)
+{
+	struct srtp_stream *st;
+	if (s->nstreams)
+		*old = s->streams[0];
+	else {
+		memset(&s->streams[0], 0, sizeof(s->streams[0]));
+		s->streams[0].ssrc = po->ssrc0;
+		s->nstreams = 1;
+	}
+	st = &s->streams[0];
+	st->s_l_set = 1;
+	st->roc += po->wraps;
+	st->s_l = (uint16_t)po->s_l_last;
+	if (!prot)
+		st->replay_rtp = plan_replay(&st->replay_rtp, po, n);
+}
+
+static void plan_unapply(struct srtp *s, unsigned nstreams0,
+			 const struct srtp_stream *old)
+{
+	if (nstreams0)
+		s->streams[0] = *old;
+	s->nstreams = nstreams0;
+}
+
 /*
  * Returns 0 / errno like run_batch, or -1 when the batch is not eligible
  * (nothing touched: caller runs the general engine).
@@ -1910,6 +1960,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	void *stream, *entry_ev = NULL;
 	struct ws *w;
 	int err = 0, parsed = 0, planned = 0;
+	void *pst;
 	/* planned path: stream state before the call (undo) */
 	struct srtp *ps = sessv[0];
 	unsigned ps_n = ps->nstreams;
@@ -1934,6 +1985,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			return EIO;
 	}
 	stream = b->stream ? b->stream : w->stream;
+	pst = w->pstream;
 
 	err = pool_reserve(w, &w->up, n * 12);
 	if (!err)
@@ -1978,63 +2030,71 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	for (k = 0; k < nsess; k++)
 		cm_h[k] = sessv[k]->rtp.dev;
 
-	entry_ev = w->ev[0];
-	if (b->stream) {
-		err = sgpu_event_record(entry_ev, stream);
-		if (!err)
-			err = sgpu_stream_wait(w->pstream, entry_ev);
-		if (err)
-			goto out;
-	}
-	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->pstream);
-	if (!err && !prot)
-		err = sgpu_memset(nfail_d, 0, 4, w->pstream);
-	if (err)
-		goto out;
 
-	/* 0. one stream: plan on the device (speculative scan, verified) */
-	if (nsess == 1 && ps->nstreams <= 1 && !getenv("RE_SRTP_NOPLAN")) {
+	/* 0. one stream: plan on the device (speculative scan, verified).
+	 *    Everything is queued on one stream with a single sync: the
+	 *    crypto launches are guarded on the device by the plan's verdict
+	 *    (sgpu_plan_out.skip), so a rejected plan modifies nothing. */
+	if (nsess == 1 && ps->nstreams <= 1 && !t_noplan &&
+	    !getenv("RE_SRTP_NOPLAN")) {
 		struct sgpu_plan_in in;
 		struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
 		struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
 		uint32_t *scr = (uint32_t *)(w->pl.d + sizeof(*po));
-		const struct srtp_stream *st0 =
-			ps->nstreams ? &ps->streams[0] : NULL;
 		const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 				      (T > 4 ? T : 4u)) : 0u;
-		int capok = 1;
+		int capok = 1, q;
 
-		memset(&in, 0, sizeof(in));
-		in.n = (uint32_t)n;
-		in.prot = (uint32_t)prot;
-		in.fresh = !st0 || !st0->s_l_set;
-		in.ssrc_any = !st0;
-		in.ssrc = st0 ? st0->ssrc : 0;
-		in.roc = st0 ? st0->roc : 0;
-		in.s_l = st0 ? st0->s_l : 0;
-		in.lix = st0 ? st0->replay_rtp.lix : 0;
-		in.bitmap = st0 ? st0->replay_rtp.bitmap : 0;
-		in.tag = T;
+		plan_in(&in, ps, (uint32_t)n, prot, T, need);
 		memcpy(up_h, b->pos, n * 4);
 		memcpy(up_h + n, b->end, n * 4);
-		err = sgpu_memcpy_h2d(up_d, up_h, n * 8, w->pstream);
+		err = sgpu_memcpy_h2d(w->cm.d, cm_h, 4, stream);
+		if (!err && !prot)
+			err = sgpu_memset(nfail_d, 0, 4, stream);
 		if (!err)
-			err = sgpu_parse_headers(b->arena, up_d, up_d + n, hd_d,
-						 NULL, (uint32_t)n, 0,
-						 w->pstream);
+			err = sgpu_memcpy_h2d(up_d, up_h, n * 8, stream);
 		if (!err)
-			err = sgpu_plan_rtp(&in, hd_d, up_d, up_d + n, desc_d,
-					    scr, po_d, w->pstream);
+			err = sgpu_parse_headers(b->arena, b->arena_size, up_d,
+						 up_d + n, hd_d, NULL,
+						 (uint32_t)n, 0, stream);
 		if (!err)
-			err = sgpu_memcpy_d2h(po, po_d, sizeof(*po),
-					      w->pstream);
+			err = sgpu_plan_rtp(&in, hd_d, up_d, up_d + n, NULL,
+					    b->arena_size, desc_d, scr, po_d,
+					    stream);
 		if (err)
 			goto out;
-		/* device arenas cannot grow (cap_short) */
+		/* device arenas cannot grow (cap_short), checked while the
+		 * GPU plans */
 		if (prot)
 			for (i = 0; i < n; i++)
 				capok &= (uint64_t)b->end[i] + need <= b->cap[i];
-		err = sgpu_stream_sync(w->pstream);
+		for (q = 0; q < 4 && capok && !err; q++) {
+			struct sgpu_compact C = {
+				up_d, up_d + n, hd_d, desc_d, NULL,
+				(const uint32_t *)w->cm.d, NULL, 0,
+				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1,
+				&po_d->skip[q]};
+			err = sgpu_run_compact(b->arena, b->arena_size, &C,
+					       c0->mode, (int)c0->nr, q, prot,
+					       stream);
+		}
+		if (!err)
+			err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+		if (!err && !prot && capok)
+			err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+		if (err)
+			goto out;
+		/* per-packet results, speculatively, while the GPU runs */
+		if (capok) {
+			if (prot)
+				for (i = 0; i < n; i++)
+					b->end[i] += T;
+			else
+				for (i = 0; i < n; i++)
+					b->end[i] -= T;
+			memset(b->err, 0, n * sizeof(*b->err));
+		}
+		err = sgpu_stream_sync(stream);
 		if (err)
 			goto out;
 		parsed = 1;
@@ -2044,60 +2104,52 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				"dec", n, po->fail, po->wraps, capok,
 				now_ms() - t0);
 		if (!po->fail && capok) {
-			struct srtp_stream *st;
-			if (!prot && st0)
-				ps_old = *st0;
-			if (!st0) {
-				memset(&ps->streams[0], 0, sizeof(ps->streams[0]));
-				ps->streams[0].ssrc = po->ssrc0;
-				ps->nstreams = 1;
-			}
-			st = &ps->streams[0];
-			st->s_l_set = 1;
-			st->roc += po->wraps;
-			st->s_l = (uint16_t)po->s_l_last;
-			if (!prot)
-				st->replay_rtp = plan_replay(&st->replay_rtp, po,
-							     n);
-			fl[nfl++] = (struct flaunch){0, (uint32_t)n,
-						     (po->hl0 >> 2) & 3u, 0};
+			plan_apply(ps, po, prot, n, &ps_old);
+			for (q = 0; q < 4; q++)
+				fl[nfl++] = (struct flaunch){0, (uint32_t)n,
+							     (uint32_t)q, 0};
 			planned = 1;
-			/* pstream work is complete (synchronised above) */
-			{
-				struct sgpu_compact C = {
-					up_d, up_d + n, hd_d, desc_d, NULL,
-					(const uint32_t *)w->cm.d, NULL, 0,
-					(uint32_t)n, vd_d, save_d, nfail_d, 0, 1};
-				err = sgpu_run_compact(b->arena,
-						       b->arena_size, &C,
-						       c0->mode, (int)c0->nr,
-						       (int)fl[0].shift, prot,
-						       stream);
-			}
-			if (err)
-				goto out;
-			/* per-packet results, while the GPU runs */
-			for (i = 0; i < n; i++) {
-				b->end[i] = prot ? b->end[i] + T : b->end[i] - T;
-				b->err[i] = 0;
-			}
 			if (trace)
 				t1 = t2 = now_ms();
-			goto finish;
+			goto checked;
 		}
+		if (capok)
+			memcpy(b->end, up_h + n, n * 4);
 		/* not plannable: headers down for the host scan */
-		err = sgpu_memcpy_d2h(w->hd.h, hd_d, n * sizeof(*hd_d),
-				      w->pstream);
+		pst = stream;
+		err = sgpu_memcpy_d2h(w->hd.h, hd_d, n * sizeof(*hd_d), stream);
+		if (!err && !prot)
+			err = sgpu_memset(nfail_d, 0, 4, stream);
 		if (err)
 			goto out;
 	}
 
 	/* 1. parse stream: staged windows up, headers parsed, back down,
 	 *    chunk by chunk (ordered after the caller's prior work) */
+	if (!parsed) {
+		entry_ev = w->ev[0];
+		if (b->stream) {
+			err = sgpu_event_record(entry_ev, stream);
+			if (!err)
+				err = sgpu_stream_wait(w->pstream, entry_ev);
+		}
+		if (!err)
+			err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4,
+					      w->pstream);
+		if (!err && !prot)
+			err = sgpu_memset(nfail_d, 0, 4, w->pstream);
+		if (err)
+			goto out;
+	}
+	else {
+		err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
+		if (err)
+			goto out;
+	}
 	for (k = 0; k < nch && !err; k++) {
 		const size_t a = k * CH, e = a + CH < n ? a + CH : n;
 		if (parsed) {
-			err = sgpu_event_record(w->ev[k], w->pstream);
+			err = sgpu_event_record(w->ev[k], pst);
 			continue;
 		}
 		memcpy(up_h + a, b->pos + a, (e - a) * 4);
@@ -2114,7 +2166,8 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 					      w->pstream);
 		}
 		if (!err)
-			err = sgpu_parse_headers(b->arena, up_d + a,
+			err = sgpu_parse_headers(b->arena, b->arena_size,
+						 up_d + a,
 						 up_d + n + a, hd_d + a, NULL,
 						 (uint32_t)(e - a), 0,
 						 w->pstream);
@@ -2214,7 +2267,8 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				b->sess ? up_d + 2 * n : NULL,
 				(const uint32_t *)w->cm.d,
 				fl[q].has_idx ? idx_d : NULL, fl[q].base,
-				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1};
+				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1,
+				NULL};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[q].shift, prot, stream);
@@ -2222,11 +2276,11 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	}
 	if (trace)
 		t2 = now_ms();
- finish:
 	if (!err && !prot)
 		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
+ checked:
 	if (trace)
 		fprintf(stderr, "re_srtp fast %s n=%zu%s: stage %.3f ms, "
 			"parse-wait %.3f, scan %.3f, launch %.3f, tail %.3f, "
@@ -2244,7 +2298,9 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				b->sess ? up_d + 2 * n : NULL,
 				(const uint32_t *)w->cm.d,
 				fl[k].has_idx ? idx_d : NULL, fl[k].base,
-				fl[k].n, vd_d, save_d, nfail_d, 1, nsess == 1};
+				fl[k].n, vd_d, save_d, nfail_d, 1, nsess == 1,
+				planned ? &((struct sgpu_plan_out *)w->pl.d)->
+					  skip[fl[k].shift] : NULL};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[k].shift, prot, stream);
@@ -2253,11 +2309,8 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			err = sgpu_stream_sync(stream);
 		if (err)
 			goto out;
-		if (planned) {
-			if (ps_n)
-				ps->streams[0] = ps_old;
-			ps->nstreams = ps_n;
-		}
+		if (planned)
+			plan_unapply(ps, ps_n, &ps_old);
 		ulog_undo(w);
 		memcpy(b->pos, up_h, n * 4);
 		memcpy(b->end, up_h + n, n * 4);
@@ -2303,6 +2356,225 @@ static int run_batch(int op, struct srtp **sessv, size_t nsess,
 			return r;
 	}
 	return run_batch_general(op, sessv, nsess, b);
+}
+
+/* ---- fully device-resident batches ------------------------------------ */
+
+static int run_batch(int op, struct srtp **sessv, size_t nsess,
+		     struct srtp_batch *b);
+
+/* single-stream RTP batch planned and processed on the device; -1: not
+ * plannable (nothing modified), else 0 / errno */
+static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
+{
+	const int prot = op == OP_RTP_ENC;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
+	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
+			      (T > 4 ? T : 4u)) : 0u;
+	const unsigned ns0 = s->nstreams;
+	struct srtp_stream old;
+	struct sgpu_plan_in in;
+	struct sgpu_plan_out *po, *po_d;
+	struct sgpu_hdr *hd_d;
+	uint64_t *desc_d;
+	uint32_t *scr, *es_d, *save_d, *nfail_d, nfail = 0, cm = c0->dev;
+	uint8_t *vd_d;
+	void *stream;
+	struct ws *w = ws_get();
+	int err, q;
+
+	if (!w)
+		return ENOMEM;
+	stream = d->stream ? d->stream : w->stream;
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 12);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out) +
+				   (n / 256 + 8) * 4);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (err)
+		return err;
+	hd_d = (struct sgpu_hdr *)w->hd.d;
+	desc_d = (uint64_t *)w->dsc.d;
+	nfail_d = (uint32_t *)w->vs.d;
+	save_d = (uint32_t *)(w->vs.d + 64);
+	vd_d = w->vs.d + 64 + n * 4;
+	po = (struct sgpu_plan_out *)w->pl.h;
+	po_d = (struct sgpu_plan_out *)w->pl.d;
+	scr = (uint32_t *)(w->pl.d + sizeof(*po));
+	es_d = (uint32_t *)w->es.d;
+
+	plan_in(&in, s, (uint32_t)n, prot, T, need);
+	*(uint32_t *)w->cm.h = cm;
+	err = sgpu_memcpy_h2d(w->cm.d, w->cm.h, 4, stream);
+	if (!err)
+		err = sgpu_memset(nfail_d, 0, 4, stream);
+	if (!err)
+		err = sgpu_memcpy_d2d(es_d, d->end, n * 4, stream);
+	if (!err)
+		err = sgpu_parse_headers(d->arena, d->arena_size, d->pos, es_d,
+					 hd_d, NULL, (uint32_t)n, 0, stream);
+	if (!err)
+		err = sgpu_plan_rtp(&in, hd_d, d->pos, es_d, d->cap,
+				    d->arena_size, desc_d, scr, po_d, stream);
+	for (q = 0; q < 4 && !err; q++) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, NULL,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 0, 1, &po_d->skip[q]};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, q, prot, stream);
+	}
+	if (!err)
+		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
+					(uint32_t)n,
+					prot ? (int32_t)T : -(int32_t)T, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	if (po->fail)
+		return -1;
+	plan_apply(s, po, prot, n, &old);
+	if (!nfail)
+		return 0;
+	/* a forged packet: undo on the device, fold on the host engine */
+	for (q = 0; q < 4 && !err; q++) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, NULL,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 1, 1, &po_d->skip[q]};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, q, prot, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, es_d, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	plan_unapply(s, ns0, &old);
+	return -1;
+}
+
+/* any other batch: stage the device arrays through the host engine */
+static int dev_staged(int op, struct srtp **sessv, size_t nsess,
+		      struct srtp_batch_dev *d)
+{
+	const size_t n = d->n;
+	struct srtp_batch hb;
+	uint32_t *hpos = malloc(n * 4), *hend = malloc(n * 4);
+	uint32_t *hcap = malloc(n * 4), *hsess = d->sess ? malloc(n * 4) : NULL;
+	int32_t *herrv = malloc(n * 4);
+	void *stream = d->stream;
+	int err = 0, r;
+
+	if (!hpos || !hend || !hcap || !herrv || (d->sess && !hsess)) {
+		err = ENOMEM;
+		goto out;
+	}
+	err = sgpu_memcpy_d2h(hpos, d->pos, n * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(hend, d->end, n * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(hcap, d->cap, n * 4, stream);
+	if (!err && d->sess)
+		err = sgpu_memcpy_d2h(hsess, d->sess, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		goto out;
+	memset(&hb, 0, sizeof(hb));
+	hb.arena = d->arena;
+	hb.arena_size = d->arena_size;
+	hb.pos = hpos;
+	hb.end = hend;
+	hb.cap = hcap;
+	hb.err = herrv;
+	hb.sess = hsess;
+	hb.n = n;
+	hb.stream = stream;
+	t_noplan = 1;
+	r = run_batch(op, sessv, nsess, &hb);
+	t_noplan = 0;
+	if (r) {
+		err = r;
+		goto out;
+	}
+	err = sgpu_memcpy_h2d(d->pos, hpos, n * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_h2d(d->end, hend, n * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_h2d(d->err, herrv, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+ out:
+	free(hpos);
+	free(hend);
+	free(hcap);
+	free(hsess);
+	free(herrv);
+	return err;
+}
+
+static int run_dev(int op, struct srtp **sessv, size_t nsess,
+		   struct srtp_batch_dev *d)
+{
+	size_t k;
+	if (!sessv || !nsess || !d || !d->arena || !d->pos || !d->end ||
+	    !d->cap || !d->err)
+		return EINVAL;
+	for (k = 0; k < nsess; k++)
+		if (!sessv[k])
+			return EINVAL;
+	if (d->n == 0)
+		return 0;
+	if (d->n > UINT32_MAX / 4 || d->arena_size > UINT32_MAX)
+		return EINVAL;
+	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess == 1 &&
+	    !d->sess && sessv[0]->nstreams <= 1 &&
+	    !getenv("RE_SRTP_NOPLAN") && !getenv("RE_SRTP_GENERAL")) {
+		int r = dev_planned(op, sessv[0], d);
+		if (r >= 0)
+			return r;
+	}
+	return dev_staged(op, sessv, nsess, d);
+}
+
+int srtp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			   struct srtp_batch_dev *b)
+{
+	return run_dev(OP_RTP_ENC, sessv, nsess, b);
+}
+
+int srtp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			   struct srtp_batch_dev *b)
+{
+	return run_dev(OP_RTP_DEC, sessv, nsess, b);
+}
+
+int srtcp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			    struct srtp_batch_dev *b)
+{
+	return run_dev(OP_RTCP_ENC, sessv, nsess, b);
+}
+
+int srtcp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
+			    struct srtp_batch_dev *b)
+{
+	return run_dev(OP_RTCP_DEC, sessv, nsess, b);
 }
 
 int srtp_encrypt_batch(struct srtp **sessv, size_t nsess,

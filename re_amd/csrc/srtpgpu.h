@@ -152,6 +152,8 @@ struct sgpu_compact {
 	uint32_t *nfail;                /* +1 per speculation miss (device) */
 	int undo;                       /* restore the pre-call bytes */
 	int uniform;                    /* every packet: one session context */
+	const uint32_t *guard;          /* device word; nonzero: do nothing
+					   (a rejected device plan) or NULL */
 };
 
 /* launch the compact kernel of class (mode, nr, shift, prot) */
@@ -177,6 +179,8 @@ struct sgpu_plan_in {
 	uint64_t bitmap;
 	uint32_t tag;           /* bytes the tag adds / removes */
 	uint32_t ssrc_any;      /* no stream yet: take packet 0's SSRC */
+	uint32_t need;          /* protect: tag room end + need <= cap */
+	uint32_t pad;
 };
 
 enum {
@@ -186,7 +190,9 @@ enum {
 	SPF_ORDER   = 1u << 3,  /* s_l speculation broken (reordering) */
 	SPF_TIMEOUT = 1u << 4,  /* ETIMEDOUT */
 	SPF_REPLAY  = 1u << 5,  /* index not strictly increasing */
-	SPF_SIZE    = 1u << 6,  /* packet too long for 32-bit offsets */
+	SPF_SIZE    = 1u << 6,  /* payload of 1 MiB or more */
+	SPF_CAP     = 1u << 7,  /* protect: tag does not fit (ENOMEM) */
+	SPF_BAD     = 1u << 8,  /* invalid window (pos/end/cap/arena) */
 };
 
 #define SGPU_PLAN_TAIL 65
@@ -197,14 +203,24 @@ struct sgpu_plan_out {
 	uint32_t hl0;           /* header length of packet 0 */
 	uint32_t s_l_last;      /* s_l after the last packet */
 	uint32_t pad;
+	uint32_t skip[4];       /* guard of the shift-class-s crypto launch:
+				   fail || class(hl0) != s */
 	uint64_t tail_ix[SGPU_PLAN_TAIL]; /* ix of the last min(n,65) packets */
 };
 
-/* plan n packets (hdr/pos/end device arrays) into desc (device); scratch
- * holds >= n/256 + 2 words; out is a device pointer */
+/* plan n packets (hdr/pos/end/cap device arrays; cap may be NULL) into
+ * desc (device); scratch holds >= n/256 + 2 words; out is a device
+ * pointer.  out->fail is the guard of the launches that follow. */
 int   sgpu_plan_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
-		    const uint32_t *pos, const uint32_t *end, uint64_t *desc,
-		    uint32_t *scratch, struct sgpu_plan_out *out, void *stream);
+		    const uint32_t *pos, const uint32_t *end, const uint32_t *cap,
+		    uint64_t arena_size, uint64_t *desc, uint32_t *scratch,
+		    struct sgpu_plan_out *out, void *stream);
+
+/* guarded per-packet results of a device-planned batch (device arrays):
+ * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */
+int   sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
+			uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
+			void *stream);
 
 /* store 4 raw bytes (LE word vals[i]) at arena + offs[i], any alignment
  * (restores tag bytes before a re-run) -- device arrays */
@@ -221,9 +237,10 @@ struct sgpu_hdr {               /* 12 bytes */
 };
 /* eix (RTCP, optional): 3 words per packet, the BE word at end-4-tl for
  * tl = 0, 4, 10 (the E-bit/SRTCP-index word for each tag length). */
-int   sgpu_parse_headers(const uint8_t *arena, const uint32_t *pos,
-			 const uint32_t *end, struct sgpu_hdr *out,
-			 uint32_t *eix, uint32_t n, int rtcp, void *stream);
+int   sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,
+			 const uint32_t *pos, const uint32_t *end,
+			 struct sgpu_hdr *out, uint32_t *eix, uint32_t n,
+			 int rtcp, void *stream);
 
 /* kernel timing (HIP events recorded on the launch stream) */
 void  sgpu_prof_enable(int on);
@@ -236,6 +253,7 @@ void *sgpu_host_alloc(size_t n);
 void  sgpu_host_free(void *p);
 int   sgpu_memcpy_h2d(void *dst, const void *src, size_t n, void *stream);
 int   sgpu_memcpy_d2h(void *dst, const void *src, size_t n, void *stream);
+int   sgpu_memcpy_d2d(void *dst, const void *src, size_t n, void *stream);
 int   sgpu_memset(void *dst, int v, size_t n, void *stream);
 int   sgpu_stream_sync(void *stream);
 int   sgpu_device_sync(void);

@@ -59,6 +59,20 @@ class SrtpBatch(ctypes.Structure):
                 ("stream", ctypes.c_void_p)]
 
 
+class SrtpBatchDev(ctypes.Structure):
+    """struct srtp_batch_dev (include/re_srtp_batch.h): every per-packet
+    array is a device pointer"""
+    _fields_ = [("arena", ctypes.c_void_p),
+                ("arena_size", ctypes.c_size_t),
+                ("pos", ctypes.c_void_p),
+                ("end", ctypes.c_void_p),
+                ("cap", ctypes.c_void_p),
+                ("err", ctypes.c_void_p),
+                ("sess", ctypes.c_void_p),
+                ("n", ctypes.c_size_t),
+                ("stream", ctypes.c_void_p)]
+
+
 class StreamState(ctypes.Structure):
     _fields_ = [("replay_rtp_bitmap", ctypes.c_uint64),
                 ("replay_rtp_lix", ctypes.c_uint64),
@@ -77,7 +91,9 @@ EXPORTS = (
     "srtcp_decrypt", "srtp_suite_name",
     "srtp_encrypt_mbufs", "srtp_decrypt_mbufs", "srtcp_encrypt_mbufs",
     "srtcp_decrypt_mbufs", "srtp_encrypt_batch", "srtp_decrypt_batch",
-    "srtcp_encrypt_batch", "srtcp_decrypt_batch", "srtp_stream_export",
+    "srtcp_encrypt_batch", "srtcp_decrypt_batch", "srtp_encrypt_batch_dev",
+    "srtp_decrypt_batch_dev", "srtcp_encrypt_batch_dev",
+    "srtcp_decrypt_batch_dev", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
     "srtp_gpu_prof", "srtp_gpu_prof_read",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
@@ -107,6 +123,8 @@ def load():
             ctypes.POINTER(ctypes.c_int), sz]
         getattr(L, f + "_batch").argtypes = [
             ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatch)]
+        getattr(L, f + "_batch_dev").argtypes = [
+            ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatchDev)]
     L.srtp_suite_name.restype = ctypes.c_char_p
     L.srtp_suite_name.argtypes = [ctypes.c_int]
     L.srtp_gpu_error.restype = ctypes.c_char_p
@@ -261,6 +279,24 @@ def device_batch(opname, sessions, arena_ptr, arena_size, pos, end, cap,
     sv = (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
     rc = getattr(lib(), opname + "_batch")(sv, len(sessions), ctypes.byref(b))
     return rc, err
+
+
+def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
+                     end_ptr, cap_ptr, err_ptr, n, sess_ptr=None,
+                     stream=None):
+    """srtp_*_batch_dev: arena and every per-packet array (uint32 pos/end/
+    cap, int32 err, optional uint32 sess) are device pointers; pos/end/err
+    are updated on the device.  Returns rc."""
+    b = SrtpBatchDev()
+    b.arena = arena_ptr
+    b.arena_size = arena_size
+    b.pos, b.end, b.cap, b.err = pos_ptr, end_ptr, cap_ptr, err_ptr
+    b.sess = sess_ptr
+    b.n = n
+    b.stream = stream
+    sv = (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
+    return getattr(lib(), opname + "_batch_dev")(sv, len(sessions),
+                                                 ctypes.byref(b))
 
 
 def prof_enable(on=True):

@@ -345,3 +345,67 @@ def test_device_planner_and_its_fallbacks(suite, torch_cuda):
                 for u, v in zip(x, y):
                     assert (u == v).all(), (name, mode)
             assert A[2] == B[2] and A[3] == B[3], (name, mode)
+
+
+def run_dev(torch, opname, sessions, arena, pos, end, cap, sess):
+    """srtp_*_batch_dev with every per-packet array in HBM"""
+    dev = torch.from_numpy(arena.copy()).cuda()
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).cuda()
+    p = t(pos.astype(np.int64), np.int64).to(torch.int32)
+    e = t(end.astype(np.int64), np.int64).to(torch.int32)
+    c = t(cap.astype(np.int64), np.int64).to(torch.int32)
+    er = torch.full((len(pos),), -1, dtype=torch.int32, device="cuda")
+    s = t(sess.astype(np.int64), np.int64).to(torch.int32) \
+        if sess is not None else None
+    torch.cuda.synchronize()
+    rc = P.device_batch_dev(opname, sessions, dev.data_ptr(), arena.nbytes,
+                            p.data_ptr(), e.data_ptr(), c.data_ptr(),
+                            er.data_ptr(), len(pos),
+                            s.data_ptr() if s is not None else None)
+    assert rc == 0, (rc, P.lib().srtp_gpu_error())
+    torch.cuda.synchronize()
+    u32 = lambda x: x.cpu().numpy().view(np.uint32)
+    return dev.cpu().numpy(), u32(p), u32(e), er.cpu().numpy()
+
+
+@pytest.mark.parametrize("suite", [1, 4])
+def test_device_resident_api(suite, torch_cuda):
+    """srtp_*_batch_dev == srtp_*_batch: planned single stream, forged
+    packet (undo + fold), multi-session (staged), SRTCP (staged)"""
+    torch = torch_cuda
+    rng = np.random.default_rng(9 + suite)
+    key = keys_for(suite, 1)[0]
+    seqs = list(range(65300, 65300 + 2000))
+    pkts = seq_batch(rng, seqs)
+    arena, pos, end, cap, _ = to_arena(pkts)
+    txa, txb = P.Srtp(suite, key), P.Srtp(suite, key)
+    a = run_dev(torch, "srtp_encrypt", [txa], arena, pos, end, cap, None)
+    b = run(torch, "srtp_encrypt", [txb], arena, pos, end, cap, None, False)
+    for x, y in zip(a, b):
+        assert (x == y).all()
+    assert states([txa], [0x5151]) == states([txb], [0x5151])
+    # receive with one forged packet
+    prot = [(0, a[0][pos[i]:a[2][i]].tobytes()) for i in range(len(pkts))]
+    q = bytearray(prot[700][1])
+    q[40] ^= 1
+    prot[700] = (0, bytes(q))
+    a2, p2, e2, c2, _ = to_arena(prot)
+    rxa, rxb = P.Srtp(suite, key), P.Srtp(suite, key)
+    da = run_dev(torch, "srtp_decrypt", [rxa], a2, p2, e2, c2, None)
+    db = run(torch, "srtp_decrypt", [rxb], a2, p2, e2, c2, None, True)
+    for x, y in zip(da, db):
+        assert (x == y).all()
+    assert da[3][700] == P.EAUTH and (np.delete(da[3], 700) == 0).all()
+    assert states([rxa], [0x5151]) == states([rxb], [0x5151])
+    # multi-session: staged through the host engine
+    keys = keys_for(suite, 3)
+    mp = make_traffic(rng, 600, 3, enosr=False)
+    ma, mpos, mend, mcap, msess = to_arena(mp)
+    sa = [P.Srtp(suite, k) for k in keys]
+    sb = [P.Srtp(suite, k) for k in keys]
+    x = run_dev(torch, "srtp_encrypt", sa, ma, mpos, mend, mcap, msess)
+    y = run(torch, "srtp_encrypt", sb, ma, mpos, mend, mcap, msess, True)
+    for u, v in zip(x, y):
+        assert (u == v).all()
+    for c in [txa, txb, rxa, rxb] + sa + sb:
+        c.close()

@@ -47,24 +47,6 @@ CONFIGS = {
 }
 
 
-def shard_state(rank, per_rank, s0, ssrc, receiver):
-    """Stream state after a sequential sender/receiver processed packets
-    0 .. rank*per_rank-1 with seq = (s0+i) mod 2^16 (srtp.c:203-213,
-    279-280; replay.c:32-62)."""
-    import re_amd.srtp as P
-    st = P.StreamState()
-    last = s0 + rank * per_rank - 1
-    st.ssrc = ssrc
-    st.roc = last >> 16
-    st.s_l = last & 0xffff
-    st.s_l_set = 1
-    if receiver:
-        st.replay_rtp_lix = last
-        st.replay_rtp_bitmap = (1 << 64) - 1 if rank * per_rank >= 64 else \
-            (1 << (rank * per_rank)) - 1
-    return st
-
-
 def cpu_baseline(cfg):
     """Reference src/srtp (oracle/_ref, OpenSSL) on the host cores, bounded
     sample; falls back to the portable restatement (kind "port")."""
@@ -125,6 +107,7 @@ def main():
     import torch
     import torch.distributed as dist
     import re_amd.srtp as P
+    from re_amd import shard as S
     from re_amd import workload as W
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,7 +126,7 @@ def main():
     n, suite, nsess = cfg["n"], cfg["suite"], cfg["nsess"]
     s0 = 65000
     if cfg_id == 5:
-        s0 = (65000 + rank * n)           # global index of this shard
+        s0 = S.shard_seq0(rank, n, 65000)   # this shard's first seq
     lengths = cfg["length"] if cfg["length"] else W.mixed_lengths(n)
     sess = W.random_sessions(n, nsess) if nsess > 1 else None
     arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
@@ -163,10 +146,10 @@ def main():
         e2, rx = P.alloc_many(nsess, suite, keys.tobytes())
         assert not e1 and not e2, (e1, e2, P.lib().srtp_gpu_error())
         if cfg_id == 5 and rank > 0:
-            assert tx[0].import_(shard_state(rank, n, 65000,
-                                             W.SSRC_BASE, False)) == 0
-            assert rx[0].import_(shard_state(rank, n, 65000,
-                                             W.SSRC_BASE, True)) == 0
+            assert tx[0].import_(S.shard_state(
+                rank, n, 65000, W.SSRC_BASE, False, P.StreamState)) == 0
+            assert rx[0].import_(S.shard_state(
+                rank, n, 65000, W.SSRC_BASE, True, P.StreamState)) == 0
         return tx, rx
 
     # per-call descriptor arrays (the API updates pos/end in place).
@@ -238,9 +221,7 @@ def main():
     counters = torch.tensor([n * args.steps, rtp_bytes * args.steps, errors],
                             dtype=torch.float64, device=dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    S.reduce_results(dist if world > 1 else None, counters, tmax)
     tot_pkts, tot_bytes, tot_err = [float(x) for x in counters.tolist()]
     T = float(tmax.item())
     verified = None

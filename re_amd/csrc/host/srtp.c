@@ -2044,6 +2044,10 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 				      (T > 4 ? T : 4u)) : 0u;
 		int capok = 1, q;
+		/* CTR kernels are specialised per header shift class (one
+		 * launch runs, the others exit on their guard); GCM is not */
+		const int gcm = c0->mode == SGPU_MODE_GCM;
+		const int nclass = gcm ? 1 : 4;
 
 		plan_in(&in, ps, (uint32_t)n, prot, T, need);
 		memcpy(up_h, b->pos, n * 4);
@@ -2068,12 +2072,12 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		if (prot)
 			for (i = 0; i < n; i++)
 				capok &= (uint64_t)b->end[i] + need <= b->cap[i];
-		for (q = 0; q < 4 && capok && !err; q++) {
+		for (q = 0; q < nclass && capok && !err; q++) {
 			struct sgpu_compact C = {
 				up_d, up_d + n, hd_d, desc_d, NULL,
 				(const uint32_t *)w->cm.d, NULL, 0,
 				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1,
-				&po_d->skip[q]};
+				gcm ? &po_d->fail : &po_d->skip[q]};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr, q, prot,
 					       stream);
@@ -2105,7 +2109,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				now_ms() - t0);
 		if (!po->fail && capok) {
 			plan_apply(ps, po, prot, n, &ps_old);
-			for (q = 0; q < 4; q++)
+			for (q = 0; q < nclass; q++)
 				fl[nfl++] = (struct flaunch){0, (uint32_t)n,
 							     (uint32_t)q, 0};
 			planned = 1;
@@ -2299,8 +2303,11 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				(const uint32_t *)w->cm.d,
 				fl[k].has_idx ? idx_d : NULL, fl[k].base,
 				fl[k].n, vd_d, save_d, nfail_d, 1, nsess == 1,
-				planned ? &((struct sgpu_plan_out *)w->pl.d)->
-					  skip[fl[k].shift] : NULL};
+				!planned ? NULL :
+				c0->mode == SGPU_MODE_GCM ?
+				&((struct sgpu_plan_out *)w->pl.d)->fail :
+				&((struct sgpu_plan_out *)w->pl.d)->
+					  skip[fl[k].shift]};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[k].shift, prot, stream);
@@ -2374,6 +2381,8 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 			      (T > 4 ? T : 4u)) : 0u;
 	const unsigned ns0 = s->nstreams;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const int nclass = gcm ? 1 : 4;
 	struct srtp_stream old;
 	struct sgpu_plan_in in;
 	struct sgpu_plan_out *po, *po_d;
@@ -2425,11 +2434,12 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!err)
 		err = sgpu_plan_rtp(&in, hd_d, d->pos, es_d, d->cap,
 				    d->arena_size, desc_d, scr, po_d, stream);
-	for (q = 0; q < 4 && !err; q++) {
+	for (q = 0; q < nclass && !err; q++) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1, &po_d->skip[q]};
+			save_d, nfail_d, 0, 1,
+			gcm ? &po_d->fail : &po_d->skip[q]};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, q, prot, stream);
 	}
@@ -2451,11 +2461,12 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!nfail)
 		return 0;
 	/* a forged packet: undo on the device, fold on the host engine */
-	for (q = 0; q < 4 && !err; q++) {
+	for (q = 0; q < nclass && !err; q++) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 1, &po_d->skip[q]};
+			save_d, nfail_d, 1, 1,
+			gcm ? &po_d->fail : &po_d->skip[q]};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, q, prot, stream);
 	}

@@ -1,0 +1,50 @@
+"""Multi-GPU sharding of one SRTP stream (BASELINE config 5).
+
+Packets are independent once their index is known, so a stream of
+world * n packets with monotone seq = (s0 + i) mod 2^16 shards into
+contiguous ranges, one per rank, with no data collective: rank r starts
+from the stream state the sequential reference would hold after packets
+0 .. r*n-1 (src/srtp/srtp.c:203-213, 279-280 sender; 310-321, 426-427
+receiver; src/srtp/replay.c:32-62 window), handed to its contexts with
+srtp_stream_import().  RCCL (or gloo on CPU) only reduces the counters.
+"""
+
+
+def shard_state(rank, per_rank, s0, ssrc, receiver, state_cls=None):
+    """Stream state after a sequential sender (receiver) processed packets
+    0 .. rank*per_rank-1 with seq = (s0 + i) mod 2^16, starting from a
+    fresh stream.  Returns a StreamState (re_amd.srtp) or a dict."""
+    k = rank * per_rank
+    st = {"ssrc": ssrc, "roc": 0, "s_l": 0, "s_l_set": 0,
+          "replay_rtp_lix": 0, "replay_rtp_bitmap": 0}
+    if k:
+        last = s0 + k - 1            # 48-bit index of the last packet
+        st["roc"] = last >> 16
+        st["s_l"] = last & 0xffff
+        st["s_l_set"] = 1
+        if receiver:
+            st["replay_rtp_lix"] = last
+            st["replay_rtp_bitmap"] = (1 << 64) - 1 if k >= 64 else \
+                (1 << k) - 1
+    if state_cls is None:
+        return st
+    o = state_cls()
+    for f, v in st.items():
+        setattr(o, f, v)
+    return o
+
+
+def shard_seq0(rank, per_rank, s0):
+    """first sequence number of rank's shard"""
+    return (s0 + rank * per_rank) & 0xffff
+
+
+def reduce_results(dist, counters, elapsed):
+    """whole-job counters (sum over ranks) and step time (max over ranks)
+    -- the only collectives of the sharded run.  counters / elapsed are
+    torch tensors on the rank's device (float64)."""
+    if dist is not None and dist.is_initialized() and \
+            dist.get_world_size() > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return counters, elapsed

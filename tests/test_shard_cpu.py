@@ -1,0 +1,125 @@
+"""CPU coverage of the multi-GPU path (bench.py --gpus N, BASELINE config 5).
+
+The sharded run hands each rank the stream state the sequential reference
+would hold at its shard boundary (re_amd/shard.py) and reduces only the
+counters.  Checked here against an exact sequential model of the
+sender/receiver state machine (src/srtp/srtp.c:203-213, 279-280,
+310-321, 426-427; misc.c:22-41; replay.c:32-62), single-process and in
+a world_size-2 gloo group.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from re_amd import shard as S
+
+
+def get_index(roc, s_l, seq):
+    # misc.c:22-41, with the int wrap of roc - 1
+    if s_l < 32768:
+        v = roc - 1 if seq - s_l > 32768 else roc
+    else:
+        v = roc + 1 if s_l - 32768 > seq else roc
+    v = (v + 2**31) % 2**32 - 2**31          # (int32_t)
+    return (seq + v * 65536) % 2**64
+
+
+def replay_check(r, ix):
+    if ix > r["lix"]:
+        d = ix - r["lix"]
+        r["bitmap"] = ((r["bitmap"] << d) | 1) % 2**64 if d < 64 else 1
+        r["lix"] = ix
+        return True
+    d = r["lix"] - ix
+    if d >= 64 or r["bitmap"] & (1 << d):
+        return False
+    r["bitmap"] |= 1 << d
+    return True
+
+
+def model(seqs, receiver):
+    """sequential state after the packets (all authentic)"""
+    st = {"roc": 0, "s_l": 0, "s_l_set": 0}
+    rp = {"lix": 0, "bitmap": 0}
+    for seq in seqs:
+        if not st["s_l_set"]:
+            st["s_l"], st["s_l_set"] = seq, 1
+        diff = seq - st["s_l"]
+        if receiver and diff > 32768:
+            continue                              # ETIMEDOUT
+        if diff <= -32768:
+            st["roc"] = (st["roc"] + 1) % 2**32
+            st["s_l"] = 0
+        if receiver:
+            ix = get_index(st["roc"], st["s_l"], seq)
+            if not replay_check(rp, ix):
+                continue                          # EALREADY
+        if seq > st["s_l"]:
+            st["s_l"] = seq
+    if receiver:
+        st["replay_rtp_lix"] = rp["lix"]
+        st["replay_rtp_bitmap"] = rp["bitmap"]
+    return st
+
+
+def check_rank(rank, per_rank, s0):
+    seqs = [(s0 + i) & 0xffff for i in range(rank * per_rank)]
+    for receiver in (False, True):
+        got = S.shard_state(rank, per_rank, s0, 0x0102, receiver)
+        want = model(seqs, receiver)
+        for k, v in want.items():
+            assert got[k] == v, (rank, per_rank, s0, receiver, k, got[k], v)
+    assert S.shard_seq0(rank, per_rank, s0) == (s0 + rank * per_rank) & 0xffff
+
+
+@pytest.mark.parametrize("s0", [0, 65000, 65535])
+@pytest.mark.parametrize("per_rank", [1, 63, 64, 1000, 70000])
+def test_shard_state_matches_sequential_model(s0, per_rank):
+    for rank in (0, 1, 3):
+        check_rank(rank, per_rank, s0)
+
+
+def _worker(rank, world, port, per_rank, s0, q):
+    try:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" %
+                                port, rank=rank, world_size=world)
+        check_rank(rank, per_rank, s0)
+        counters = torch.tensor([per_rank, per_rank * 1200.0, 0.0],
+                                dtype=torch.float64)
+        t = torch.tensor([0.5 + rank], dtype=torch.float64)
+        S.reduce_results(dist, counters, t)
+        assert counters.tolist() == [world * per_rank,
+                                     world * per_rank * 1200.0, 0.0]
+        assert t.item() == 0.5 + (world - 1)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("per_rank,s0", [(70000, 65000), (1000, 0)])
+def test_gloo_world2_shards_and_reduction(per_rank, s0):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, per_rank, s0, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

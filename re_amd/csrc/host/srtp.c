@@ -67,9 +67,10 @@ struct comp {
 };
 
 struct srtp {
-	struct comp rtp, rtcp;
+	unsigned nstreams;      /* next to streams[0]: one cache line for
+				   the common one-stream session */
 	struct srtp_stream streams[SRTP_MAX_STREAMS];
-	unsigned nstreams;
+	struct comp rtp, rtcp;
 	uint32_t slot;
 	int dev;
 };
@@ -972,6 +973,18 @@ struct pool {
 	size_t cap;
 };
 
+struct ulog {
+	struct srtp *s;                 /* session entry: old nstreams */
+	struct srtp_stream *st;         /* stream entry: old state */
+	unsigned nstreams;
+	struct srtp_stream old;
+};
+
+struct ulogv {
+	struct ulog *v;
+	size_t n, cap;
+};
+
 struct ws {
 	void *stream;
 	struct pool ctl;        /* jobs | verdict | save */
@@ -990,16 +1003,10 @@ struct ws {
 	struct pool es;         /* device API: original ends */
 	void **ev;              /* per-chunk parse events */
 	size_t nev;
-	struct ulog *ulog;      /* stream-state undo log */
-	size_t nulog, ulog_cap;
+	struct ulogv ulog[1];   /* stream-state undo log */
 };
 
-struct ulog {
-	struct srtp *s;                 /* session entry: old nstreams */
-	struct srtp_stream *st;         /* stream entry: old state */
-	unsigned nstreams;
-	struct srtp_stream old;
-};
+
 
 static __thread struct ws *t_ws;
 
@@ -1605,18 +1612,18 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 static uint32_t g_epoch;
 static __thread int t_noplan;   /* fallback of a rejected device plan */
 
-static int ulog_push(struct ws *w, struct srtp *s, struct srtp_stream *st)
+static int ulog_push(struct ulogv *L, struct srtp *s, struct srtp_stream *st)
 {
 	struct ulog *u;
-	if (w->nulog == w->ulog_cap) {
-		size_t nc = w->ulog_cap ? 2 * w->ulog_cap : 256;
-		struct ulog *nu = realloc(w->ulog, nc * sizeof(*nu));
+	if (L->n == L->cap) {
+		size_t nc = L->cap ? 2 * L->cap : 256;
+		struct ulog *nu = realloc(L->v, nc * sizeof(*nu));
 		if (!nu)
 			return ENOMEM;
-		w->ulog = nu;
-		w->ulog_cap = nc;
+		L->v = nu;
+		L->cap = nc;
 	}
-	u = &w->ulog[w->nulog++];
+	u = &L->v[L->n++];
 	u->s = s;
 	u->st = st;
 	if (s)
@@ -1626,10 +1633,10 @@ static int ulog_push(struct ws *w, struct srtp *s, struct srtp_stream *st)
 	return 0;
 }
 
-static void ulog_undo(struct ws *w)
+static void ulog_undo(struct ulogv *L)
 {
-	while (w->nulog) {
-		struct ulog *u = &w->ulog[--w->nulog];
+	while (L->n) {
+		struct ulog *u = &L->v[--L->n];
 		if (u->st)
 			*u->st = u->old;
 		else
@@ -1638,7 +1645,7 @@ static void ulog_undo(struct ws *w)
 }
 
 /* stream_get (stream.c:29-84) with an undo log entry on first touch */
-static int fs_stream(struct ws *w, struct srtp *s, uint32_t ssrc,
+static int fs_stream(struct ulogv *w, struct srtp *s, uint32_t ssrc,
 		     uint32_t epoch, int log, struct srtp_stream **sp)
 {
 	unsigned i;
@@ -1666,7 +1673,7 @@ static int fs_stream(struct ws *w, struct srtp *s, uint32_t ssrc,
 }
 
 struct fscan {
-	struct ws *w;
+	struct ulogv *log_v;            /* stream-state undo log */
 	struct srtp **sessv;
 	const uint32_t *sidx;
 	const struct sgpu_hdr *hd;     /* pinned */
@@ -1702,7 +1709,7 @@ static inline struct srtp_stream *fs_get(struct fscan *F, struct srtp *s,
 	fs_flush(F);
 	F->lst = NULL;
 	F->ls = NULL;
-	*err = fs_stream(F->w, s, ssrc, F->epoch, F->log, &st);
+	*err = fs_stream(F->log_v, s, ssrc, F->epoch, F->log, &st);
 	if (*err) {
 		if (*err == ENOMEM)
 			F->nomem = 1;
@@ -1722,6 +1729,8 @@ static inline void fs_none(struct fscan *F, size_t i, int err, uint32_t pos)
 	F->pos[i] = pos;
 }
 
+#define PF_DIST 24
+
 /* srtp_encrypt (srtp.c:183-285) over packets [a, b); per-class counts */
 static void scan_enc(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 {
@@ -1736,6 +1745,10 @@ static void scan_enc(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 	const uint32_t *__restrict sidx = F->sidx;
 	size_t i;
 	for (i = a; i < b; i++) {
+		/* many sessions: their states are scattered; prefetch the
+		 * one PF_DIST packets ahead */
+		if (sidx && i + PF_DIST < b)
+			__builtin_prefetch(F->sessv[sidx[i + PF_DIST]], 1, 1);
 		struct srtp *s = F->sessv[sidx ? sidx[i] : 0];
 		const struct sgpu_hdr h = hd[i];
 		const uint32_t start = pos[i], end = endv[i];
@@ -1786,6 +1799,10 @@ static void scan_dec(struct fscan *F, size_t a, size_t b, uint32_t cnt[4])
 	const uint32_t *__restrict sidx = F->sidx;
 	size_t i;
 	for (i = a; i < b; i++) {
+		/* many sessions: their states are scattered; prefetch the
+		 * one PF_DIST packets ahead */
+		if (sidx && i + PF_DIST < b)
+			__builtin_prefetch(F->sessv[sidx[i + PF_DIST]], 1, 1);
 		struct srtp *s = F->sessv[sidx ? sidx[i] : 0];
 		const struct sgpu_hdr h = hd[i];
 		const uint32_t start = pos[i], end = endv[i];
@@ -1948,7 +1965,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	const size_t nch = (n + CH - 1) / CH;
 	const struct comp *c0 = &sessv[0]->rtp;
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
-	struct fscan F;
+	struct fscan FT[1];
 	struct flaunch *fl = NULL;
 	size_t nfl = 0, i, k;
 	uint32_t *up_h, *up_d, *cm_h;
@@ -2195,21 +2212,21 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	/* 2. sequential scan per chunk, crypto launched behind it */
 	if (trace)
 		t1 = now_ms();
-	memset(&F, 0, sizeof(F));
-	F.w = w;
-	F.sessv = sessv;
-	F.sidx = b->sess;
-	F.hd = (const struct sgpu_hdr *)w->hd.h;
-	F.desc = (uint64_t *)w->dsc.h;
-	F.pos = b->pos;
-	F.end = b->end;
-	F.cap = b->cap;
-	F.err = b->err;
-	F.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
-	F.log = !prot;
-	F.mode = c0->mode;
-	F.tag_len = c0->tag_len;
-	w->nulog = 0;
+	memset(FT, 0, sizeof(FT));
+	FT[0].sessv = sessv;
+	FT[0].sidx = b->sess;
+	FT[0].hd = (const struct sgpu_hdr *)w->hd.h;
+	FT[0].desc = (uint64_t *)w->dsc.h;
+	FT[0].pos = b->pos;
+	FT[0].end = b->end;
+	FT[0].cap = b->cap;
+	FT[0].err = b->err;
+	FT[0].epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
+	FT[0].log = !prot;
+	FT[0].mode = c0->mode;
+	FT[0].tag_len = c0->tag_len;
+	FT[0].log_v = &w->ulog[0];
+	w->ulog[0].n = 0;
 	for (k = 0; k < nch && !err; k++) {
 		const size_t a = k * CH, e = a + CH < n ? a + CH : n;
 		uint32_t cnt[4] = {0, 0, 0, 0}, nz = 0, sh = 0, q;
@@ -2220,23 +2237,23 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		if (trace)
 			tb = now_ms();
 		if (prot)
-			scan_enc(&F, a, e, cnt);
+			scan_enc(&FT[0], a, e, cnt);
 		else
-			scan_dec(&F, a, e, cnt);
+			scan_dec(&FT[0], a, e, cnt);
+		if (FT[0].nomem)
+			err = ENOMEM;
 		if (trace) {
 			twait += tb - ta;
 			tscan += now_ms() - tb;
 		}
-		if (F.nomem) {
-			err = ENOMEM;
+		if (err)
 			break;
-		}
 		for (q = 0; q < 4; q++)
 			if (cnt[q]) {
 				nz++;
 				sh = q;
 			}
-		err = sgpu_memcpy_h2d(desc_d + a, F.desc + a, (e - a) * 8,
+		err = sgpu_memcpy_h2d(desc_d + a, FT[0].desc + a, (e - a) * 8,
 				      stream);
 		if (err || !nz)
 			continue;
@@ -2252,9 +2269,9 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				o += cnt[q];
 			}
 			for (i = a; i < e; i++)
-				if (F.desc[i])
-					idx_h[st[(F.hd[i].hdr_len >> 2) & 3]++] =
-						(uint32_t)i;
+				if (FT[0].desc[i])
+					idx_h[st[(FT[0].hd[i].hdr_len >> 2) & 3]++]
+						= (uint32_t)i;
 			o = (uint32_t)a;
 			for (q = 0; q < 4; q++) {
 				if (cnt[q])
@@ -2318,14 +2335,13 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			goto out;
 		if (planned)
 			plan_unapply(ps, ps_n, &ps_old);
-		ulog_undo(w);
+		ulog_undo(&w->ulog[0]);
 		memcpy(b->pos, up_h, n * 4);
 		memcpy(b->end, up_h + n, n * 4);
 		free(fl);
 		return run_batch_general(op, sessv, nsess, b);
 	}
  out:
-	w->nulog = 0;
 	free(fl);
 	return err;
 }

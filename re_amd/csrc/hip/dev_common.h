@@ -197,10 +197,15 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16])
 }
 
 /* ---- GHASH: Z = (X) * H with the 4-bit table at tab (LDS or global) ---- */
-/* X given as 4 big-endian words x0..x3 (x0 = bytes 0..3).  rem4 in LDS. */
+/* X given as 4 big-endian words x0..x3 (x0 = bytes 0..3).  rem4 in LDS.
+ * Entry i*H lives at tab + i * stride + laneoff: stride 16 / laneoff 0 for
+ * a plain table; stride 256 / laneoff (lane & 15) * 16 for the 16x
+ * replicated LDS image, where each 16-lane group of a ds_read_b128 hits
+ * 16 distinct bank quads whatever the nibbles (conflict-free). */
 __device__ __forceinline__ void ghash_mul(uint32_t &x0, uint32_t &x1,
 					  uint32_t &x2, uint32_t &x3,
-					  const uint8_t *tab,
+					  const uint8_t *tab, uint32_t stride,
+					  uint32_t laneoff,
 					  const uint32_t *rem4)
 {
 	uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
@@ -218,9 +223,10 @@ __device__ __forceinline__ void ghash_mul(uint32_t &x0, uint32_t &x1,
 			z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
 			z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
 			z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
-			z0 = (z0 >> 4) ^ rem4[rem];
-			const uint4 t = *(const uint4 *)(tab + nib * 16u);
-			z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+			const uint4 t = *(const uint4 *)(tab + nib * stride +
+							 laneoff);
+			z0 = xor3(z0 >> 4, rem4[rem], t.x);
+			z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
 		}
 	}
 	x0 = z0; x1 = z1; x2 = z2; x3 = z3;

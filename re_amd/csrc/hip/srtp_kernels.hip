@@ -721,7 +721,7 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 {
 	if (!njobs)
 		return 0;
-	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(false, nr, prot)
+	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(false, false, nr, prot)
 		  : nr == 10 ? sgpu_pick_ctr10(false, false, shift, prot)
 			     : sgpu_pick_ctr14(false, false, shift, prot);
 	if (!f) {
@@ -750,7 +750,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 {
 	if (!c->n)
 		return 0;
-	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(true, nr, prot)
+	kfn_t f = mode == SGPU_MODE_GCM ?
+			  sgpu_pick_gcm(true, c->uniform != 0, nr, prot)
 		  : nr == 10 ? sgpu_pick_ctr10(true, c->uniform != 0, shift, prot)
 			     : sgpu_pick_ctr14(true, c->uniform != 0, shift, prot);
 	if (!f) {
@@ -770,7 +771,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 	return launch(f, a, c->n,
 		      c->undo ? -1 : prof_slot(mode, nr, shift, prot),
 		      (hipStream_t)stream,
-		      mode == SGPU_MODE_GCM ? KBLOCK
+		      mode == SGPU_MODE_GCM ? sgpu_gcm_block(c->uniform != 0)
 					    : sgpu_ctr_block(c->uniform != 0, prot));
 }
 

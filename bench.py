@@ -199,7 +199,11 @@ def main():
         for s in tx + rx:
             s.close()
     torch.cuda.synchronize()
-    sess_sets = [make_sessions() for _ in range(args.steps)]
+    # the C session pointer arrays are built once per set (not timed);
+    # the Srtp handles stay alive until the end (they own the sessions)
+    sess_objs = [make_sessions() for _ in range(args.steps)]
+    sess_sets = [(P.session_array(tx), P.session_array(rx))
+                 for tx, rx in sess_objs]
     P.prof_enable(True)
     P.prof_read()
     if world > 1:
@@ -236,8 +240,8 @@ def main():
         verified = bool(torch.equal(a2[win], p2[win])) and tot_err == 0
         del win, a2, p2
 
-    for ss in sess_sets:
-        for s in ss[0] + ss[1]:
+    for tx, rx in sess_objs:
+        for s in tx + rx:
             s.close()
 
     if rank != 0:
@@ -258,9 +262,17 @@ def main():
                      "gbs": nbytes / (avg_ms * 1e-3) / 1e9})
     kern.sort(key=lambda d: -d["avg_ms"] * d["launches"])
     dom = kern[0] if kern else None
+    # HBM bytes per launch of the same kernel, from the committed PMC
+    # passes of this configuration (scripts/gpu_pmc.sh, pmc_summary.py);
+    # scaled if this run's launches carry a different packet count
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get("bytes_per_launch")
+    tj = args.traffic_json or os.path.join(ROOT, "profiles",
+                                           "r01_pmc_traffic.json")
+    if dom and os.path.exists(tj):
+        ent = json.load(open(tj)).get("config%d" % cfg_id, {}).get(dom["dir"])
+        if ent:
+            traffic = round(ent["traffic_bytes_per_launch"] *
+                            dom["pkts_per_launch"] / ent["grid"])
     roof = None
     if dom:
         roof = {"bound": "hbm", "achieved": round(dom["gbs"], 2),

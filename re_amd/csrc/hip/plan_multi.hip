@@ -1,0 +1,394 @@
+/*
+ * plan_multi.hip -- device planning of multi-session RTP batches.
+ *
+ * The host's sequential state machine (srtp_encrypt srtp.c:203-213,
+ * 279-280; srtp_decrypt srtp.c:310-321, 426-427; srtp_get_index
+ * misc.c:22-41; srtp_replay_check replay.c:32-62) runs per stream, and
+ * streams of different sessions are independent.  Here:
+ *   1. packets are stably sorted by session (hipCUB LSD radix sort of the
+ *      session index, values = packet index), so each session's packets
+ *      form one segment in array order;
+ *   2. inside a segment packet k is assumed to see s_l = seq of packet
+ *      k-1 (the session's stored s_l for the first), ROC rollovers are
+ *      prefix-summed, and every assumption is verified exactly as in the
+ *      single-stream planner (srtp_kernels.hip k_plan_*);
+ *   3. each touched session's final stream state is written out.
+ * Any verification miss sets out->fail: the host then plans sequentially
+ * and nothing launched behind the plan (guarded on out->skip[]) runs.
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <errno.h>
+#include <stdio.h>
+#include "../srtpgpu.h"
+
+#define MP_BLOCK 256
+
+__device__ __forceinline__ uint64_t mp_desc(uint64_t ix, uint32_t flags)
+{
+	return (ix & 0xffffull) | ((uint64_t)(uint32_t)(ix >> 16) << 16) |
+	       ((uint64_t)flags << 48);
+}
+
+/* misc.c:22-41, including the int wrap of roc +- 1 */
+__device__ __forceinline__ int32_t mp_v(uint32_t roc, uint32_t s_l,
+					uint32_t seq)
+{
+	if (s_l < 32768)
+		return ((int)seq - (int)s_l > 32768) ? (int32_t)(roc - 1)
+						     : (int32_t)roc;
+	return ((int)s_l - 32768 > (int)seq) ? (int32_t)(roc + 1)
+					     : (int32_t)roc;
+}
+
+__device__ __forceinline__ bool mp_wrap(uint32_t seq, uint32_t sb)
+{
+	return (int)seq - (int)sb <= -32768;
+}
+
+struct mp_ctx {
+	const uint32_t *key;            /* sorted session index */
+	const uint32_t *val;            /* sorted packet index */
+	const struct sgpu_hdr *hdr;
+	const struct sgpu_sstate *st;
+	uint32_t n;
+};
+
+/* s_l seen by sorted position k of the segment starting at f */
+__device__ __forceinline__ uint32_t mp_sb(const mp_ctx &c, uint32_t k,
+					  uint32_t f)
+{
+	if (k == f) {
+		const struct sgpu_sstate &S = c.st[c.key[k]];
+		return (S.flags & SST_SL_SET) ? S.s_l : c.hdr[c.val[k]].seq;
+	}
+	return c.hdr[c.val[k - 1]].seq;
+}
+
+__device__ __forceinline__ bool mp_first(const mp_ctx &c, uint32_t k)
+{
+	return k == 0 || c.key[k - 1] != c.key[k];
+}
+
+__global__ void k_mp_iota(uint32_t *v, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (i < n)
+		v[i] = i;
+}
+
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
+	   const uint32_t *end, const uint32_t *cap, uint64_t asz,
+	   uint32_t *bcnt, struct sgpu_plan_out *out)
+{
+	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	bool wrap = false;
+	uint32_t f = 0;
+	if (k < in.n) {
+		const uint32_t i = c.val[k], s = c.key[k];
+		const bool first = mp_first(c, k);
+		const bool last = k + 1 == in.n || c.key[k + 1] != s;
+		const struct sgpu_hdr h = c.hdr[i];
+		const uint32_t hl0 = c.hdr[0].hdr_len;
+		const struct sgpu_sstate S = c.st[s];
+		const uint32_t seq = h.seq;
+		const uint32_t sb = first ? ((S.flags & SST_SL_SET) ? S.s_l : seq)
+					  : c.hdr[c.val[k - 1]].seq;
+		if (s >= in.nsess)
+			f |= SPF_BAD;
+		if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (((h.hdr_len ^ hl0) >> 2) & 3u)
+			f |= SPF_CLASS;
+		/* one SSRC per session: the stored one, or the segment's */
+		if (first ? ((S.flags & SST_EXISTS) && h.ssrc != S.ssrc)
+			  : h.ssrc != c.hdr[c.val[k - 1]].ssrc)
+			f |= SPF_SSRC;
+		if (!in.prot && h.hdr_len != 0xffffffffu &&
+		    end[i] - pos[i] - h.hdr_len < in.tag)
+			f |= SPF_PARSE;
+		if (!in.prot && (int)seq - (int)sb > 32768)
+			f |= SPF_TIMEOUT;
+		if (end[i] - pos[i] >= (1u << 20) - 64u)
+			f |= SPF_SIZE;
+		if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
+		    (cap && (end[i] > cap[i] || cap[i] > asz)))
+			f |= SPF_BAD;
+		if (in.prot && cap &&
+		    (uint64_t)end[i] + in.need > (uint64_t)cap[i])
+			f |= SPF_CAP;
+		wrap = mp_wrap(seq, sb);
+		if (!last && !wrap && seq < sb)
+			f |= SPF_ORDER;
+		if (k == 0)
+			out->hl0 = hl0;
+		if (f)
+			atomicOr(&out->fail, f);
+	}
+	const int cnt = __syncthreads_count(wrap);
+	if (threadIdx.x == 0)
+		bcnt[blockIdx.x] = (uint32_t)cnt;
+}
+
+/* exclusive scan of the per-block wrap counts (one workgroup) */
+__global__ void __launch_bounds__(1024)
+k_mp_scan(uint32_t *bcnt, uint32_t nb)
+{
+	__shared__ uint32_t part[1024];
+	const uint32_t per = (nb + 1023u) / 1024u;
+	const uint32_t a = threadIdx.x * per;
+	uint32_t sum = 0;
+	for (uint32_t k = a; k < a + per && k < nb; k++)
+		sum += bcnt[k];
+	part[threadIdx.x] = sum;
+	__syncthreads();
+	for (uint32_t d = 1; d < 1024; d <<= 1) {
+		uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+		__syncthreads();
+		part[threadIdx.x] += v;
+		__syncthreads();
+	}
+	uint32_t run = part[threadIdx.x] - sum;
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
+		const uint32_t v = bcnt[k];
+		bcnt[k] = run;
+		run += v;
+	}
+}
+
+/* per position: exclusive wrap prefix; per session: segment bounds */
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mp_mark(mp_ctx c, const uint32_t *bpre, uint32_t *pex, uint32_t *segf,
+	  uint32_t *segl)
+{
+	__shared__ uint32_t wsum[MP_BLOCK / 64];
+	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	bool wrap = false, first = false, last = false;
+	if (k < c.n) {
+		first = mp_first(c, k);
+		last = k + 1 == c.n || c.key[k + 1] != c.key[k];
+		/* the segment start is only needed for k == f */
+		const uint32_t sb = first ? mp_sb(c, k, k)
+					  : c.hdr[c.val[k - 1]].seq;
+		wrap = mp_wrap(c.hdr[c.val[k]].seq, sb);
+	}
+	const uint64_t m = __ballot(wrap);
+	if (lane == 0)
+		wsum[wv] = (uint32_t)__popcll(m);
+	__syncthreads();
+	uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+	for (uint32_t q = 0; q < wv; q++)
+		pre += wsum[q];
+	if (k >= c.n)
+		return;
+	pex[k] = bpre[blockIdx.x] + pre;
+	if (first)
+		segf[c.key[k]] = k;
+	if (last)
+		segl[c.key[k]] = k;
+}
+
+/* exact index of sorted position k (segment start f) */
+__device__ __forceinline__ uint64_t mp_ix(const mp_ctx &c,
+					  const struct sgpu_mplan_in &in,
+					  const uint32_t *pex, uint32_t k,
+					  uint32_t f, uint32_t *flp,
+					  uint32_t *rocp, bool *wrapp,
+					  uint32_t *sbp)
+{
+	const struct sgpu_sstate &S = c.st[c.key[k]];
+	const uint32_t seq = c.hdr[c.val[k]].seq;
+	const uint32_t sb = mp_sb(c, k, f);
+	const bool wrap = mp_wrap(seq, sb);
+	const uint32_t fseq = c.hdr[c.val[f]].seq;
+	const bool wf = mp_wrap(fseq, mp_sb(c, f, f));
+	/* ROC after this packet's own rollover */
+	const uint32_t roc = S.roc + (pex[k] + (wrap ? 1u : 0u)) -
+			     (pex[f] + (wf ? 1u : 0u)) + (wf ? 1u : 0u);
+	uint64_t ix;
+	uint32_t fl = SD_RUN | SD_CIPHER;
+	if (in.prot) {
+		ix = 65536ull * roc + seq;                   /* srtp.c:215 */
+	}
+	else {
+		const int32_t v = mp_v(roc, wrap ? 0u : sb, seq);
+		ix = seq + (uint64_t)(int64_t)v * 65536ull;
+		if ((uint32_t)v != roc)
+			fl |= (uint32_t)v + 1u == roc ? SD_ROC_P1 : SD_ROC_M1;
+	}
+	if (flp)
+		*flp = fl;
+	if (rocp)
+		*rocp = roc;
+	if (wrapp)
+		*wrapp = wrap;
+	if (sbp)
+		*sbp = sb;
+	return ix;
+}
+
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mp_desc(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
+	  const uint32_t *segf, uint64_t *desc, struct sgpu_plan_out *out)
+{
+	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (k >= c.n)
+		return;
+	const uint32_t s = c.key[k], f = segf[s];
+	uint32_t fl;
+	const uint64_t ix = mp_ix(c, in, pex, k, f, &fl, NULL, NULL, NULL);
+	if (!in.prot) {
+		/* replay: every packet new (replay.c:32-62) */
+		bool ok;
+		if (k == f) {
+			const struct sgpu_sstate &S = c.st[s];
+			if (ix > S.lix)
+				ok = true;
+			else {
+				const uint64_t d = S.lix - ix;
+				ok = d < 64 && !(S.bitmap & (1ull << d));
+			}
+		}
+		else {
+			ok = ix > mp_ix(c, in, pex, k - 1, f, NULL, NULL, NULL,
+					NULL);
+		}
+		if (!ok)
+			atomicOr(&out->fail, (uint32_t)SPF_REPLAY);
+	}
+	desc[c.val[k]] = mp_desc(ix, fl);
+}
+
+/* final state of every touched session; launch guards */
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mp_final(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
+	   const uint32_t *segf, const uint32_t *segl,
+	   struct sgpu_sstate *st_out, struct sgpu_plan_out *out)
+{
+	const uint32_t s = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (s == 0)
+		for (int q = 0; q < 4; q++)
+			out->skip[q] = out->fail ||
+				       (((out->hl0 >> 2) & 3u) != (uint32_t)q);
+	if (s >= in.nsess)
+		return;
+	const struct sgpu_sstate S = c.st[s];
+	struct sgpu_sstate o = S;
+	o.flags &= ~SST_TOUCHED;
+	const uint32_t l = segl[s];
+	if (l == 0xffffffffu) {
+		st_out[s] = o;
+		return;
+	}
+	const uint32_t f = segf[s];
+	uint32_t roc, sb;
+	bool wrap;
+	(void)mp_ix(c, in, pex, l, f, NULL, &roc, &wrap, &sb);
+	const uint32_t seq = c.hdr[c.val[l]].seq;
+	o.ssrc = (S.flags & SST_EXISTS) ? S.ssrc : c.hdr[c.val[f]].ssrc;
+	o.roc = roc;
+	o.s_l = wrap ? seq : (seq > sb ? seq : sb);
+	o.flags = SST_EXISTS | SST_SL_SET | SST_TOUCHED;
+	if (!in.prot) {
+		/* replay fold over the last <= 65 indices (older bits have
+		 * shifted out: every index is new and increasing) */
+		uint64_t lix = S.lix, bm = S.bitmap;
+		uint32_t k = f;
+		if (l - f + 1 > 65) {
+			k = l - 64;
+			lix = mp_ix(c, in, pex, k - 1, f, NULL, NULL, NULL,
+				    NULL);
+			bm = 1;
+		}
+		for (; k <= l; k++) {
+			const uint64_t ix = mp_ix(c, in, pex, k, f, NULL, NULL,
+						  NULL, NULL);
+			if (ix > lix) {
+				const uint64_t d = ix - lix;
+				bm = d < 64 ? (bm << d) | 1ull : 1ull;
+				lix = ix;
+			}
+			else {
+				bm |= 1ull << (lix - ix);
+			}
+		}
+		o.lix = lix;
+		o.bitmap = bm;
+	}
+	st_out[s] = o;
+}
+
+/* ---- host side ------------------------------------------------------ */
+
+static size_t mp_align(size_t x)
+{
+	return (x + 255) & ~(size_t)255;
+}
+
+static size_t mp_cub_bytes(uint32_t n, uint32_t bits)
+{
+	size_t tb = 0;
+	(void)hipcub::DeviceRadixSort::SortPairs(
+		(void *)NULL, tb, (const uint32_t *)NULL, (uint32_t *)NULL,
+		(const uint32_t *)NULL, (uint32_t *)NULL, (int)n, 0,
+		(int)bits);
+	return tb;
+}
+
+extern "C" size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess)
+{
+	const uint32_t nb = (n + MP_BLOCK - 1) / MP_BLOCK;
+	return 4 * mp_align((size_t)n * 4) + mp_align((size_t)nb * 4 + 64) +
+	       2 * mp_align((size_t)nsess * 4) + mp_align(mp_cub_bytes(n, 32));
+}
+
+extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
+			      const struct sgpu_hdr *hdr, const uint32_t *pos,
+			      const uint32_t *end, const uint32_t *cap,
+			      uint64_t arena_size, const uint32_t *sess,
+			      const struct sgpu_sstate *st_in,
+			      struct sgpu_sstate *st_out, uint64_t *desc,
+			      void *scratch, size_t scratch_bytes,
+			      struct sgpu_plan_out *out, void *stream)
+{
+	hipStream_t st = (hipStream_t)stream;
+	const uint32_t n = in->n, nb = (n + MP_BLOCK - 1) / MP_BLOCK;
+	uint8_t *p = (uint8_t *)scratch;
+	uint32_t *kout = (uint32_t *)p;  p += mp_align((size_t)n * 4);
+	uint32_t *vin = (uint32_t *)p;   p += mp_align((size_t)n * 4);
+	uint32_t *vout = (uint32_t *)p;  p += mp_align((size_t)n * 4);
+	uint32_t *pex = (uint32_t *)p;   p += mp_align((size_t)n * 4);
+	uint32_t *bcnt = (uint32_t *)p;  p += mp_align((size_t)nb * 4 + 64);
+	uint32_t *segf = (uint32_t *)p;  p += mp_align((size_t)in->nsess * 4);
+	uint32_t *segl = (uint32_t *)p;  p += mp_align((size_t)in->nsess * 4);
+	size_t tb = mp_cub_bytes(n, in->key_bits);
+	if (!n || !in->nsess ||
+	    (size_t)(p - (uint8_t *)scratch) + tb > scratch_bytes)
+		return EINVAL;
+	if (hipMemsetAsync(out, 0, sizeof(*out), st) != hipSuccess ||
+	    hipMemsetAsync(segl, 0xff, (size_t)in->nsess * 4, st) !=
+	    hipSuccess)
+		return EIO;
+	hipLaunchKernelGGL(k_mp_iota, dim3(nb), dim3(MP_BLOCK), 0, st, vin, n);
+	if (hipcub::DeviceRadixSort::SortPairs(p, tb, sess, kout, vin, vout,
+					       (int)n, 0, (int)in->key_bits,
+					       st) != hipSuccess)
+		return EIO;
+	mp_ctx c = {kout, vout, hdr, st_in, n};
+	hipLaunchKernelGGL(k_mp_count, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
+			   pos, end, cap, arena_size, bcnt, out);
+	hipLaunchKernelGGL(k_mp_scan, dim3(1), dim3(1024), 0, st, bcnt, nb);
+	hipLaunchKernelGGL(k_mp_mark, dim3(nb), dim3(MP_BLOCK), 0, st, c,
+			   (const uint32_t *)bcnt, pex, segf, segl);
+	hipLaunchKernelGGL(k_mp_desc, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
+			   (const uint32_t *)pex, (const uint32_t *)segf, desc,
+			   out);
+	hipLaunchKernelGGL(k_mp_final,
+			   dim3((in->nsess + MP_BLOCK - 1) / MP_BLOCK),
+			   dim3(MP_BLOCK), 0, st, *in, c, (const uint32_t *)pex,
+			   (const uint32_t *)segf, (const uint32_t *)segl,
+			   st_out, out);
+	return hipGetLastError() == hipSuccess ? 0 : EIO;
+}

@@ -67,11 +67,13 @@ struct comp {
 };
 
 struct srtp {
-	unsigned nstreams;      /* next to streams[0]: one cache line for
-				   the common one-stream session */
+	/* hot fields first: one cache line with stream 0 covers what the
+	 * batch paths read per session (count, device slot, suite) */
+	unsigned nstreams;
+	uint32_t slot;          /* device session table slot */
+	int suite;              /* enum srtp_suite */
 	struct srtp_stream streams[SRTP_MAX_STREAMS];
 	struct comp rtp, rtcp;
-	uint32_t slot;
 	int dev;
 };
 
@@ -237,6 +239,7 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 			goto out;
 		}
 		s->slot = slots[i];
+		s->suite = (int)suite;
 		s->dev = sgpu_get_device();
 		comp_set(&s->rtp, &p, 1, 2 * slots[i]);
 		comp_set(&s->rtcp, &p, !(flags & SRTP_UNENCRYPTED_SRTCP),
@@ -1001,6 +1004,8 @@ struct ws {
 	struct pool cm;         /* session -> comp index */
 	struct pool pl;         /* device planner: out | scratch */
 	struct pool es;         /* device API: original ends */
+	struct pool ms;         /* multi-session plan: states in | out */
+	struct pool mscr;       /* multi-session plan: device scratch */
 	void **ev;              /* per-chunk parse events */
 	size_t nev;
 	struct ulogv ulog[1];   /* stream-state undo log */
@@ -1953,6 +1958,214 @@ static void plan_unapply(struct srtp *s, unsigned nstreams0,
 	s->nstreams = nstreams0;
 }
 
+/* ---- multi-session device plan ----------------------------------------- */
+
+/* session states in (pinned) -> device; -1 if some session has 2+ streams */
+static int mplan_gather(struct srtp **sessv, size_t nsess,
+			struct sgpu_sstate *st)
+{
+	size_t k;
+	for (k = 0; k < nsess; k++) {
+		const struct srtp *s = sessv[k];
+		if (k + 16 < nsess)
+			__builtin_prefetch(sessv[k + 16], 0, 1);
+		if (s->nstreams > 1)
+			return -1;
+		memset(&st[k], 0, sizeof(st[k]));
+		if (s->nstreams) {
+			const struct srtp_stream *x = &s->streams[0];
+			st[k].ssrc = x->ssrc;
+			st[k].roc = x->roc;
+			st[k].s_l = x->s_l;
+			st[k].flags = SST_EXISTS | (x->s_l_set ? SST_SL_SET : 0);
+			st[k].lix = x->replay_rtp.lix;
+			st[k].bitmap = x->replay_rtp.bitmap;
+		}
+	}
+	return 0;
+}
+
+/* device results -> sessions (touched ones only) */
+static void mplan_apply(struct srtp **sessv, size_t nsess,
+			const struct sgpu_sstate *o, int prot)
+{
+	size_t k;
+	for (k = 0; k < nsess; k++) {
+		struct srtp *s;
+		struct srtp_stream *x;
+		if (k + 16 < nsess && (o[k + 16].flags & SST_TOUCHED))
+			__builtin_prefetch(sessv[k + 16], 1, 1);
+		if (!(o[k].flags & SST_TOUCHED))
+			continue;
+		s = sessv[k];
+		if (!s->nstreams) {
+			memset(&s->streams[0], 0, sizeof(s->streams[0]));
+			s->nstreams = 1;
+		}
+		x = &s->streams[0];
+		x->ssrc = o[k].ssrc;
+		x->roc = o[k].roc;
+		x->s_l = (uint16_t)o[k].s_l;
+		x->s_l_set = 1;
+		if (!prot) {
+			x->replay_rtp.lix = o[k].lix;
+			x->replay_rtp.bitmap = o[k].bitmap;
+		}
+	}
+}
+
+/* undo mplan_apply from the gathered pre-call states */
+static void mplan_unapply(struct srtp **sessv, size_t nsess, struct ws *w)
+{
+	const struct sgpu_sstate *in = (const struct sgpu_sstate *)w->ms.h;
+	const struct sgpu_sstate *o = in + nsess;
+	size_t k;
+	for (k = 0; k < nsess; k++) {
+		struct srtp *s;
+		struct srtp_stream *x;
+		if (!(o[k].flags & SST_TOUCHED))
+			continue;
+		s = sessv[k];
+		if (!(in[k].flags & SST_EXISTS)) {
+			s->nstreams = 0;
+			continue;
+		}
+		x = &s->streams[0];
+		x->roc = in[k].roc;
+		x->s_l = (uint16_t)in[k].s_l;
+		x->s_l_set = (in[k].flags & SST_SL_SET) ? 1 : 0;
+		x->replay_rtp.lix = in[k].lix;
+		x->replay_rtp.bitmap = in[k].bitmap;
+	}
+}
+
+/*
+ * Returns 0 (planned and launched; *nfailp holds the speculation misses,
+ * fl/nfl the launches), an errno, -1 (not eligible: nothing done) or -2
+ * (plan rejected: headers parsed on the device and downloaded to w->hd.h,
+ * windows/sessions staged in w->up, nothing else modified).
+ */
+static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
+			struct srtp_batch *b, struct ws *w, void *stream,
+			const struct comp *c0, uint32_t T,
+			struct flaunch *fl, size_t *nfl, uint32_t *nfailp)
+{
+	const int prot = op == OP_RTP_ENC;
+	const size_t n = b->n;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const int nclass = gcm ? 1 : 4;
+	const uint32_t need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
+	struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
+	struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
+	uint32_t *up_h = (uint32_t *)w->up.h, *up_d = (uint32_t *)w->up.d;
+	struct sgpu_hdr *hd_d = (struct sgpu_hdr *)w->hd.d;
+	uint64_t *desc_d = (uint64_t *)w->dsc.d;
+	uint32_t *nfail_d = (uint32_t *)w->vs.d;
+	uint32_t *save_d = (uint32_t *)(w->vs.d + 64);
+	uint8_t *vd_d = w->vs.d + 64 + n * 4;
+	struct sgpu_sstate *sin_h, *sin_d, *sout_h, *sout_d;
+	struct sgpu_mplan_in in;
+	size_t scr, i;
+	uint32_t bits = 1;
+	int err, capok = 1, q;
+
+	while (bits < 32 && ((size_t)1 << bits) < nsess)
+		bits++;
+	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
+	err = pool_reserve(w, &w->ms, nsess * 2 * sizeof(struct sgpu_sstate));
+	if (!err)
+		err = pool_reserve(w, &w->mscr, scr);
+	if (err)
+		return err;
+	sin_h = (struct sgpu_sstate *)w->ms.h;
+	sin_d = (struct sgpu_sstate *)w->ms.d;
+	sout_h = sin_h + nsess;
+	sout_d = sin_d + nsess;
+	if (mplan_gather(sessv, nsess, sin_h))
+		return -1;
+
+	memset(&in, 0, sizeof(in));
+	in.n = (uint32_t)n;
+	in.nsess = (uint32_t)nsess;
+	in.prot = (uint32_t)prot;
+	in.tag = T;
+	in.need = need;
+	in.key_bits = bits;
+	memcpy(up_h, b->pos, n * 4);
+	memcpy(up_h + n, b->end, n * 4);
+	memcpy(up_h + 2 * n, b->sess, n * 4);
+	err = sgpu_memcpy_h2d(w->cm.d, w->cm.h, nsess * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_h2d(sin_d, sin_h,
+				      nsess * sizeof(struct sgpu_sstate), stream);
+	if (!err && !prot)
+		err = sgpu_memset(nfail_d, 0, 4, stream);
+	if (!err)
+		err = sgpu_memcpy_h2d(up_d, up_h, n * 12, stream);
+	if (!err)
+		err = sgpu_parse_headers(b->arena, b->arena_size, up_d,
+					 up_d + n, hd_d, NULL, (uint32_t)n, 0,
+					 stream);
+	if (!err)
+		err = sgpu_mplan_rtp(&in, hd_d, up_d, up_d + n, NULL,
+				     b->arena_size, up_d + 2 * n, sin_d, sout_d,
+				     desc_d, w->mscr.d, w->mscr.cap, po_d,
+				     stream);
+	if (err)
+		return err;
+	if (prot)
+		for (i = 0; i < n; i++)
+			capok &= (uint64_t)b->end[i] + need <= b->cap[i];
+	for (q = 0; q < nclass && capok && !err; q++) {
+		struct sgpu_compact C = {
+			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 0, 0,
+			gcm ? &po_d->fail : &po_d->skip[q]};
+		err = sgpu_run_compact(b->arena, b->arena_size, &C, c0->mode,
+				       (int)c0->nr, q, prot, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(sout_h, sout_d,
+				      nsess * sizeof(struct sgpu_sstate), stream);
+	if (!err && !prot && capok)
+		err = sgpu_memcpy_d2h(nfailp, nfail_d, 4, stream);
+	if (err)
+		return err;
+	if (capok) {
+		if (prot)
+			for (i = 0; i < n; i++)
+				b->end[i] += T;
+		else
+			for (i = 0; i < n; i++)
+				b->end[i] -= T;
+		memset(b->err, 0, n * sizeof(*b->err));
+	}
+	err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	if (getenv("RE_SRTP_TRACE"))
+		fprintf(stderr, "re_srtp mplan %s n=%zu nsess=%zu: fail 0x%x "
+			"cap %d\n", prot ? "enc" : "dec", n, nsess, po->fail,
+			capok);
+	if (!po->fail && capok) {
+		mplan_apply(sessv, nsess, sout_h, prot);
+		for (q = 0; q < nclass; q++)
+			fl[(*nfl)++] = (struct flaunch){0, (uint32_t)n,
+							(uint32_t)q, 0};
+		return 0;
+	}
+	if (capok)
+		memcpy(b->end, up_h + n, n * 4);
+	*nfailp = 0;
+	err = sgpu_memcpy_d2h(w->hd.h, hd_d, n * sizeof(*hd_d), stream);
+	if (!err && !prot)
+		err = sgpu_memset(nfail_d, 0, 4, stream);
+	return err ? err : -2;
+}
+
 /*
  * Returns 0 / errno like run_batch, or -1 when the batch is not eligible
  * (nothing touched: caller runs the general engine).
@@ -1987,10 +2200,11 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 
 	if (n == 0)
 		return -1;
+	/* RTP contexts derive from the suite alone (srtp.c:101-153) */
 	for (k = 0; k < nsess; k++) {
-		const struct comp *c = &sessv[k]->rtp;
-		if (c->mode != c0->mode || c->nr != c0->nr ||
-		    c->tag_len != c0->tag_len)
+		if (k + 16 < nsess)
+			__builtin_prefetch(sessv[k + 16], 0, 1);
+		if (sessv[k]->suite != sessv[0]->suite)
 			return -1;
 	}
 	w = ws_get();
@@ -2045,8 +2259,32 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	vd_d = w->vs.d + 64 + n * 4;
 	cm_h = (uint32_t *)w->cm.h;
 	for (k = 0; k < nsess; k++)
-		cm_h[k] = sessv[k]->rtp.dev;
+		cm_h[k] = 2u * sessv[k]->slot;          /* comp[0] = RTP */
 
+
+	/* 0b. many sessions, at most one stream each: plan on the device
+	 *     (stable sort by session + per-session speculation); host work
+	 *     is O(sessions): gather the states, apply the results. */
+	if (b->sess && nsess > 1 && !t_noplan && !getenv("RE_SRTP_NOPLAN")) {
+		int r = run_mplanned(op, sessv, nsess, b, w, stream, c0, T, fl,
+				     &nfl, &nfail);
+		if (r == 0) {
+			planned = 2;
+			if (trace)
+				t1 = t2 = now_ms();
+			goto checked;
+		}
+		if (r > 0) {
+			err = r;
+			goto out;
+		}
+		if (r == -2) {
+			/* plan rejected after parsing: headers are on the
+			 * device (and host), the scan path takes over */
+			parsed = 1;
+			pst = stream;
+		}
+	}
 
 	/* 0. one stream: plan on the device (speculative scan, verified).
 	 *    Everything is queued on one stream with a single sync: the
@@ -2325,6 +2563,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				&((struct sgpu_plan_out *)w->pl.d)->fail :
 				&((struct sgpu_plan_out *)w->pl.d)->
 					  skip[fl[k].shift]};
+			C.uniform = planned != 2 && nsess == 1;
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[k].shift, prot, stream);
@@ -2333,8 +2572,10 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			err = sgpu_stream_sync(stream);
 		if (err)
 			goto out;
-		if (planned)
+		if (planned == 1)
 			plan_unapply(ps, ps_n, &ps_old);
+		else if (planned == 2)
+			mplan_unapply(sessv, nsess, w);
 		ulog_undo(&w->ulog[0]);
 		memcpy(b->pos, up_h, n * 4);
 		memcpy(b->end, up_h + n, n * 4);
@@ -2360,14 +2601,11 @@ static int run_batch(int op, struct srtp **sessv, size_t nsess,
 		for (i = 0; i < nsess; i++)
 			if (!sessv[i])
 				return EINVAL;
-		if (b->sess)
-			for (i = 0; i < b->n; i++)
-				if (b->sess[i] >= nsess)
-					return EINVAL;
 		for (i = 0; i < b->n; i++) {
 			if ((b->pos[i] & 3) || b->end[i] > b->cap[i] ||
 			    b->cap[i] > b->arena_size ||
-			    b->pos[i] > b->end[i])
+			    b->pos[i] > b->end[i] ||
+			    (b->sess && b->sess[i] >= nsess))
 				return EINVAL;
 			/* the compact kernels cache the CTR counter block
 			 * for payloads under 1 MiB (kern_common.h CtrKs) */

@@ -216,6 +216,49 @@ int   sgpu_plan_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
 		    uint64_t arena_size, uint64_t *desc, uint32_t *scratch,
 		    struct sgpu_plan_out *out, void *stream);
 
+/*
+ * Multi-session device planning (many sessions with at most one RTP
+ * stream each, e.g. 64K sessions x 1 SSRC): packets are stably sorted by
+ * session on the device, every session's run of packets gets the
+ * single-stream speculation above, and each touched session's final state
+ * is returned (sgpu_sstate), so the host work is O(sessions).
+ */
+enum {
+	SST_EXISTS  = 1u << 0,  /* stream 0 exists */
+	SST_SL_SET  = 1u << 1,  /* s_l set */
+	SST_TOUCHED = 1u << 2,  /* (out) the batch had packets for it */
+};
+
+struct sgpu_sstate {            /* 32 bytes */
+	uint32_t ssrc;
+	uint32_t roc;
+	uint32_t s_l;
+	uint32_t flags;         /* SST_* */
+	uint64_t lix;           /* replay_rtp */
+	uint64_t bitmap;
+};
+
+struct sgpu_mplan_in {
+	uint32_t n;
+	uint32_t nsess;
+	uint32_t prot;
+	uint32_t tag;
+	uint32_t need;
+	uint32_t key_bits;      /* bits of the session index */
+};
+
+/* device scratch needed by sgpu_mplan_rtp */
+size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess);
+
+int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
+		     const struct sgpu_hdr *hdr, const uint32_t *pos,
+		     const uint32_t *end, const uint32_t *cap,
+		     uint64_t arena_size, const uint32_t *sess,
+		     const struct sgpu_sstate *st_in,
+		     struct sgpu_sstate *st_out, uint64_t *desc,
+		     void *scratch, size_t scratch_bytes,
+		     struct sgpu_plan_out *out, void *stream);
+
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */
 int   sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,

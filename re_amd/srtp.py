@@ -276,9 +276,17 @@ def device_batch(opname, sessions, arena_ptr, arena_size, pos, end, cap,
         b.sess = sess_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     b.n = n
     b.stream = stream
-    sv = (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
-    rc = getattr(lib(), opname + "_batch")(sv, len(sessions), ctypes.byref(b))
+    sv = session_array(sessions)
+    rc = getattr(lib(), opname + "_batch")(sv, len(sv), ctypes.byref(b))
     return rc, err
+
+
+def session_array(sessions):
+    """`struct srtp *sessv[]` for the batch calls.  Build it once per
+    session set (O(sessions) Python work) and pass it back in."""
+    if isinstance(sessions, ctypes.Array):
+        return sessions
+    return (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
 
 
 def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
@@ -294,8 +302,8 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
     b.sess = sess_ptr
     b.n = n
     b.stream = stream
-    sv = (ctypes.c_void_p * len(sessions))(*[s.ptr.value for s in sessions])
-    return getattr(lib(), opname + "_batch_dev")(sv, len(sessions),
+    sv = session_array(sessions)
+    return getattr(lib(), opname + "_batch_dev")(sv, len(sv),
                                                  ctypes.byref(b))
 
 

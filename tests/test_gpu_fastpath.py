@@ -409,3 +409,78 @@ def test_device_resident_api(suite, torch_cuda):
         assert (u == v).all()
     for c in [txa, txb, rxa, rxb] + sa + sb:
         c.close()
+
+
+def multi_session_traffic(rng, n, nsess, s0=None, forge=()):
+    """in-order traffic of nsess sessions, one SSRC each, interleaved at
+    random (the multi-session device planner's case)"""
+    nxt = {}
+    out = []
+    for _ in range(n):
+        s = int(rng.integers(0, nsess))
+        seq = nxt.get(s, (s0 if s0 is not None else
+                          int(rng.integers(0, 65536))))
+        nxt[s] = (seq + 1) & 0xffff
+        out.append((s, rtp_packet(rng, seq, 0x7000 + s,
+                                  plen=int(rng.integers(0, 400)))))
+    return out
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_multi_session_device_planner(suite, torch_cuda):
+    """many sessions, one SSRC each: planned on the device (sort by
+    session + per-session speculation); must equal the host scan
+    (RE_SRTP_NOPLAN) and the general engine, across two consecutive
+    batches, with a forged packet forcing undo + exact fold"""
+    torch = torch_cuda
+    rng = np.random.default_rng(55 + suite)
+    nsess = 40
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    batches = [multi_session_traffic(rng, 2500, nsess, s0=65400)]
+    # second batch continues every session (ROC wraps inside)
+    last = {}
+    for s, p in batches[0]:
+        last[s] = int.from_bytes(p[2:4], "big")
+    nb = []
+    for _ in range(2500):
+        s = int(rng.integers(0, nsess))
+        last[s] = (last.get(s, 0) + 1) & 0xffff
+        nb.append((s, rtp_packet(rng, last[s], 0x7000 + s, plen=120)))
+    batches.append(nb)
+    res = {}
+    for mode in ("plan", "noplan", "general"):
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        outs = []
+        for bi, pk in enumerate(batches):
+            arena, pos, end, cap, sess = to_arena(pk)
+            if mode == "noplan":
+                os.environ["RE_SRTP_NOPLAN"] = "1"
+            enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap, sess,
+                      mode == "general")
+            os.environ.pop("RE_SRTP_NOPLAN", None)
+            prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
+                    for i, (s, _) in enumerate(pk)]
+            if bi == 1:
+                q = bytearray(prot[1234][1])
+                q[-3] ^= 0x10
+                prot[1234] = (prot[1234][0], bytes(q))
+            a2, p2, e2, c2, s2 = to_arena(prot)
+            if mode == "noplan":
+                os.environ["RE_SRTP_NOPLAN"] = "1"
+            dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
+                      mode == "general")
+            os.environ.pop("RE_SRTP_NOPLAN", None)
+            outs.append((enc, dec))
+        res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
+        for c in tx + rx:
+            c.close()
+    A = res["plan"]
+    assert int(A[0][1][1][3][1234]) == P.EAUTH
+    for mode in ("noplan", "general"):
+        B = res[mode]
+        for (ea, da), (eb, db) in zip(A[0], B[0]):
+            for x, y in zip(ea + da, eb + db):
+                assert (x == y).all(), mode
+        assert A[1] == B[1] and A[2] == B[2], mode

@@ -97,6 +97,8 @@ def main():
                     help="override packets per GPU (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--same-device", action="store_true",
+                    help="testing only: all ranks on cuda:0, gloo counters")
     ap.add_argument("--host-arrays", action="store_true",
                     help="srtp_*_batch with host pos/end/err arrays instead "
                          "of the device-resident srtp_*_batch_dev")
@@ -117,10 +119,17 @@ def main():
     cfg = dict(CONFIGS[cfg_id])
     if args.packets:
         cfg["n"] = args.packets
-    torch.cuda.set_device(local)
+    # --same-device (testing only): every rank on cuda:0, counters over
+    # gloo -- rehearses the sharded path on a one-GPU box
+    gpu = 0 if args.same_device else local
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if args.same_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl",
+                                    device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu)
     P.load()
 
     n, suite, nsess = cfg["n"], cfg["suite"], cfg["nsess"]

@@ -45,6 +45,12 @@ def reduce_results(dist, counters, elapsed):
     torch tensors on the rank's device (float64)."""
     if dist is not None and dist.is_initialized() and \
             dist.get_world_size() > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        cpu = dist.get_backend() == "gloo" and counters.is_cuda
+        c = counters.cpu() if cpu else counters
+        e = elapsed.cpu() if cpu else elapsed
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        if cpu:
+            counters.copy_(c)
+            elapsed.copy_(e)
     return counters, elapsed

@@ -1112,7 +1112,7 @@ static int undo_job(const struct rec *r, struct sgpu_job *u)
  */
 static int round_launch(struct ws *w, struct engine *E, int sel,
 			uint8_t *arena_d, uint64_t asz, const uint32_t *joff,
-			int prot, uint32_t *pm)
+			int prot, uint32_t *pm, void *stream)
 {
 	uint32_t cnt[16] = {0}, start[17], k, m = 0;
 	size_t i, need = 0;
@@ -1180,7 +1180,7 @@ static int round_launch(struct ws *w, struct engine *E, int sel,
 		w->cls_idx[slot] = (uint32_t)i;
 		m++;
 	}
-	err = sgpu_memcpy_h2d(jd, jh, m * sizeof(struct sgpu_job), w->stream);
+	err = sgpu_memcpy_h2d(jd, jh, m * sizeof(struct sgpu_job), stream);
 	if (err)
 		return err;
 	for (k = 0; k < 16; k++) {
@@ -1190,7 +1190,7 @@ static int round_launch(struct ws *w, struct engine *E, int sel,
 		err = sgpu_run_class(arena_d, asz, jd + a, b - a, vd + a,
 				     (uint32_t *)(vd + m) + a, (k >> 3) & 1,
 				     (k >> 2) & 1 ? 14 : 10, (int)(k & 3),
-				     sel == SEL_RUN ? prot : 0, w->stream);
+				     sel == SEL_RUN ? prot : 0, stream);
 		if (err)
 			return err;
 	}
@@ -1199,13 +1199,13 @@ static int round_launch(struct ws *w, struct engine *E, int sel,
 }
 
 /* D2H of verdicts + saved tag words for the m jobs just launched */
-static int round_fetch(struct ws *w, uint32_t m)
+static int round_fetch(struct ws *w, uint32_t m, void *stream)
 {
 	size_t off = (size_t)m * sizeof(struct sgpu_job);
 	if (!m)
 		return 0;
 	return sgpu_memcpy_d2h(w->ctl.h + off, w->ctl.d + off, (size_t)m * 5,
-			       w->stream);
+			       stream);
 }
 
 static void round_collect(struct ws *w, struct engine *E, uint32_t m)
@@ -1329,10 +1329,10 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 				if (E.rec[i].need_run)
 					E.rec[i].job.off = E.pi[i].start;
 			err = round_launch(w, &E, SEL_RUN, w->stage.d, bytes,
-					   soff, prot, &m);
+					   soff, prot, &m, w->stream);
 		}
 		if (!err)
-			err = round_fetch(w, m);
+			err = round_fetch(w, m, w->stream);
 		if (!err)
 			err = sgpu_memcpy_d2h(w->stage.h, w->stage.d, bytes,
 					      w->stream);
@@ -1460,7 +1460,9 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 		err = ENOMEM;
 		goto out;
 	}
-	stream = b->stream ? b->stream : w->stream;
+	/* the caller's stream; NULL is the default (null) stream, which
+	 * orders this call after the caller's prior default-stream work */
+	stream = b->stream;
 
 	/* 1. header parse on the device: pos/end up, parsed headers down */
 	err = pool_reserve(w, &w->hdr, n * (8 + sizeof(struct sgpu_hdr) + 12));
@@ -1563,7 +1565,7 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 					goto out;
 			}
 			err = round_launch(w, &E, SEL_UNDO, b->arena,
-					   b->arena_size, NULL, 0, &mu);
+					   b->arena_size, NULL, 0, &mu, stream);
 			if (!err)
 				err = sgpu_stream_sync(stream);
 			if (err)
@@ -1576,9 +1578,9 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 				break;
 		}
 		err = round_launch(w, &E, SEL_RUN, b->arena, b->arena_size,
-				   NULL, prot, &m);
+				   NULL, prot, &m, stream);
 		if (!err)
-			err = round_fetch(w, m);
+			err = round_fetch(w, m, stream);
 		if (!err)
 			err = sgpu_stream_sync(stream);
 		if (err)
@@ -2215,7 +2217,9 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		if (!w->pstream)
 			return EIO;
 	}
-	stream = b->stream ? b->stream : w->stream;
+	/* the caller's stream; NULL is the default (null) stream, which
+	 * orders this call after the caller's prior default-stream work */
+	stream = b->stream;
 	pst = w->pstream;
 
 	err = pool_reserve(w, &w->up, n * 12);
@@ -2387,11 +2391,10 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	 *    chunk by chunk (ordered after the caller's prior work) */
 	if (!parsed) {
 		entry_ev = w->ev[0];
-		if (b->stream) {
-			err = sgpu_event_record(entry_ev, stream);
-			if (!err)
-				err = sgpu_stream_wait(w->pstream, entry_ev);
-		}
+		/* the parse stream starts after the caller's prior work */
+		err = sgpu_event_record(entry_ev, stream);
+		if (!err)
+			err = sgpu_stream_wait(w->pstream, entry_ev);
 		if (!err)
 			err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4,
 					      w->pstream);
@@ -2650,7 +2653,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 
 	if (!w)
 		return ENOMEM;
-	stream = d->stream ? d->stream : w->stream;
+	stream = d->stream;     /* NULL: the default (null) stream */
 	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
 	if (!err)
 		err = pool_reserve(w, &w->dsc, n * 12);

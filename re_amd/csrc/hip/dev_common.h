@@ -161,6 +161,85 @@ __device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
 	aes_rounds<NR, 1>(smem, lo, rk, s0, s1, s2, s3);
 }
 
+/*
+ * Four-table AES ("T4"): 128 KiB LDS image, no rotations in the rounds.
+ *   - half 0 [0, 64 KiB):   T0 at entry*256 + [0,128), T1 at +128
+ *   - half 1 [64, 128 KiB): T2 = rotl16(T0) at +0,     T3 = rotl24(T0) at +128
+ *   each as 32 lane replicas (conflict-free ds_read_b32 like the T0/T1 image).
+ *   Half-1 addresses are one v_perm_b32 as well: the lane offset register
+ *   hi = lo | 0x10000 supplies byte 2.
+ *   A middle round column is xor3(xor3(T0[a], T1[b], T2[c]), T3[d], rk):
+ *   16 lookups + 16 address perms + 8 bitop3, round keys plain (the T0/T1
+ *   form needs 4 more half-rate v_alignbit per round).
+ * Measured on gfx950 (profiles/r01_ubench_valu_rates.log): v_perm_b32,
+ * v_alignbit_b32 and v_add3_u32 issue at half the rate of v_xor_b32 /
+ * v_bitop3_b32, so the rotations cost as much as 8 XORs.
+ */
+#define TT4_BYTES 131072u
+
+#define TT_ADDRH(x, k, hi) \
+	__builtin_amdgcn_perm((x), (hi), 0x0C020000u | ((4u + (k)) << 8))
+
+__device__ __forceinline__ void tt4_fill(uint8_t *smem, const uint32_t *T0g)
+{
+	uint32_t *s = (uint32_t *)smem;
+	for (uint32_t i = threadIdx.x; i < TT4_BYTES / 4; i += blockDim.x) {
+		const uint32_t e = (i >> 6) & 255u;
+		const uint32_t k = ((i >> 13) & 2u) | ((i >> 5) & 1u);
+		const uint32_t t = T0g[e];
+		s[i] = k ? __builtin_amdgcn_alignbit(t, t, 32 - 8 * k) : t;
+	}
+}
+
+struct Tt4 {
+	const uint8_t *smem;
+	uint32_t lo, hi;
+
+	__device__ __forceinline__ uint32_t t0(uint32_t x) const
+	{
+		return lds_u32(smem, TT_ADDR(x, 0, lo));
+	}
+	__device__ __forceinline__ uint32_t t1(uint32_t x) const
+	{
+		return lds_u32(smem, TT_ADDR(x, 1, lo) + 128);
+	}
+	__device__ __forceinline__ uint32_t t2(uint32_t x) const
+	{
+		return lds_u32(smem, TT_ADDRH(x, 2, hi));
+	}
+	__device__ __forceinline__ uint32_t t3(uint32_t x) const
+	{
+		return lds_u32(smem, TT_ADDRH(x, 3, hi) + 128);
+	}
+};
+
+/* one middle round on (s0..s3), k plain */
+__device__ __forceinline__ void aes4_round(const Tt4 &T, const uint32_t *k,
+					   uint32_t &s0, uint32_t &s1,
+					   uint32_t &s2, uint32_t &s3)
+{
+	const uint32_t a0 = T.t0(s0), b1 = T.t1(s1), c2 = T.t2(s2), d3 = T.t3(s3);
+	const uint32_t a1 = T.t0(s1), b2 = T.t1(s2), c3 = T.t2(s3), d0 = T.t3(s0);
+	const uint32_t a2 = T.t0(s2), b3 = T.t1(s3), c0 = T.t2(s0), d1 = T.t3(s1);
+	const uint32_t a3 = T.t0(s3), b0 = T.t1(s0), c1 = T.t2(s1), d2 = T.t3(s2);
+	s0 = xor3(xor3(a0, b1, c2), d3, k[0]);
+	s1 = xor3(xor3(a1, b2, c3), d0, k[1]);
+	s2 = xor3(xor3(a2, b3, c0), d1, k[2]);
+	s3 = xor3(xor3(a3, b0, c1), d2, k[3]);
+}
+
+template <int NR, int FIRST>
+__device__ __forceinline__ void aes4_rounds(const Tt4 &T, const uint32_t *rk,
+					    uint32_t &s0, uint32_t &s1,
+					    uint32_t &s2, uint32_t &s3)
+{
+#pragma unroll
+	for (int r = FIRST; r < NR; r++)
+		aes4_round(T, rk + 4 * r, s0, s1, s2, s3);
+	/* the final round reads half 0 only (same as the T0/T1 image) */
+	aes_final(T.smem, T.lo, rk + 4 * NR, s0, s1, s2, s3);
+}
+
 /* ---- SHA-1 compression, W[] holds the 16 big-endian message words ---- */
 /* Round = alignbit + bitop3 + 2 x add3 + alignbit; schedule = bitop3 (xor3)
  * + xor + alignbit (FIPS 180-4 6.1.2, rolling 16-word W). */

@@ -7,20 +7,21 @@
 #include "kern_common.h"
 
 /*
- * Occupancy.  The 64 KiB T-table image allows one LDS image per block and
- * two blocks per CU.  Single-key protect fits 128 VGPRs: 512-thread
- * blocks, 2 per CU = 4 waves/SIMD.  Single-key unprotect keeps ciphertext
- * and MAC schedule live together (~150 VGPRs): one 768-thread block per
- * CU = 3 waves/SIMD.  Per-lane keys: 512-thread blocks, 2 waves/SIMD.
+ * Occupancy.  The 128 KiB four-table image (dev_common.h, T4) allows one
+ * block per CU.  Single-key protect (round keys and HMAC midstates in
+ * SGPRs) fits 128 VGPRs: 1024-thread blocks = 4 waves/SIMD.  Single-key
+ * unprotect keeps ciphertext and plaintext of a chunk live (~150 VGPRs):
+ * 768-thread blocks = 3 waves/SIMD, no scratch.  Per-lane keys need ~190
+ * VGPRs: 512-thread blocks = 2 waves/SIMD.
  */
 __host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
 {
-	return !uni ? 1 : (prot ? 4 : 3);
+	return uni ? (prot ? 4 : 3) : 1;
 }
 
 __host__ __device__ constexpr unsigned ctr_block(bool prot, bool uni)
 {
-	return (uni && !prot) ? 768u : 512u;
+	return uni ? (prot ? 1024u : 768u) : 512u;
 }
 
 /*
@@ -39,10 +40,10 @@ __attribute__((amdgpu_flat_work_group_size(1, ctr_block(PROT, UNI))))
 __attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
 k_ctr_hmac(const KArgs a)
 {
-	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
 	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
 		return;
-	tt_fill(smem, a.t0);
+	tt4_fill(smem, a.t0);
 	__syncthreads();
 
 	uint8_t *const arena = a.arena;
@@ -72,6 +73,11 @@ k_ctr_hmac(const KArgs a)
 		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
 		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
 	}
+	/* the table stores middle-round keys rot16'd for the T0/T1 image;
+	 * the four-table rounds take them plain */
+#pragma unroll
+	for (int k = 4; k < 4 * NR; k++)
+		rk[k] = rot16(rk[k]);
 	if (UNI) {
 #pragma unroll
 		for (int k = 0; k < 4 * (NR + 1); k++)
@@ -99,7 +105,7 @@ k_ctr_hmac(const KArgs a)
 	}
 
 	/* compact launches never carry packets of 1 MiB or more (host) */
-	CtrKs<NR, COMPACT> C;
+	CtrKs<NR, COMPACT, true> C;
 	C.init(smem, lo, rk, iv);
 
 	uint32_t h[5];
@@ -155,35 +161,11 @@ k_ctr_hmac(const KArgs a)
 		const bool need_ks = do_cipher && (c0 + 64u > c_off) &&
 				     (c0 < c_end);
 		if (need_ks) {
-			uint32_t mask[16];
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				const uint32_t bpos = c0 + 4u * jj;
-				const uint32_t nbytes =
-					(bpos >= c_off && bpos < c_end) ?
-					min(c_end - bpos, 4u) : 0u;
-				mask[jj] = nbytes >= 4 ? 0xffffffffu :
-					   ((1u << (8 * nbytes)) - 1u);
-			}
 			ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
 						(int32_t)(4 * k) - cw4, carry, d,
-						mask);
-			if (store_ct) {
-#pragma unroll
-				for (int jj = 0; jj < 16; jj++) {
-					const uint32_t bpos = c0 + 4u * jj;
-					if (bpos >= c_off && bpos < c_end) {
-						const uint32_t nbytes =
-							min(c_end - bpos, 4u);
-						if (nbytes == 4)
-							*(uint32_t *)(pkt + bpos) =
-								d[jj];
-						else
-							st_partial(pkt + bpos,
-								   d[jj], nbytes);
-					}
-				}
-			}
+						c0, c_off, c_end);
+			if (store_ct)
+				store_region(pkt, c0, d, c_off, c_end);
 		}
 		/* protect: the MAC covers the ciphertext just produced */
 		if (PROT && mac) {
@@ -212,28 +194,29 @@ k_ctr_hmac(const KArgs a)
 			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
 		}
 		if (!PROT) {
-			/* keystream first (hides the chunk load), then the MAC
-			 * over the received ciphertext, then decrypt */
-			uint32_t ks[16];
+			/* decrypt into p and store it, then the MAC over the
+			 * received ciphertext d (no 16-word keystream buffer) */
+			uint32_t p[16];
 #pragma unroll
 			for (int jj = 0; jj < 16; jj++)
-				ks[jj] = 0;
+				p[jj] = d[jj];
 			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
-						 (int32_t)(4 * k) - cw4, carry, ks,
-						 NULL);
+						 (int32_t)(4 * k) - cw4, carry, p);
+			if (store_ct) {
+#pragma unroll
+				for (int g = 0; g < 4; g++)
+					*(uint4 *)(pkt + c0 + 16u * g) =
+						make_uint4(p[4 * g], p[4 * g + 1],
+							   p[4 * g + 2], p[4 * g + 3]);
+			}
 #pragma unroll
 			for (int jj = 0; jj < 16; jj++)
 				w[jj] = bswap32(d[jj]);
 			sha1_compress(h, w);
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				d[jj] ^= ks[jj];
+			continue;
 		}
-		else {
-			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
-						 (int32_t)(4 * k) - cw4, carry, d,
-						 NULL);
-		}
+		ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
+					 (int32_t)(4 * k) - cw4, carry, d);
 		if (store_ct) {
 #pragma unroll
 			for (int g = 0; g < 4; g++)
@@ -307,32 +290,19 @@ k_ctr_hmac(const KArgs a)
 			const uint32_t c0 = 64u * kk;
 			if (!(c0 + 64u > c_off && c0 < c_end))
 				continue;
-			uint32_t ksw[16], mask[16];
+			uint32_t d[16];
 #pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				ksw[jj] = 0;
-				mask[jj] = 0xffffffffu;
+			for (int g = 0; g < 4; g++) {
+				uint4 v = make_uint4(0, 0, 0, 0);
+				if (c0 + 16u * g < c_end)
+					v = ld16(pkt, pasz, c0 + 16u * g);
+				d[4 * g] = v.x; d[4 * g + 1] = v.y;
+				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
 			}
-			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
-						 (int32_t)(4 * kk) - cw4, carry,
-						 ksw, mask);
-#pragma unroll
-			for (int jj = 0; jj < 16; jj++) {
-				const uint32_t bpos = c0 + 4u * jj;
-				if (bpos >= c_off && bpos < c_end) {
-					uint32_t nbytes = min(c_end - bpos, 4u);
-					if (nbytes == 4) {
-						uint32_t *p = (uint32_t *)(pkt + bpos);
-						*p = *p ^ ksw[jj];
-					}
-					else {
-						uint32_t v = 0;
-						for (uint32_t q = 0; q < nbytes; q++)
-							v |= (uint32_t)pkt[bpos + q] << (8 * q);
-						st_partial(pkt + bpos, v ^ ksw[jj], nbytes);
-					}
-				}
-			}
+			ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
+						 (int32_t)(4 * kk) - cw4, carry, d,
+						 c0, c_off, c_end);
+			store_region(pkt, c0, d, c_off, c_end);
 		}
 		vd &= (uint8_t)~SV_CIPHERED;
 	}

@@ -55,8 +55,9 @@ __device__ __forceinline__ void st_be32(uint8_t *p, uint32_t v)
 
 /* ------------------------------------------------------------------ */
 /* CTR keystream block b (IV + b, 128-bit big-endian add, OpenSSL
- * CRYPTO_ctr128_encrypt semantics) */
-template <int NR>
+ * CRYPTO_ctr128_encrypt semantics).  T4: the four-table LDS image
+ * (dev_common.h); round keys are then plain for every round. */
+template <int NR, bool T4>
 __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
 					  const uint32_t *rk, const uint32_t iv[4],
 					  int32_t b, uint32_t ks[4])
@@ -66,7 +67,14 @@ __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
 	uint32_t s0 = iv[0], s1 = iv[1];
 	uint32_t s2 = bswap32((uint32_t)(c >> 32));
 	uint32_t s3 = bswap32((uint32_t)c);
-	aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
+	if (T4) {
+		const Tt4 T = {smem, lo, lo | 0x10000u};
+		s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+		aes4_rounds<NR, 1>(T, rk, s0, s1, s2, s3);
+	}
+	else {
+		aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
+	}
 	ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
 }
 
@@ -78,8 +86,13 @@ __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
  * 2..3 vary, round 1 has two varying lookups (columns 2..3 are constant)
  * and round 2 has eight.  Those constants are computed once per packet.
  * CACHED = false is the plain counter (any packet size).
+ *
+ * T0/T1 image (T4 = false): middle-round keys rot16'd, constants
+ *   A0,P0,A1,P1 (round 1) and R0,C1a,C1b,C2,C3a,C3b (round 2).
+ * T4 image: plain keys; round 1 s0 = A0 ^ T3[t3.b3], s1 = A1 ^ T2[t3.b2];
+ *   round 2 needs R0 (col 0), C1a (col 1), C2 (col 2), C3a (col 3).
  */
-template <int NR, bool CACHED>
+template <int NR, bool CACHED, bool T4 = false>
 struct CtrKs {
 	uint32_t t0, t1, t2, t3c;       /* IV ^ rk[0..3] (t3c: bytes 14,15 = rk) */
 	uint32_t A0, P0, A1, P1;        /* round 1: s0 = A0^rot16(P0^T1[t3.b3]) */
@@ -96,6 +109,22 @@ struct CtrKs {
 		if (!CACHED)
 			return;
 		const uint32_t *k1 = rk + 4, *k2 = rk + 8;
+		if (T4) {
+			const Tt4 T = {smem, lo, lo | 0x10000u};
+			/* round 1 (t3 bytes 0..1 constant) */
+			A0 = xor3(T.t0(t0), T.t1(t1), T.t2(t2)) ^ k1[0];
+			A1 = xor3(T.t0(t1), T.t1(t2), T.t3(t0)) ^ k1[1];
+			const uint32_t S2 = xor3(xor3(T.t0(t2), T.t1(t3c), T.t2(t0)),
+						 T.t3(t1), k1[2]);
+			const uint32_t S3 = xor3(xor3(T.t0(t3c), T.t1(t0), T.t2(t1)),
+						 T.t3(t2), k1[3]);
+			/* round 2 constants */
+			R0 = xor3(T.t2(S2), T.t3(S3), k2[0]);
+			C1a = xor3(T.t1(S2), T.t2(S3), k2[1]);
+			C2 = xor3(T.t0(S2), T.t1(S3), k2[2]);
+			C3a = xor3(T.t0(S3), T.t3(S2), k2[3]);
+			return;
+		}
 		A0 = lds_u32(smem, TT_ADDR(t0, 0, lo)) ^
 		     lds_u32(smem, TT_ADDR(t1, 1, lo) + 128);
 		P0 = lds_u32(smem, TT_ADDR(t2, 2, lo)) ^ k1[0];
@@ -133,10 +162,22 @@ struct CtrKs {
 		if (!CACHED) {
 			const uint32_t iv[4] = {t0 ^ rk[0], t1 ^ rk[1],
 						t2 ^ rk[2], t3c ^ rk[3]};
-			ctr_block<NR>(smem, lo, rk, iv, b, ks);
+			ctr_block<NR, T4>(smem, lo, rk, iv, b, ks);
 			return;
 		}
 		const uint32_t t3 = t3c ^ bswap32((uint32_t)b);
+		if (T4) {
+			const Tt4 T = {smem, lo, lo | 0x10000u};
+			const uint32_t s0 = A0 ^ T.t3(t3);
+			const uint32_t s1 = A1 ^ T.t2(t3);
+			uint32_t r0 = xor3(T.t0(s0), T.t1(s1), R0);
+			uint32_t r1 = xor3(T.t0(s1), T.t3(s0), C1a);
+			uint32_t r2 = xor3(T.t2(s0), T.t3(s1), C2);
+			uint32_t r3 = xor3(T.t1(s0), T.t2(s1), C3a);
+			aes4_rounds<NR, 3>(T, rk, r0, r1, r2, r3);
+			ks[0] = r0; ks[1] = r1; ks[2] = r2; ks[3] = r3;
+			return;
+		}
 		/* round 1: two varying lookups */
 		const uint32_t s0 = A0 ^ rot16(P0 ^ lds_u32(smem,
 					TT_ADDR(t3, 3, lo) + 128));
@@ -279,24 +320,37 @@ __device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
 	return true;
 }
 
+/* byte mask of chunk word bpos..bpos+3 inside the cipher region
+ * [c_off, c_end) (c_off is a multiple of 4) */
+__device__ __forceinline__ uint32_t region_mask(uint32_t bpos, uint32_t c_off,
+						uint32_t c_end)
+{
+	const uint32_t nbytes = (bpos >= c_off && bpos < c_end) ?
+				min(c_end - bpos, 4u) : 0u;
+	return nbytes >= 4 ? 0xffffffffu : ((1u << (8 * nbytes)) - 1u);
+}
+
 /*
  * XOR the keystream into the 16 words d[] of chunk k as each AES block is
  * produced (no 16-word keystream buffer).  Word jj of the chunk takes
  * keystream word jj - SHIFT of block blk0 = 4k - cw4; the first SHIFT words
- * take the tail of the previous chunk's last block (carry).  mask[]: per
- * word byte mask of the cipher region (all ones in the steady state).
+ * take the tail of the previous chunk's last block (carry).  MASKED: only
+ * the bytes inside the cipher region [c_off, c_end) change (chunk starts
+ * at byte c0); the mask is computed per word, not held in an array.
  */
-template <int NR, int SHIFT, bool MASKED, bool CACHED>
+template <int NR, int SHIFT, bool MASKED, bool CACHED, bool T4>
 __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 				       const uint32_t *rk,
-				       const CtrKs<NR, CACHED> &C,
+				       const CtrKs<NR, CACHED, T4> &C,
 				       int32_t blk0, uint32_t carry[4],
-				       uint32_t d[16], const uint32_t *mask)
+				       uint32_t d[16], uint32_t c0 = 0,
+				       uint32_t c_off = 0, uint32_t c_end = 0)
 {
+#define KS_MASK(jj) (MASKED ? region_mask(c0 + 4u * (jj), c_off, c_end) \
+			    : 0xffffffffu)
 #pragma unroll
 	for (int q = 0; q < SHIFT; q++)
-		d[q] ^= MASKED ? (carry[4 - SHIFT + q] & mask[q])
-			       : carry[4 - SHIFT + q];
+		d[q] ^= carry[4 - SHIFT + q] & KS_MASK(q);
 #pragma unroll
 	for (int m = 0; m < 4; m++) {
 		uint32_t B[4];
@@ -305,7 +359,7 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 		for (int q = 0; q < 4; q++) {
 			const int jj = SHIFT + 4 * m + q;
 			if (jj < 16)
-				d[jj] ^= MASKED ? (B[q] & mask[jj]) : B[q];
+				d[jj] ^= B[q] & KS_MASK(jj);
 			else
 				carry[q] = B[q];
 		}
@@ -313,6 +367,25 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 #pragma unroll
 			for (int q = 0; q < 4; q++)
 				carry[q] = B[q];
+		}
+	}
+#undef KS_MASK
+}
+
+/* store the words of chunk c0 that lie in the cipher region */
+__device__ __forceinline__ void store_region(uint8_t *pkt, uint32_t c0,
+					     const uint32_t d[16],
+					     uint32_t c_off, uint32_t c_end)
+{
+#pragma unroll
+	for (int jj = 0; jj < 16; jj++) {
+		const uint32_t bpos = c0 + 4u * jj;
+		if (bpos >= c_off && bpos < c_end) {
+			const uint32_t nbytes = min(c_end - bpos, 4u);
+			if (nbytes == 4)
+				*(uint32_t *)(pkt + bpos) = d[jj];
+			else
+				st_partial(pkt + bpos, d[jj], nbytes);
 		}
 	}
 }

@@ -4,24 +4,46 @@
  * (AES-256).
  */
 #pragma once
+#include <type_traits>
 #include "kern_common.h"
 
 /*
  * Occupancy.  The 128 KiB four-table image (dev_common.h, T4) allows one
- * block per CU.  Single-key protect (round keys and HMAC midstates in
- * SGPRs) fits 128 VGPRs: 1024-thread blocks = 4 waves/SIMD.  Single-key
- * unprotect keeps ciphertext and plaintext of a chunk live (~150 VGPRs):
- * 768-thread blocks = 3 waves/SIMD, no scratch.  Per-lane keys need ~190
- * VGPRs: 512-thread blocks = 2 waves/SIMD.
+ * block per CU.  Single-key launches (round keys and HMAC midstates in
+ * SGPRs) keep the pipelined chunk (ciphertext, plaintext, next keystream,
+ * quad-transpose temporaries) in ~170 VGPRs: 768-thread blocks = 3
+ * waves/SIMD, no scratch.  Per-lane keys need ~190 VGPRs: 512-thread
+ * blocks = 2 waves/SIMD.
  */
-__host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
-{
-	return uni ? (prot ? 4 : 3) : 1;
-}
+/* build knobs (kernel-variant experiments, scripts/build_variants.sh) */
+/* _P: protect, _U: unprotect */
+#ifndef CTR_COAL_P          /* quad-coalesced steady-state chunk access */
+#define CTR_COAL_P 1
+#endif
+#ifndef CTR_COAL_U
+#define CTR_COAL_U 0
+#endif
+#ifndef CTR_PIPE_P          /* keystream one chunk ahead of the MAC */
+#define CTR_PIPE_P 0
+#endif
+#ifndef CTR_PIPE_U
+#define CTR_PIPE_U 1
+#endif
+#ifndef CTR_UNI_PROT_BLOCK  /* single-key protect block size */
+#define CTR_UNI_PROT_BLOCK 1024
+#endif
+#ifndef CTR_UNI_UNP_BLOCK   /* single-key unprotect block size */
+#define CTR_UNI_UNP_BLOCK 768
+#endif
 
 __host__ __device__ constexpr unsigned ctr_block(bool prot, bool uni)
 {
-	return uni ? (prot ? 1024u : 768u) : 512u;
+	return uni ? (prot ? CTR_UNI_PROT_BLOCK : CTR_UNI_UNP_BLOCK) : 512u;
+}
+
+__host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
+{
+	return uni ? (int)(ctr_block(prot, uni) / 256u) : 1;
 }
 
 /*
@@ -127,14 +149,19 @@ k_ctr_hmac(const KArgs a)
 	 * input: steady-state body */
 	uint32_t kf0 = nchunk, kf1 = nchunk;
 	if (do_cipher && do_hmac) {
-		kf0 = min((c_off + 63u) / 64u, nchunk);
+		/* a cipher region starting in the first 16 bytes (RTP without
+		 * CSRC/extension, SRTCP) lets chunk 0 run the steady body: its
+		 * words before c_off take the zero carry and stay unchanged */
+		kf0 = c_off < 16u ? 0u : min((c_off + 63u) / 64u, nchunk);
 		kf1 = max(min(c_end, A) / 64u, kf0);
 	}
 
 	uint32_t carry[4] = {0, 0, 0, 0};
+	uint32_t ks[16];     /* keystream of the next chunk (pipelined loop) */
 
-	/* general chunk: any mix of header, cipher, MAC and padding */
-	auto chunk_general = [&](uint32_t k) {
+	/* general chunk: any mix of header, cipher, MAC and padding;
+	 * have_ks: ks[] already holds this chunk's keystream */
+	auto chunk_general = [&](uint32_t k, bool have_ks) {
 		const uint32_t c0 = 64u * k;
 		uint32_t d[16], w[16];
 #pragma unroll
@@ -161,9 +188,17 @@ k_ctr_hmac(const KArgs a)
 		const bool need_ks = do_cipher && (c0 + 64u > c_off) &&
 				     (c0 < c_end);
 		if (need_ks) {
-			ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
+			if (have_ks) {
+#pragma unroll
+				for (int jj = 0; jj < 16; jj++)
+					d[jj] ^= ks[jj] & region_mask(c0 + 4u * jj,
+								      c_off, c_end);
+			}
+			else {
+				ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
 						(int32_t)(4 * k) - cw4, carry, d,
 						c0, c_off, c_end);
+			}
 			if (store_ct)
 				store_region(pkt, c0, d, c_off, c_end);
 		}
@@ -183,56 +218,101 @@ k_ctr_hmac(const KArgs a)
 
 	uint32_t k = 0;
 	for (; k < kf0; k++)
-		chunk_general(k);
-	for (; k < kf1; k++) {
+		chunk_general(k, false);
+	/*
+	 * Steady state, software-pipelined: the keystream of chunk k+1 is
+	 * generated in the same basic block as the MAC of chunk k (no
+	 * dependence between them).  The last iteration's keystream is that
+	 * of chunk kf1, which the general tail chunk uses (have_ks).
+	 * Chunk bytes move quad-coalesced (quad_load/quad_store) over the
+	 * part [K0, K1) of the range that all four lanes of a quad share.
+	 */
+	constexpr bool PIPE = PROT ? CTR_PIPE_P : CTR_PIPE_U;
+	constexpr bool COAL = PROT ? CTR_COAL_P : CTR_COAL_U;
+	const bool piped = PIPE && kf0 < kf1;
+	if (piped)
+		chunk_ks<NR, SHIFT>(smem, lo, rk, C, (int32_t)(4 * kf0) - cw4,
+				    carry, ks);
+	const uint32_t lane = threadIdx.x & 63u;
+	uint32_t K0 = kf1, K1 = kf1;
+	uint64_t qb[4];
+	if constexpr (COMPACT && COAL) {
+		quad_offsets(j.off, lane, qb);
+		const uint64_t act = __ballot(1);
+		uint32_t a0 = max(kf0, qdpp<DPP_QXOR1>(kf0));
+		a0 = max(a0, qdpp<DPP_QXOR2>(a0));
+		uint32_t a1 = min(kf1, qdpp<DPP_QXOR1>(kf1));
+		a1 = min(a1, qdpp<DPP_QXOR2>(a1));
+		if (((act >> (lane & ~3u)) & 0xfull) == 0xfull && a0 < a1) {
+			K0 = a0;
+			K1 = a1;
+		}
+	}
+	auto steady = [&](uint32_t k, auto coal) {
+		constexpr bool CO = decltype(coal)::value;
 		const uint32_t c0 = 64u * k;
-		uint32_t d[16], w[16];
-#pragma unroll
-		for (int g = 0; g < 4; g++) {
-			const uint4 v = *(const uint4 *)(pkt + c0 + 16u * g);
-			d[4 * g] = v.x; d[4 * g + 1] = v.y;
-			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+		uint32_t d[16], o[16], w[16];
+		if constexpr (CO) {
+			quad_load(arena, qb, c0, lane, d);
 		}
-		if (!PROT) {
-			/* decrypt into p and store it, then the MAC over the
-			 * received ciphertext d (no 16-word keystream buffer) */
-			uint32_t p[16];
+		else {
 #pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				p[jj] = d[jj];
-			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
-						 (int32_t)(4 * k) - cw4, carry, p);
-			if (store_ct) {
-#pragma unroll
-				for (int g = 0; g < 4; g++)
-					*(uint4 *)(pkt + c0 + 16u * g) =
-						make_uint4(p[4 * g], p[4 * g + 1],
-							   p[4 * g + 2], p[4 * g + 3]);
+			for (int g = 0; g < 4; g++) {
+				const uint4 v = *(const uint4 *)(pkt + c0 + 16u * g);
+				d[4 * g] = v.x; d[4 * g + 1] = v.y;
+				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
 			}
+		}
+		if constexpr (PIPE) {
 #pragma unroll
 			for (int jj = 0; jj < 16; jj++)
-				w[jj] = bswap32(d[jj]);
-			sha1_compress(h, w);
-			continue;
+				o[jj] = d[jj] ^ ks[jj];
+			chunk_ks<NR, SHIFT>(smem, lo, rk, C,
+					    (int32_t)(4 * (k + 1)) - cw4, carry,
+					    ks);
 		}
-		ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
-					 (int32_t)(4 * k) - cw4, carry, d);
-		if (store_ct) {
+		else {
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				o[jj] = d[jj];
+			ks_xor<NR, SHIFT, false, COMPACT>(smem, lo, rk, C,
+							  (int32_t)(4 * k) - cw4,
+							  carry, o);
+		}
+		/* branch-free: protect always stores here (do_cipher),
+		 * unprotect writes the received bytes back when it must not
+		 * decrypt */
+		uint32_t s[16];
+#pragma unroll
+		for (int jj = 0; jj < 16; jj++)
+			s[jj] = (PROT || store_ct) ? o[jj] : d[jj];
+		if constexpr (CO) {
+			quad_store(arena, qb, c0, lane, s);
+		}
+		else {
 #pragma unroll
 			for (int g = 0; g < 4; g++)
 				*(uint4 *)(pkt + c0 + 16u * g) =
-					make_uint4(d[4 * g], d[4 * g + 1],
-						   d[4 * g + 2], d[4 * g + 3]);
+					make_uint4(s[4 * g], s[4 * g + 1],
+						   s[4 * g + 2], s[4 * g + 3]);
 		}
-		if (PROT) {
+		/* the MAC covers the ciphertext: produced (protect) or
+		 * received (unprotect) */
 #pragma unroll
-			for (int jj = 0; jj < 16; jj++)
-				w[jj] = bswap32(d[jj]);
-			sha1_compress(h, w);
-		}
+		for (int jj = 0; jj < 16; jj++)
+			w[jj] = bswap32(PROT ? o[jj] : d[jj]);
+		sha1_compress(h, w);
+	};
+	for (; k < K0; k++)
+		steady(k, std::false_type());
+	if constexpr (COMPACT && COAL) {
+		for (; k < K1; k++)
+			steady(k, std::true_type());
+		for (; k < kf1; k++)
+			steady(k, std::false_type());
 	}
 	for (; k < nchunk; k++)
-		chunk_general(k);
+		chunk_general(k, piped && k == kf1);
 
 	uint8_t vd = 0;
 	if (do_hmac) {

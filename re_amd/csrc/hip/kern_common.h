@@ -372,6 +372,135 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 #undef KS_MASK
 }
 
+/*
+ * The 16 keystream words of chunk k (blk0 = 4k - cw4) into ks[], carry as
+ * in ks_xor.  Used one chunk ahead of the MAC: the AES lookups of chunk
+ * k+1 (LDS-latency bound) have no dependence on the SHA-1 rounds of chunk
+ * k (VALU-chain bound), so one basic block holds both and the scheduler
+ * fills each lookup's latency with SHA-1 work.
+ */
+template <int NR, int SHIFT, bool CACHED, bool T4>
+__device__ __forceinline__ void chunk_ks(const uint8_t *smem, uint32_t lo,
+					 const uint32_t *rk,
+					 const CtrKs<NR, CACHED, T4> &C,
+					 int32_t blk0, uint32_t carry[4],
+					 uint32_t ks[16])
+{
+#pragma unroll
+	for (int q = 0; q < SHIFT; q++)
+		ks[q] = carry[4 - SHIFT + q];
+#pragma unroll
+	for (int m = 0; m < 4; m++) {
+		uint32_t B[4];
+		C.block(smem, lo, rk, blk0 + m, B);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const int jj = SHIFT + 4 * m + q;
+			if (jj < 16)
+				ks[jj] = B[q];
+			else
+				carry[q] = B[q];
+		}
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/*
+ * Quad-coalesced chunk access.  With one packet per lane, a wave64 load of
+ * 16 B per lane touches 64 cache lines (one per packet).  Instead the four
+ * lanes of a quad move one packet's 64-byte chunk together: in access g,
+ * lane j of the quad reads/writes bytes [16j, 16j+16) of the chunk of quad
+ * lane g, so one instruction touches 16 lines, 64 contiguous bytes each.
+ * A 4x4 transpose across the quad (two DPP quad_perm + select stages)
+ * turns "quarter j of packet g" into "quarter g of my packet" and back.
+ * scripts/ubench_ctr.hip: the per-lane pattern costs the fused CTR+HMAC
+ * loop ~30 % over its compute time, the coalesced one ~1 %.
+ */
+#define DPP_QXOR1 0xB1   /* quad_perm [1,0,3,2] */
+#define DPP_QXOR2 0x4E   /* quad_perm [2,3,0,1] */
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+/* x[r][c] = word c of register r; transposes (register, quad lane).  The
+ * selects are v_bitop3 with lane masks (a ?: on many values can become a
+ * divergent branch, which would split the loop body). */
+__device__ __forceinline__ void quad_transpose(uint32_t x[4][4], uint32_t lane)
+{
+	const uint32_t m0 = 0u - (lane & 1u), m1 = 0u - ((lane >> 1) & 1u);
+#pragma unroll
+	for (int c = 0; c < 4; c++) {
+#pragma unroll
+		for (int r = 0; r < 4; r += 2) {
+			const uint32_t t0 = qdpp<DPP_QXOR1>(x[r][c]);
+			const uint32_t t1 = qdpp<DPP_QXOR1>(x[r + 1][c]);
+			x[r + 1][c] = sha_ch(m0, x[r + 1][c], t0);
+			x[r][c] = sha_ch(m0, t1, x[r][c]);
+		}
+#pragma unroll
+		for (int r = 0; r < 2; r++) {
+			const uint32_t t0 = qdpp<DPP_QXOR2>(x[r][c]);
+			const uint32_t t2 = qdpp<DPP_QXOR2>(x[r + 2][c]);
+			x[r + 2][c] = sha_ch(m1, x[r + 2][c], t0);
+			x[r][c] = sha_ch(m1, t2, x[r][c]);
+		}
+	}
+}
+
+/* qb[g] = arena offset of the packet of quad lane g + 16 * (my quad index)
+ * (offsets, not pointers: the arena pointer keeps the accesses global) */
+__device__ __forceinline__ void quad_offsets(uint64_t off, uint32_t lane,
+					     uint64_t qb[4])
+{
+	const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
+	const uint32_t l4[4] = {qdpp<0x00>(lo), qdpp<0x55>(lo),
+				qdpp<0xAA>(lo), qdpp<0xFF>(lo)};
+	const uint32_t h4[4] = {qdpp<0x00>(hi), qdpp<0x55>(hi),
+				qdpp<0xAA>(hi), qdpp<0xFF>(hi)};
+#pragma unroll
+	for (int g = 0; g < 4; g++)
+		qb[g] = ((uint64_t)h4[g] << 32 | l4[g]) + 16u * (lane & 3u);
+}
+
+/* own 16 words of chunk c0 (every lane of the quad takes part) */
+__device__ __forceinline__ void quad_load(const uint8_t *arena,
+					  const uint64_t qb[4], uint32_t c0,
+					  uint32_t lane, uint32_t d[16])
+{
+	uint32_t x[4][4];
+#pragma unroll
+	for (int g = 0; g < 4; g++) {
+		const uint4 v = *(const uint4 *)(arena + qb[g] + c0);
+		x[g][0] = v.x; x[g][1] = v.y; x[g][2] = v.z; x[g][3] = v.w;
+	}
+	quad_transpose(x, lane);
+#pragma unroll
+	for (int q = 0; q < 4; q++)
+#pragma unroll
+		for (int c = 0; c < 4; c++)
+			d[4 * q + c] = x[q][c];
+}
+
+__device__ __forceinline__ void quad_store(uint8_t *arena, const uint64_t qb[4],
+					   uint32_t c0, uint32_t lane,
+					   const uint32_t s[16])
+{
+	uint32_t x[4][4];
+#pragma unroll
+	for (int q = 0; q < 4; q++)
+#pragma unroll
+		for (int c = 0; c < 4; c++)
+			x[q][c] = s[4 * q + c];
+	quad_transpose(x, lane);
+#pragma unroll
+	for (int g = 0; g < 4; g++)
+		*(uint4 *)(arena + qb[g] + c0) =
+			make_uint4(x[g][0], x[g][1], x[g][2], x[g][3]);
+}
+
 /* store the words of chunk c0 that lie in the cipher region */
 __device__ __forceinline__ void store_region(uint8_t *pkt, uint32_t c0,
 					     const uint32_t d[16],

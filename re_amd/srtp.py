@@ -9,7 +9,10 @@ import errno
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libre_srtp_amd.so")
+# RE_SRTP_LIB: an alternative build of the same library (kernel variant
+# experiments, scripts/build_variants.sh); default the in-tree build
+LIB_PATH = os.environ.get("RE_SRTP_LIB") or os.path.join(
+    HERE, "lib", "libre_srtp_amd.so")
 
 SRTP_AES_CM_128_HMAC_SHA1_32 = 0
 SRTP_AES_CM_128_HMAC_SHA1_80 = 1

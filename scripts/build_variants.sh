@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build kernel variants of the library for A/B timing on the GPU box:
+#   scripts/build_variants.sh NAME "-DKNOB=V ..." [NAME "-D..."]...
+# -> re_amd/lib/variants/NAME.so (load with RE_SRTP_LIB=...; bench.py as usual)
+set -e
+cd "$(dirname "$0")/../re_amd"
+make -s -j8 >/dev/null
+mkdir -p lib/variants /tmp/variants
+HIPCC=/opt/rocm/bin/hipcc
+FL="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-parameter -I../include -Icsrc"
+while [ $# -ge 2 ]; do
+  name=$1; defs=$2; shift 2
+  $HIPCC $FL $defs -c csrc/hip/ctr10.hip -o /tmp/variants/ctr10_$name.o &
+  $HIPCC $FL $defs -c csrc/hip/gcm.hip -o /tmp/variants/gcm_$name.o &
+  wait
+  objs="build/srtp.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/plan_multi.o"
+  $HIPCC -shared -fPIC --offload-arch=gfx950 -o lib/variants/$name.so $objs \
+    /tmp/variants/ctr10_$name.o /tmp/variants/gcm_$name.o -lpthread
+  echo "built lib/variants/$name.so ($defs)"
+done

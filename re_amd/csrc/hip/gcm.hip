@@ -1,6 +1,7 @@
 /*
  * gcm.hip -- AES-GCM (AEAD_AES_128_GCM / AEAD_AES_256_GCM) kernels.
  */
+#include <type_traits>
 #include "kern_common.h"
 
 /* OpenSSL gcm_gmult_4bit rem_4bit (values << 16 into the top word) */
@@ -281,6 +282,366 @@ k_gcm(const KArgs a)
 		verdict[i] = vd;
 }
 
+/* ------------------------------------------------------------------ */
+/*
+ * Single-key AES-GCM (compact launches whose packets share one session
+ * context -- the BASELINE config-3 path).  Same structure as the CTR
+ * kernel (k_ctr.h): 64-byte chunks aligned to the packet, a branch-free
+ * steady-state body with quad-coalesced chunk access, general byte-exact
+ * chunks at the head/tail.  GHASH uses an 8-bit table (ghash8_mul).
+ *
+ * LDS: T0/T1 image [0, 64 KiB) + GHASH M8 image [64, 128 KiB).
+ */
+#define GH8_OFF TT_BYTES
+#define GH8_BYTES 65536u
+#ifndef GCMU_BLOCK
+#define GCMU_BLOCK 768u     /* ~168 VGPRs: 3 waves/SIMD, no scratch */
+#endif
+#ifndef GCMU_COAL
+#define GCMU_COAL 1
+#endif
+
+/*
+ * M8[b] = b * H for all bytes b (OpenSSL Htable convention, BE words),
+ * from the 4-bit table: M8[b] = T4[b >> 4] ^ T4[b & 15] * x^4 (one 4-bit
+ * Shoup shift step, reduction rem_4bit[r] = clmul(r, 0xE1) << 21 in the
+ * top word).  Image: entry b at b * 256 + (lane & 15) * 16, 16 replicas:
+ * a ds_read_b128 serves 16 lanes per LDS cycle, each from its own 16-byte
+ * bank group whatever the entries (conflict-free).
+ */
+__device__ __forceinline__ void gh8_fill(uint8_t *img, const uint32_t (*ht)[4])
+{
+	for (uint32_t i = threadIdx.x; i < 256u * 16u; i += blockDim.x) {
+		const uint32_t b = i >> 4, r = i & 15u;
+		const uint4 L = *(const uint4 *)ht[b & 15u];
+		const uint4 H = *(const uint4 *)ht[b >> 4];
+		const uint32_t m = L.w & 15u;
+		const uint32_t red = (m ^ (m << 5) ^ (m << 6) ^ (m << 7)) << 21;
+		*(uint4 *)(img + b * 256u + r * 16u) = make_uint4(
+			(L.x >> 4) ^ red ^ H.x,
+			__builtin_amdgcn_alignbit(L.x, L.y, 4) ^ H.y,
+			__builtin_amdgcn_alignbit(L.y, L.z, 4) ^ H.z,
+			__builtin_amdgcn_alignbit(L.z, L.w, 4) ^ H.w);
+	}
+}
+
+/*
+ * X = X * H (SP 800-38D 6.3) with the 8-bit table and one deferred
+ * reduction.  With X_i the byte i of X and i = 4w + q:
+ *   X * H = sum_i M8[X_i] x^(8i) = sum_q x^(8q) A_q,
+ *   A_q   = sum_w M8[X_(4w+q)] x^(32w)        (word shifts: free)
+ * evaluated by Horner in q on an 8-word accumulator (x^8 = an 8-bit right
+ * shift of BE words), then the degrees 128..247 are folded back with
+ * x^128 = 1 + x + x^2 + x^7.  16 ds_read_b128 + ~110 VALU per block, no
+ * per-byte reduction table (OpenSSL's gcm_gmult_4bit: 32 lookups + 32
+ * reduction lookups).  hi16 = (lane & 15) * 16 | 0x10000 (image base).
+ */
+__device__ __forceinline__ void ghash8_mul(uint32_t x[4], const uint8_t *smem,
+					   uint32_t hi16)
+{
+	uint32_t R[8];
+#pragma unroll
+	for (int q = 3; q >= 0; q--) {
+		uint4 M[4];
+#pragma unroll
+		for (int w = 0; w < 4; w++)
+			M[w] = *(const uint4 *)(smem + TT_ADDRH(x[w], 3 - q, hi16));
+		const uint32_t A0 = M[0].x;
+		const uint32_t A1 = M[0].y ^ M[1].x;
+		const uint32_t A2 = xor3(M[0].z, M[1].y, M[2].x);
+		const uint32_t A3 = xor3(M[0].w, M[1].z, M[2].y) ^ M[3].x;
+		const uint32_t A4 = xor3(M[1].w, M[2].z, M[3].y);
+		const uint32_t A5 = M[2].w ^ M[3].z;
+		const uint32_t A6 = M[3].w;
+		if (q == 3) {
+			R[0] = A0; R[1] = A1; R[2] = A2; R[3] = A3;
+			R[4] = A4; R[5] = A5; R[6] = A6; R[7] = 0;
+		}
+		else {
+			R[7] = __builtin_amdgcn_alignbit(R[6], R[7], 8);
+			R[6] = __builtin_amdgcn_alignbit(R[5], R[6], 8) ^ A6;
+			R[5] = __builtin_amdgcn_alignbit(R[4], R[5], 8) ^ A5;
+			R[4] = __builtin_amdgcn_alignbit(R[3], R[4], 8) ^ A4;
+			R[3] = __builtin_amdgcn_alignbit(R[2], R[3], 8) ^ A3;
+			R[2] = __builtin_amdgcn_alignbit(R[1], R[2], 8) ^ A2;
+			R[1] = __builtin_amdgcn_alignbit(R[0], R[1], 8) ^ A1;
+			R[0] = (R[0] >> 8) ^ A0;
+		}
+	}
+	const uint32_t u0 = R[4], u1 = R[5], u2 = R[6], u3 = R[7];
+	x[0] = xor3(xor3(R[0], u0, u0 >> 1), u0 >> 2, u0 >> 7);
+	x[1] = xor3(xor3(R[1], u1, __builtin_amdgcn_alignbit(u0, u1, 1)),
+		    __builtin_amdgcn_alignbit(u0, u1, 2),
+		    __builtin_amdgcn_alignbit(u0, u1, 7));
+	x[2] = xor3(xor3(R[2], u2, __builtin_amdgcn_alignbit(u1, u2, 1)),
+		    __builtin_amdgcn_alignbit(u1, u2, 2),
+		    __builtin_amdgcn_alignbit(u1, u2, 7));
+	x[3] = xor3(xor3(R[3], u3, __builtin_amdgcn_alignbit(u2, u3, 1)),
+		    __builtin_amdgcn_alignbit(u2, u3, 2),
+		    __builtin_amdgcn_alignbit(u2, u3, 7));
+}
+
+/*
+ * One packet.  The cipher region is walked in 64-byte units aligned to its
+ * start c_off (four GHASH blocks each, so no block straddles two units):
+ * full units run a branch-free body (quad-coalesced when the four lanes of
+ * a quad all have one), the remainder (< 64 bytes) takes the byte-exact
+ * per-block path of the general kernel (k_gcm).  Returns the SV_* verdict.
+ */
+template <int NR, bool PROT>
+__device__ __forceinline__ uint8_t gcmu_packet(const uint8_t *smem, uint32_t lo,
+					       uint32_t hi16, const uint32_t *rk,
+					       const CtrKs<NR, true> &C,
+					       uint8_t *arena, uint64_t asz,
+					       const struct sgpu_job &j,
+					       uint32_t lane)
+{
+	uint8_t *pkt = arena + j.off;
+	const uint64_t pasz = asz - j.off;
+	const uint32_t A = j.a_len;
+	const uint32_t c_off = j.c_off, c_len = j.c_len;
+	const uint32_t c_end = c_off + c_len;
+	uint32_t X[4] = {0, 0, 0, 0};
+	for (uint32_t p = 0; p < A; p += 16) {
+		uint32_t w[4];
+		aad_block(pkt, pasz, p, A, false, 0u, w);
+		X[0] ^= w[0]; X[1] ^= w[1]; X[2] ^= w[2]; X[3] ^= w[3];
+		ghash8_mul(X, smem, hi16);
+	}
+
+	const uint32_t nunit = c_len / 64u;
+	uint32_t M1 = 0;
+	uint64_t qb[4];
+	if (GCMU_COAL) {
+		quad_offsets((uint64_t)j.off + c_off, lane, qb);
+		const uint64_t act = __ballot(1);
+		uint32_t a1 = min(nunit, qdpp<DPP_QXOR1>(nunit));
+		a1 = min(a1, qdpp<DPP_QXOR2>(a1));
+		if (((act >> (lane & ~3u)) & 0xfull) == 0xfull)
+			M1 = a1;
+	}
+	auto unit = [&](uint32_t m, auto coal) {
+		constexpr bool CO = decltype(coal)::value;
+		const uint32_t p0 = c_off + 64u * m;
+		uint32_t d[16], o[16];
+		if constexpr (CO) {
+			quad_load(arena, qb, 64u * m, lane, d);
+		}
+		else {
+#pragma unroll
+			for (int g = 0; g < 4; g++) {
+				const uint4 v = *(const uint4 *)(pkt + p0 + 16u * g);
+				d[4 * g] = v.x; d[4 * g + 1] = v.y;
+				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+			}
+		}
+#pragma unroll
+		for (int b = 0; b < 4; b++) {
+			uint32_t ks[4];
+			C.block(smem, lo, rk, (int32_t)(4u * m + b + 2u), ks);
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				o[4 * b + q] = d[4 * b + q] ^ ks[q];
+		}
+		if constexpr (CO) {
+			quad_store(arena, qb, 64u * m, lane, o);
+		}
+		else {
+#pragma unroll
+			for (int g = 0; g < 4; g++)
+				*(uint4 *)(pkt + p0 + 16u * g) =
+					make_uint4(o[4 * g], o[4 * g + 1],
+						   o[4 * g + 2], o[4 * g + 3]);
+		}
+#pragma unroll
+		for (int b = 0; b < 4; b++) {
+			const uint32_t *c = PROT ? o + 4 * b : d + 4 * b;
+			X[0] ^= bswap32(c[0]); X[1] ^= bswap32(c[1]);
+			X[2] ^= bswap32(c[2]); X[3] ^= bswap32(c[3]);
+			ghash8_mul(X, smem, hi16);
+		}
+	};
+	uint32_t m = 0;
+	if (GCMU_COAL)
+		for (; m < M1; m++)
+			unit(m, std::true_type());
+	for (; m < nunit; m++)
+		unit(m, std::false_type());
+
+	/* remainder: whole 16-byte blocks, then the partial one (k_gcm) */
+	const uint32_t nfull = c_len / 16u;
+	for (uint32_t b = 4u * nunit; b < nfull; b++) {
+		const uint32_t p = c_off + 16u * b;
+		const uint4 v = ld16(pkt, pasz, p);
+		uint32_t ks[4];
+		C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
+		const uint32_t o0 = v.x ^ ks[0], o1 = v.y ^ ks[1];
+		const uint32_t o2 = v.z ^ ks[2], o3 = v.w ^ ks[3];
+		*(uint4 *)(pkt + p) = make_uint4(o0, o1, o2, o3);
+		X[0] ^= bswap32(PROT ? o0 : v.x); X[1] ^= bswap32(PROT ? o1 : v.y);
+		X[2] ^= bswap32(PROT ? o2 : v.z); X[3] ^= bswap32(PROT ? o3 : v.w);
+		ghash8_mul(X, smem, hi16);
+	}
+	if (c_len > 16u * nfull) {
+		const uint32_t b = nfull, p = c_off + 16u * b;
+		const uint4 v = ld16(pkt, pasz, p);
+		const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+		uint32_t ks[4], ct[4];
+		C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
+		const uint32_t rem = c_end - p;
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t bp = 4u * q;
+			const uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
+			const uint32_t mk = nbytes >= 4 ? 0xffffffffu
+					  : ((1u << (8 * nbytes)) - 1u);
+			const uint32_t o = (d[q] ^ ks[q]) & mk;
+			ct[q] = PROT ? o : (d[q] & mk);
+			if (nbytes == 4)
+				*(uint32_t *)(pkt + p + bp) = o;
+			else if (nbytes)
+				st_partial(pkt + p + bp, o, nbytes);
+		}
+		X[0] ^= bswap32(ct[0]); X[1] ^= bswap32(ct[1]);
+		X[2] ^= bswap32(ct[2]); X[3] ^= bswap32(ct[3]);
+		ghash8_mul(X, smem, hi16);
+	}
+
+	/* length block: bitlen(AAD) || bitlen(C) */
+	{
+		const uint64_t al = (uint64_t)A * 8u, cl = (uint64_t)c_len * 8u;
+		X[0] ^= (uint32_t)(al >> 32); X[1] ^= (uint32_t)al;
+		X[2] ^= (uint32_t)(cl >> 32); X[3] ^= (uint32_t)cl;
+		ghash8_mul(X, smem, hi16);
+	}
+	/* tag = GHASH ^ E(K, J0) */
+	uint32_t e0[4];
+	C.block(smem, lo, rk, 1, e0);
+	const uint32_t t[4] = {X[0] ^ bswap32(e0[0]), X[1] ^ bswap32(e0[1]),
+			       X[2] ^ bswap32(e0[2]), X[3] ^ bswap32(e0[3])};
+	uint8_t *tp = pkt + j.tag_off;
+	uint8_t vd = SV_CIPHERED;
+	if (PROT) {
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+			st_be32(tp + 4 * q, t[q]);
+	}
+	else {
+		uint32_t diff = 0;
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			diff |= tp[q] ^ (uint8_t)(t[q >> 2] >> (24 - 8 * (q & 3)));
+		if (diff == 0)
+			vd |= SV_TAG_OK;
+	}
+	return vd;
+}
+
+template <int NR, bool PROT>
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, GCMU_BLOCK)))
+__attribute__((amdgpu_waves_per_eu(GCMU_BLOCK / 256u, 8)))
+k_gcmu(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES + GH8_BYTES];
+	__shared__ uint32_t blk_comp;
+	if (a.c.guard && *a.c.guard)          /* rejected plan */
+		return;
+	tt_fill(smem, a.t0);
+	uint8_t *__restrict__ verdict = a.verdict;
+	const bool undo = a.c.undo;
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	struct sgpu_job j;
+	uint32_t i = 0;
+	const bool live = get_job<true, SGPU_MODE_GCM, PROT>(
+		a, blockIdx.x * blockDim.x + threadIdx.x, j, i);
+	if (!live)
+		j.flags = SJ_SKIP, j.comp = 0;
+	/* the block's first live packet names the context (every packet of
+	 * a single-key launch shares it) */
+	if (threadIdx.x == 0)
+		blk_comp = 0xffffffffu;
+	__syncthreads();
+	if (live && !(j.flags & SJ_SKIP))
+		atomicMin(&blk_comp, j.comp);
+	__syncthreads();
+	const uint32_t bc = blk_comp;
+	if (bc != 0xffffffffu)
+		gh8_fill(smem + GH8_OFF, a.comps[bc].htab);
+	__syncthreads();
+	if (!live)
+		return;
+	if (j.flags & SJ_SKIP) {
+		if (verdict && !undo)
+			verdict[i] = 0;
+		return;
+	}
+	const uint32_t ci = __builtin_amdgcn_readfirstlane(j.comp);
+	const struct sgpu_comp *cp = a.comps + ci;
+	uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+	for (int k = 0; k < NR + 1; k++) {
+		uint4 v = *(const uint4 *)&cp->rk[4 * k];
+		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
+		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
+	}
+#pragma unroll
+	for (int k = 0; k < 4 * (NR + 1); k++)
+		rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
+	uint8_t *pkt = a.arena + j.off;
+
+	/* srtp_iv_calc_gcm (misc.c:93-105); J0 = IV || 0^31 || 1 */
+	uint32_t iv[4];
+	{
+		uint4 ks = *(const uint4 *)cp->k_s;
+		const uint32_t ixhi = j.ixhi, ixlo = j.ixlo;
+		const uint32_t be0 = (j.ssrc >> 16) & 0xffffu;
+		const uint32_t be1 = ((j.ssrc & 0xffffu) << 16) | (ixhi >> 16);
+		const uint32_t be2 = ((ixhi & 0xffffu) << 16) | (ixlo & 0xffffu);
+		iv[0] = ks.x ^ bswap32(be0);
+		iv[1] = ks.y ^ bswap32(be1);
+		iv[2] = ks.z ^ bswap32(be2);
+		iv[3] = 0;
+	}
+	CtrKs<NR, true> C;
+	C.init(smem, lo, rk, iv);
+
+	if (j.flags & SJ_UNDO) {
+		/* re-apply the keystream: restores a speculatively decrypted
+		 * payload before the exact re-run (counter b + 2) */
+		const uint32_t nb = (j.c_len + 15u) / 16u;
+		for (uint32_t b = 0; b < nb; b++) {
+			const uint32_t p = j.c_off + 16u * b;
+			uint32_t ks[4];
+			C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
+			const uint32_t rem = j.c_off + j.c_len - p;
+			for (int q = 0; q < 4; q++) {
+				const uint32_t bp = 4u * q;
+				const uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
+				if (nbytes == 4) {
+					uint32_t *w = (uint32_t *)(pkt + p + bp);
+					*w = *w ^ ks[q];
+				}
+				else if (nbytes) {
+					uint32_t v = 0;
+					for (uint32_t z = 0; z < nbytes; z++)
+						v |= (uint32_t)pkt[p + bp + z] << (8 * z);
+					st_partial(pkt + p + bp, v ^ ks[q], nbytes);
+				}
+			}
+		}
+		return;
+	}
+	const uint32_t hi16 = ((lane & 15u) << 4) | 0x10000u;
+	const uint8_t vd = gcmu_packet<NR, PROT>(smem, lo, hi16, rk, C, a.arena,
+						 a.asz, j, lane);
+	if (!PROT && !(vd & SV_TAG_OK))
+		atomicAdd(a.c.nfail, 1u);
+	if (verdict)
+		verdict[i] = vd;
+}
+
 kfn_t sgpu_pick_gcm(bool compact, bool uni, int nr, int prot)
 {
 #define PICKG(C, U)                                                            \
@@ -294,12 +655,17 @@ kfn_t sgpu_pick_gcm(bool compact, bool uni, int nr, int prot)
 	}
 	PICKG(false, false)
 	PICKG(true, false)
-	PICKG(true, true)
 #undef PICKG
+	if (compact && uni) {
+		if (nr == 10)
+			return prot ? k_gcmu<10, true> : k_gcmu<10, false>;
+		if (nr == 14)
+			return prot ? k_gcmu<14, true> : k_gcmu<14, false>;
+	}
 	return NULL;
 }
 
 unsigned sgpu_gcm_block(bool uni)
 {
-	return uni ? GCM_UNI_BLOCK : KBLOCK;
+	return uni ? GCMU_BLOCK : KBLOCK;
 }

@@ -501,6 +501,27 @@ __device__ __forceinline__ void quad_store(uint8_t *arena, const uint64_t qb[4],
 			make_uint4(x[g][0], x[g][1], x[g][2], x[g][3]);
 }
 
+/* store_region with volatile stores: exactly the bytes of the region,
+ * never widened to the whole word (see gcm.hip k_gcmu) */
+__device__ __forceinline__ void store_region_exact(uint8_t *pkt, uint32_t c0,
+						   const uint32_t d[16],
+						   uint32_t c_off, uint32_t c_end)
+{
+	volatile uint8_t *vp = pkt;
+#pragma unroll
+	for (int jj = 0; jj < 16; jj++) {
+		const uint32_t bpos = c0 + 4u * jj;
+		if (bpos >= c_off && bpos < c_end) {
+			const uint32_t nbytes = min(c_end - bpos, 4u);
+			if (nbytes == 4)
+				*(volatile uint32_t *)(vp + bpos) = d[jj];
+			else
+				for (uint32_t z = 0; z < nbytes; z++)
+					vp[bpos + z] = (uint8_t)(d[jj] >> (8 * z));
+		}
+	}
+}
+
 /* store the words of chunk c0 that lie in the cipher region */
 __device__ __forceinline__ void store_region(uint8_t *pkt, uint32_t c0,
 					     const uint32_t d[16],

@@ -2552,6 +2552,12 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			now_ms() - t0);
 	if (err)
 		goto out;
+	if (nfail && getenv("RE_SRTP_DEBUG_NOFOLD")) {
+		/* debugging aid: leave the speculative first pass in place */
+		fprintf(stderr, "re_srtp: %u speculation misses not folded\n",
+			nfail);
+		goto out;
+	}
 	if (nfail) {
 		/* speculation missed: undo and fold exactly */
 		for (k = 0; k < nfl && !err; k++) {

@@ -320,6 +320,23 @@ k_mp_final(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
 	st_out[s] = o;
 }
 
+/*
+ * Launch order of the crypto kernels: packets by descending number of
+ * 64-byte chunks (key 255 - chunks, stable), so a wave's lanes carry
+ * packets of about the same length -- with mixed 200/1400-B traffic
+ * (config 4) a wave otherwise runs as long as its longest packet.
+ */
+__global__ void k_mp_lenkey(const uint32_t *pos, const uint32_t *end,
+			    uint32_t *key, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint32_t L = end[i] >= pos[i] ? end[i] - pos[i] : 0u;
+	const uint32_t ch = (L + 63u) >> 6;
+	key[i] = 255u - (ch < 255u ? ch : 255u);
+}
+
 /* ---- host side ------------------------------------------------------ */
 
 static size_t mp_align(size_t x)
@@ -351,7 +368,8 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 			      const struct sgpu_sstate *st_in,
 			      struct sgpu_sstate *st_out, uint64_t *desc,
 			      void *scratch, size_t scratch_bytes,
-			      struct sgpu_plan_out *out, void *stream)
+			      struct sgpu_plan_out *out, uint32_t *order,
+			      void *stream)
 {
 	hipStream_t st = (hipStream_t)stream;
 	const uint32_t n = in->n, nb = (n + MP_BLOCK - 1) / MP_BLOCK;
@@ -390,5 +408,18 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 			   dim3(MP_BLOCK), 0, st, *in, c, (const uint32_t *)pex,
 			   (const uint32_t *)segf, (const uint32_t *)segl,
 			   st_out, out);
+	if (order) {
+		/* crypto launch order (k_mp_lenkey); pex and kout are free
+		 * once k_mp_final has run, vin is still the identity */
+		size_t tb8 = mp_cub_bytes(n, 8);
+		if (tb8 > tb)
+			return EINVAL;
+		hipLaunchKernelGGL(k_mp_lenkey, dim3(nb), dim3(MP_BLOCK), 0, st,
+				   pos, end, pex, n);
+		if (hipcub::DeviceRadixSort::SortPairs(p, tb8, pex, kout, vin,
+						       order, (int)n, 0, 8,
+						       st) != hipSuccess)
+			return EIO;
+	}
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

@@ -2066,6 +2066,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	uint32_t *save_d = (uint32_t *)(w->vs.d + 64);
 	uint8_t *vd_d = w->vs.d + 64 + n * 4;
 	struct sgpu_sstate *sin_h, *sin_d, *sout_h, *sout_d;
+	uint32_t *order_d;
 	struct sgpu_mplan_in in;
 	size_t scr, i;
 	uint32_t bits = 1;
@@ -2075,8 +2076,8 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 		bits++;
 	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
 	err = pool_reserve(w, &w->ms, nsess * 2 * sizeof(struct sgpu_sstate));
-	if (!err)
-		err = pool_reserve(w, &w->mscr, scr);
+	if (!err)   /* scratch, then the launch order (n words) */
+		err = pool_reserve(w, &w->mscr, scr + n * 4);
 	if (err)
 		return err;
 	sin_h = (struct sgpu_sstate *)w->ms.h;
@@ -2085,6 +2086,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	sout_d = sin_d + nsess;
 	if (mplan_gather(sessv, nsess, sin_h))
 		return -1;
+	order_d = (uint32_t *)(w->mscr.d + scr);
 
 	memset(&in, 0, sizeof(in));
 	in.n = (uint32_t)n;
@@ -2111,7 +2113,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (!err)
 		err = sgpu_mplan_rtp(&in, hd_d, up_d, up_d + n, NULL,
 				     b->arena_size, up_d + 2 * n, sin_d, sout_d,
-				     desc_d, w->mscr.d, w->mscr.cap, po_d,
+				     desc_d, w->mscr.d, scr, po_d, order_d,
 				     stream);
 	if (err)
 		return err;
@@ -2121,8 +2123,8 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	for (q = 0; q < nclass && capok && !err; q++) {
 		struct sgpu_compact C = {
 			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
-			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 0,
+			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
+			vd_d, save_d, nfail_d, 0, 0,
 			gcm ? &po_d->fail : &po_d->skip[q]};
 		err = sgpu_run_compact(b->arena, b->arena_size, &C, c0->mode,
 				       (int)c0->nr, q, prot, stream);

@@ -222,6 +222,8 @@ int   sgpu_plan_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
  * session on the device, every session's run of packets gets the
  * single-stream speculation above, and each touched session's final state
  * is returned (sgpu_sstate), so the host work is O(sessions).
+ * order (device, n words, or NULL): the packets by descending length, the
+ * launch order for the crypto kernels (equal work per wave).
  */
 enum {
 	SST_EXISTS  = 1u << 0,  /* stream 0 exists */
@@ -257,7 +259,8 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 		     const struct sgpu_sstate *st_in,
 		     struct sgpu_sstate *st_out, uint64_t *desc,
 		     void *scratch, size_t scratch_bytes,
-		     struct sgpu_plan_out *out, void *stream);
+		     struct sgpu_plan_out *out, uint32_t *order,
+		     void *stream);
 
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */

@@ -484,3 +484,45 @@ def test_multi_session_device_planner(suite, torch_cuda):
             for x, y in zip(ea + da, eb + db):
                 assert (x == y).all(), mode
         assert A[1] == B[1] and A[2] == B[2], mode
+
+
+@pytest.mark.parametrize("suite", list(range(6)))
+@pytest.mark.parametrize("cc", [0, 1, 3])
+def test_every_length_single_session(suite, cc, torch_cuda):
+    """one session, one header class, every payload length 0..260: the
+    single-key kernels' head/steady/tail chunk split and partial last
+    words (k_ctr_hmac UNI, k_gcmu) against the oracle, both directions"""
+    torch = torch_cuda
+    rng = np.random.default_rng(900 + 10 * suite + cc)
+    key = keys_for(suite, 1)[0]
+    pkts = [(0, rtp_packet(rng, (65500 + i) & 0xffff, 0x2468, cc=cc,
+                           plen=plen)) for i, plen in enumerate(range(261))]
+    arena, pos, end, cap, _ = to_arena(pkts)
+    tx = P.Srtp(suite, key)
+    enc = run(torch, "srtp_encrypt", [tx], arena, pos, end, cap, None, False)
+    be = O.OracleBackend()
+    octx = be.alloc(suite, key, 0)[0]
+    prot = []
+    for i, (_, p) in enumerate(pkts):
+        e, po, en, _, buf = be.call(octx, "srtp_encrypt", len(p) + 64, 0,
+                                    len(p), p, len(p) + 16)
+        assert (int(enc[3][i]), int(enc[1][i] - pos[i]),
+                int(enc[2][i] - pos[i])) == (e, po, en), i
+        assert enc[0][pos[i]:enc[2][i]].tobytes() == buf[:en], (i, len(p))
+        prot.append((0, bytes(buf[:en])))
+    be.free(octx)
+    a2, p2, e2, c2, _ = to_arena(prot)
+    rx = P.Srtp(suite, key)
+    dec = run(torch, "srtp_decrypt", [rx], a2, p2, e2, c2, None, False)
+    assert not dec[3].any(), np.flatnonzero(dec[3])[:8]
+    # whole buffer vs the oracle receiver: plaintext, and the tag bytes
+    # (the HMAC suites leave the ROC over them, srtp.c:342-344)
+    octx = be.alloc(suite, key, 0)[0]
+    for i, (_, q) in enumerate(prot):
+        e, po, en, _, buf = be.call(octx, "srtp_decrypt", len(q) + 64, 0,
+                                    len(q), q, len(q))
+        assert e == 0 and dec[0][p2[i]:dec[2][i]].tobytes() == pkts[i][1]
+        assert dec[0][p2[i]:p2[i] + len(buf)].tobytes() == buf, (i, len(q))
+    be.free(octx)
+    tx.close()
+    rx.close()

@@ -174,11 +174,14 @@ def main():
     # per-call descriptor arrays (the API updates pos/end in place).
     # Default: srtp_*_batch_dev -- windows and results resident in HBM like
     # the packets; --host-arrays: srtp_*_batch with host windows.
-    use_dev = (not args.host_arrays) and nsess == 1
+    use_dev = not args.host_arrays
+    sess_d = None
     if use_dev:
         i32 = lambda a: torch.from_numpy(
             np.asarray(a, dtype=np.uint32).view(np.int32)).to(dev)
         pos_d, end_d, cap_d = i32(pos), i32(end), i32(cap)
+        if sess is not None:
+            sess_d = i32(sess)
         p_d, e_d = torch.empty_like(pos_d), torch.empty_like(end_d)
         err_ed = torch.zeros(n, dtype=torch.int32, device=dev)
         err_dd = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -242,7 +245,9 @@ def main():
                 rc = P.device_batch_dev(opname, ss, arena.data_ptr(),
                                         arena.numel(), p_d.data_ptr(),
                                         e_d.data_ptr(), cap_d.data_ptr(),
-                                        er.data_ptr(), n, None, sptr)
+                                        er.data_ptr(), n,
+                                        sess_d.data_ptr() if sess_d
+                                        is not None else None, sptr)
                 assert rc == 0, (rc, P.lib().srtp_gpu_error())
                 nbad.add_(torch.count_nonzero(er))
             return 0

@@ -2745,6 +2745,151 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	return -1;
 }
 
+/*
+ * Many sessions with at most one RTP stream each, every array in HBM: the
+ * multi-session device planner (plan_multi.hip) plus the compact kernels
+ * in length order; host work is O(sessions) (gather the stream states,
+ * apply the returned ones).  -1: not plannable (nothing modified), or a
+ * forged packet (undone; the caller folds through the staged engine).
+ */
+static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
+			struct srtp_batch_dev *d)
+{
+	const int prot = op == OP_RTP_ENC;
+	const struct comp *c0 = &sessv[0]->rtp;
+	const size_t n = d->n;
+	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const int nclass = gcm ? 1 : 4;
+	struct sgpu_plan_out *po, *po_d;
+	struct sgpu_sstate *sin_h, *sin_d, *sout_h, *sout_d;
+	struct sgpu_mplan_in in;
+	struct sgpu_hdr *hd_d;
+	uint64_t *desc_d;
+	uint32_t *es_d, *save_d, *nfail_d, *cm_h, *order_d, nfail = 0, bits = 1;
+	uint8_t *vd_d;
+	size_t scr, k;
+	void *stream = d->stream;
+	struct ws *w = ws_get();
+	int err, q;
+
+	if (!w)
+		return ENOMEM;
+	for (k = 0; k < nsess; k++)
+		if (sessv[k]->suite != sessv[0]->suite)
+			return -1;
+	while (bits < 32 && ((size_t)1 << bits) < nsess)
+		bits++;
+	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 12);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)
+		err = pool_reserve(w, &w->cm, nsess * 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out));
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = pool_reserve(w, &w->ms,
+				   nsess * 2 * sizeof(struct sgpu_sstate));
+	if (!err)   /* scratch, then the launch order (n words) */
+		err = pool_reserve(w, &w->mscr, scr + n * 4);
+	if (err)
+		return err;
+	hd_d = (struct sgpu_hdr *)w->hd.d;
+	desc_d = (uint64_t *)w->dsc.d;
+	nfail_d = (uint32_t *)w->vs.d;
+	save_d = (uint32_t *)(w->vs.d + 64);
+	vd_d = w->vs.d + 64 + n * 4;
+	po = (struct sgpu_plan_out *)w->pl.h;
+	po_d = (struct sgpu_plan_out *)w->pl.d;
+	es_d = (uint32_t *)w->es.d;
+	cm_h = (uint32_t *)w->cm.h;
+	sin_h = (struct sgpu_sstate *)w->ms.h;
+	sin_d = (struct sgpu_sstate *)w->ms.d;
+	sout_h = sin_h + nsess;
+	sout_d = sin_d + nsess;
+	order_d = (uint32_t *)(w->mscr.d + scr);
+	if (mplan_gather(sessv, nsess, sin_h))
+		return -1;
+	for (k = 0; k < nsess; k++)
+		cm_h[k] = 2u * sessv[k]->slot;          /* comp[0] = RTP */
+
+	memset(&in, 0, sizeof(in));
+	in.n = (uint32_t)n;
+	in.nsess = (uint32_t)nsess;
+	in.prot = (uint32_t)prot;
+	in.tag = T;
+	in.need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
+	in.key_bits = bits;
+	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
+	if (!err)
+		err = sgpu_memcpy_h2d(sin_d, sin_h,
+				      nsess * sizeof(struct sgpu_sstate), stream);
+	if (!err)
+		err = sgpu_memset(nfail_d, 0, 4, stream);
+	if (!err)   /* the kernels keep reading the input windows */
+		err = sgpu_memcpy_d2d(es_d, d->end, n * 4, stream);
+	if (!err)
+		err = sgpu_parse_headers(d->arena, d->arena_size, d->pos, es_d,
+					 hd_d, NULL, (uint32_t)n, 0, stream);
+	if (!err)
+		err = sgpu_mplan_rtp(&in, hd_d, d->pos, es_d, d->cap,
+				     d->arena_size, d->sess, sin_d, sout_d,
+				     desc_d, w->mscr.d, scr, po_d, order_d,
+				     stream);
+	for (q = 0; q < nclass && !err; q++) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, d->sess,
+			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
+			vd_d, save_d, nfail_d, 0, 0,
+			gcm ? &po_d->fail : &po_d->skip[q]};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, q, prot, stream);
+	}
+	if (!err)
+		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
+					(uint32_t)n,
+					prot ? (int32_t)T : -(int32_t)T, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(sout_h, sout_d,
+				      nsess * sizeof(struct sgpu_sstate), stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	if (po->fail)
+		return -1;
+	mplan_apply(sessv, nsess, sout_h, prot);
+	if (!nfail)
+		return 0;
+	/* a forged packet: undo on the device, fold on the host engine */
+	for (q = 0; q < nclass && !err; q++) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, d->sess,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 1, 0,
+			gcm ? &po_d->fail : &po_d->skip[q]};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, q, prot, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, es_d, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	mplan_unapply(sessv, nsess, w);
+	return -1;
+}
+
 /* any other batch: stage the device arrays through the host engine */
 static int dev_staged(int op, struct srtp **sessv, size_t nsess,
 		      struct srtp_batch_dev *d)
@@ -2823,6 +2968,12 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 	    !d->sess && sessv[0]->nstreams <= 1 &&
 	    !getenv("RE_SRTP_NOPLAN") && !getenv("RE_SRTP_GENERAL")) {
 		int r = dev_planned(op, sessv[0], d);
+		if (r >= 0)
+			return r;
+	}
+	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess > 1 && d->sess &&
+	    !getenv("RE_SRTP_NOPLAN") && !getenv("RE_SRTP_GENERAL")) {
+		int r = dev_mplanned(op, sessv, nsess, d);
 		if (r >= 0)
 			return r;
 	}

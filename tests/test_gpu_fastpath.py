@@ -526,3 +526,63 @@ def test_every_length_single_session(suite, cc, torch_cuda):
     be.free(octx)
     tx.close()
     rx.close()
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_device_resident_multi_session(suite, torch_cuda):
+    """srtp_*_batch_dev with a session array (multi-session device plan,
+    every array in HBM) == srtp_*_batch (host arrays) == general engine,
+    over two consecutive batches; a forged packet forces undo + fold"""
+    torch = torch_cuda
+    rng = np.random.default_rng(77 + suite)
+    nsess = 50
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    batches = [multi_session_traffic(rng, 1500, nsess, s0=65500)]
+    last = {}
+    for s, p in batches[0]:
+        last[s] = int.from_bytes(p[2:4], "big")
+    nb = []
+    for _ in range(1500):   # continues every session (ROC wraps inside)
+        s = int(rng.integers(0, nsess))
+        last[s] = (last.get(s, 0) + 1) & 0xffff
+        nb.append((s, rtp_packet(rng, last[s], 0x7000 + s,
+                                 plen=int(rng.integers(0, 400)))))
+    batches.append(nb)
+    res = {}
+    for mode in ("dev", "host", "general"):
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        outs = []
+        for bi, pk in enumerate(batches):
+            arena, pos, end, cap, sess = to_arena(pk)
+            if mode == "dev":
+                enc = run_dev(torch, "srtp_encrypt", tx, arena, pos, end,
+                              cap, sess)
+            else:
+                enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap,
+                          sess, mode == "general")
+            prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
+                    for i, (s, _) in enumerate(pk)]
+            if bi == 1:
+                q = bytearray(prot[321][1])
+                q[-2] ^= 0x08
+                prot[321] = (prot[321][0], bytes(q))
+            a2, p2, e2, c2, s2 = to_arena(prot)
+            if mode == "dev":
+                dec = run_dev(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2)
+            else:
+                dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
+                          mode == "general")
+            outs.append((enc, dec))
+        res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
+        for c in tx + rx:
+            c.close()
+    A = res["dev"]
+    assert int(A[0][1][1][3][321]) == P.EAUTH
+    for mode in ("host", "general"):
+        B = res[mode]
+        for (ea, da), (eb, db) in zip(A[0], B[0]):
+            for x, y in zip(ea + da, eb + db):
+                assert (x == y).all(), mode
+        assert A[1] == B[1] and A[2] == B[2], mode

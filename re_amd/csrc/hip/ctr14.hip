@@ -5,6 +5,8 @@
 
 kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot)
 {
+	if (shift < 0)
+		return compact ? sgpu_pick_ctr14_any(uni, prot) : NULL;
 #define PICK(C, U, S)                                                          \
 	if (compact == C && uni == U && shift == S)                            \
 		return prot ? k_ctr_hmac<14, S, true, C, U>                    \

@@ -57,12 +57,8 @@ __host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
  * general byte-exact path.
  */
 template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>
-__global__ void
-__attribute__((amdgpu_flat_work_group_size(1, ctr_block(PROT, UNI))))
-__attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
-k_ctr_hmac(const KArgs a)
+__device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 {
-	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
 	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
 		return;
 	tt4_fill(smem, a.t0);
@@ -382,7 +378,10 @@ k_ctr_hmac(const KArgs a)
 			ks_xor<NR, SHIFT, true, COMPACT>(smem, lo, rk, C,
 						 (int32_t)(4 * kk) - cw4, carry, d,
 						 c0, c_off, c_end);
-			store_region(pkt, c0, d, c_off, c_end);
+			/* exact byte stores: this pass runs after the ROC word
+			 * was written at c_end (hipcc widened the partial last
+			 * word of store_region here, as in gcm.hip k_gcmu) */
+			store_region_exact(pkt, c0, d, c_off, c_end);
 		}
 		vd &= (uint8_t)~SV_CIPHERED;
 	}
@@ -400,3 +399,40 @@ k_ctr_hmac(const KArgs a)
 		verdict[i] = vd;
 }
 
+template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, ctr_block(PROT, UNI))))
+__attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
+k_ctr_hmac(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	ctr_hmac_body<NR, SHIFT, PROT, COMPACT, UNI>(a, smem);
+}
+
+/*
+ * One launch for a device-planned batch whose header class (SHIFT) is
+ * known only on the device: a.c.guard points at the plan's skip[0..3]
+ * (k_plan_final: skip[s] = fail || class != s), at most one of which is
+ * zero.  Saves the three empty class launches of the per-class scheme.
+ */
+template <int NR, bool PROT, bool UNI>
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, ctr_block(PROT, UNI))))
+__attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
+k_ctr_hmac_any(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	const uint32_t *g = a.c.guard;
+	const uint32_t q = !g[3] ? 3u : !g[0] ? 0u : !g[1] ? 1u : !g[2] ? 2u
+								    : 4u;
+	if (q > 3u)
+		return;                 /* rejected plan */
+	KArgs b = a;
+	b.c.guard = NULL;
+	switch (q) {
+	case 0: ctr_hmac_body<NR, 0, PROT, true, UNI>(b, smem); break;
+	case 1: ctr_hmac_body<NR, 1, PROT, true, UNI>(b, smem); break;
+	case 2: ctr_hmac_body<NR, 2, PROT, true, UNI>(b, smem); break;
+	default: ctr_hmac_body<NR, 3, PROT, true, UNI>(b, smem); break;
+	}
+}

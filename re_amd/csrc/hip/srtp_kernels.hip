@@ -769,7 +769,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 	a.save = c->save;
 	a.c = *c;
 	return launch(f, a, c->n,
-		      c->undo ? -1 : prof_slot(mode, nr, shift, prot),
+		      c->undo ? -1 : prof_slot(mode, nr, shift < 0 ? 3 : shift,
+					       prot),
 		      (hipStream_t)stream,
 		      mode == SGPU_MODE_GCM ? sgpu_gcm_block(c->uniform != 0)
 					    : sgpu_ctr_block(c->uniform != 0, prot));

@@ -2042,6 +2042,36 @@ static void mplan_unapply(struct srtp **sessv, size_t nsess, struct ws *w)
 }
 
 /*
+ * The compact crypto launches of a device-planned batch.  GCM: one launch
+ * guarded by po->fail.  AES-CM: the header class (SHIFT) is only known on
+ * the device, so one k_ctr_hmac_any launch picks it from po->skip[0..3];
+ * undo passes (rare) keep one guarded launch per class.
+ */
+static int run_classes(uint8_t *arena, uint64_t asz, struct sgpu_compact C,
+		       const struct comp *c0, struct sgpu_plan_out *po_d,
+		       int prot, void *stream)
+{
+	int q, err = 0;
+
+	if (c0->mode == SGPU_MODE_GCM) {
+		C.guard = &po_d->fail;
+		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
+					0, prot, stream);
+	}
+	if (!C.undo && !getenv("RE_SRTP_PERCLASS")) {
+		C.guard = po_d->skip;
+		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
+					-1, prot, stream);
+	}
+	for (q = 0; q < 4 && !err; q++) {
+		C.guard = &po_d->skip[q];
+		err = sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
+				       q, prot, stream);
+	}
+	return err;
+}
+
+/*
  * Returns 0 (planned and launched; *nfailp holds the speculation misses,
  * fl/nfl the launches), an errno, -1 (not eligible: nothing done) or -2
  * (plan rejected: headers parsed on the device and downloaded to w->hd.h,
@@ -2120,14 +2150,13 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (prot)
 		for (i = 0; i < n; i++)
 			capok &= (uint64_t)b->end[i] + need <= b->cap[i];
-	for (q = 0; q < nclass && capok && !err; q++) {
+	if (!err && capok) {
 		struct sgpu_compact C = {
 			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0,
-			gcm ? &po_d->fail : &po_d->skip[q]};
-		err = sgpu_run_compact(b->arena, b->arena_size, &C, c0->mode,
-				       (int)c0->nr, q, prot, stream);
+			vd_d, save_d, nfail_d, 0, 0, NULL};
+		err = run_classes(b->arena, b->arena_size, C, c0,
+				  po_d, prot, stream);
 	}
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
@@ -2333,15 +2362,13 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		if (prot)
 			for (i = 0; i < n; i++)
 				capok &= (uint64_t)b->end[i] + need <= b->cap[i];
-		for (q = 0; q < nclass && capok && !err; q++) {
+		if (!err && capok) {
 			struct sgpu_compact C = {
 				up_d, up_d + n, hd_d, desc_d, NULL,
 				(const uint32_t *)w->cm.d, NULL, 0,
-				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1,
-				gcm ? &po_d->fail : &po_d->skip[q]};
-			err = sgpu_run_compact(b->arena, b->arena_size, &C,
-					       c0->mode, (int)c0->nr, q, prot,
-					       stream);
+				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL};
+			err = run_classes(b->arena, b->arena_size, C, c0,
+					  po_d, prot, stream);
 		}
 		if (!err)
 			err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
@@ -2646,8 +2673,6 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 			      (T > 4 ? T : 4u)) : 0u;
 	const unsigned ns0 = s->nstreams;
-	const int gcm = c0->mode == SGPU_MODE_GCM;
-	const int nclass = gcm ? 1 : 4;
 	struct srtp_stream old;
 	struct sgpu_plan_in in;
 	struct sgpu_plan_out *po, *po_d;
@@ -2657,7 +2682,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	uint8_t *vd_d;
 	void *stream;
 	struct ws *w = ws_get();
-	int err, q;
+	int err;
 
 	if (!w)
 		return ENOMEM;
@@ -2699,14 +2724,13 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!err)
 		err = sgpu_plan_rtp(&in, hd_d, d->pos, es_d, d->cap,
 				    d->arena_size, desc_d, scr, po_d, stream);
-	for (q = 0; q < nclass && !err; q++) {
+	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1,
-			gcm ? &po_d->fail : &po_d->skip[q]};
-		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
-				       (int)c0->nr, q, prot, stream);
+			save_d, nfail_d, 0, 1, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  po_d, prot, stream);
 	}
 	if (!err)
 		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
@@ -2726,14 +2750,13 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!nfail)
 		return 0;
 	/* a forged packet: undo on the device, fold on the host engine */
-	for (q = 0; q < nclass && !err; q++) {
+	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 1,
-			gcm ? &po_d->fail : &po_d->skip[q]};
-		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
-				       (int)c0->nr, q, prot, stream);
+			save_d, nfail_d, 1, 1, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  po_d, prot, stream);
 	}
 	if (!err)
 		err = sgpu_memcpy_d2d(d->end, es_d, n * 4, stream);
@@ -2760,7 +2783,6 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	const size_t n = d->n;
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
 	const int gcm = c0->mode == SGPU_MODE_GCM;
-	const int nclass = gcm ? 1 : 4;
 	struct sgpu_plan_out *po, *po_d;
 	struct sgpu_sstate *sin_h, *sin_d, *sout_h, *sout_d;
 	struct sgpu_mplan_in in;
@@ -2771,7 +2793,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	size_t scr, k;
 	void *stream = d->stream;
 	struct ws *w = ws_get();
-	int err, q;
+	int err;
 
 	if (!w)
 		return ENOMEM;
@@ -2841,14 +2863,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 				     d->arena_size, d->sess, sin_d, sout_d,
 				     desc_d, w->mscr.d, scr, po_d, order_d,
 				     stream);
-	for (q = 0; q < nclass && !err; q++) {
+	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0,
-			gcm ? &po_d->fail : &po_d->skip[q]};
-		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
-				       (int)c0->nr, q, prot, stream);
+			vd_d, save_d, nfail_d, 0, 0, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  po_d, prot, stream);
 	}
 	if (!err)
 		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
@@ -2871,14 +2892,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (!nfail)
 		return 0;
 	/* a forged packet: undo on the device, fold on the host engine */
-	for (q = 0; q < nclass && !err; q++) {
+	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 0,
-			gcm ? &po_d->fail : &po_d->skip[q]};
-		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
-				       (int)c0->nr, q, prot, stream);
+			save_d, nfail_d, 1, 0, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  po_d, prot, stream);
 	}
 	if (!err)
 		err = sgpu_memcpy_d2d(d->end, es_d, n * 4, stream);

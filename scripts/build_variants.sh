@@ -11,10 +11,11 @@ FL="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-parameter -I../includ
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   $HIPCC $FL $defs -c csrc/hip/ctr10.hip -o /tmp/variants/ctr10_$name.o &
+  $HIPCC $FL $defs -c csrc/hip/ctr10a.hip -o /tmp/variants/ctr10a_$name.o &
   $HIPCC $FL $defs -c csrc/hip/gcm.hip -o /tmp/variants/gcm_$name.o &
   wait
-  objs="build/srtp.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/plan_multi.o"
+  objs="build/srtp.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/ctr14a.o build/plan_multi.o"
   $HIPCC -shared -fPIC --offload-arch=gfx950 -o lib/variants/$name.so $objs \
-    /tmp/variants/ctr10_$name.o /tmp/variants/gcm_$name.o -lpthread
+    /tmp/variants/ctr10_$name.o /tmp/variants/ctr10a_$name.o /tmp/variants/gcm_$name.o -lpthread
   echo "built lib/variants/$name.so ($defs)"
 done

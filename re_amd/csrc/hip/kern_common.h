@@ -91,7 +91,17 @@ __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
  *   A0,P0,A1,P1 (round 1) and R0,C1a,C1b,C2,C3a,C3b (round 2).
  * T4 image: plain keys; round 1 s0 = A0 ^ T3[t3.b3], s1 = A1 ^ T2[t3.b2];
  *   round 2 needs R0 (col 0), C1a (col 1), C2 (col 2), C3a (col 3).
+ *   With CTR_B15 s1 is folded into R0/C1a/C2/C3a and A1 holds the LDS
+ *   address of the T3 lookup of t3's byte 3 at b = 0.
  */
+/* CTR_B15 (T4 image only): packets whose keystream block index stays
+ * under 256 (compact launches carry packets under SGPU_CACHED_MAX_CTR
+ * bytes), so only IV byte 15 varies: round 1 has one varying lookup,
+ * round 2 four (5 instead of 10 per block) */
+#ifndef CTR_B15
+#define CTR_B15 1
+#endif
+
 template <int NR, bool CACHED, bool T4 = false>
 struct CtrKs {
 	uint32_t t0, t1, t2, t3c;       /* IV ^ rk[0..3] (t3c: bytes 14,15 = rk) */
@@ -123,6 +133,18 @@ struct CtrKs {
 			C1a = xor3(T.t1(S2), T.t2(S3), k2[1]);
 			C2 = xor3(T.t0(S2), T.t1(S3), k2[2]);
 			C3a = xor3(T.t0(S3), T.t3(S2), k2[3]);
+#if CTR_B15
+			/* b < 256: t3 byte 2 (IV byte 14) is constant too, so
+			 * s1 and the four round-2 terms it feeds are constants
+			 * and the one varying lookup's address is
+			 * AD3 ^ (b << 8) (TT_ADDRH of t3c's byte 3) */
+			const uint32_t s1 = A1 ^ T.t2(t3c);
+			R0 ^= T.t1(s1);
+			C1a ^= T.t0(s1);
+			C2 ^= T.t3(s1);
+			C3a ^= T.t2(s1);
+			A1 = TT_ADDRH(t3c, 3, lo | 0x10000u) + 128u;
+#endif
 			return;
 		}
 		A0 = lds_u32(smem, TT_ADDR(t0, 0, lo)) ^
@@ -152,9 +174,10 @@ struct CtrKs {
 		C3b = lds_u32(smem, TT_ADDR(S2, 3, lo) + 128) ^ k2[3];
 	}
 
-	/* keystream block b.  CACHED: exact for 0 <= b < 65536 (the host
-	 * sends packets of 1 MiB or more to the plain general kernels);
-	 * b < 0 only ever lands in masked words. */
+	/* keystream block b.  CACHED: exact for 0 <= b < 65536, and with
+	 * T4 && CTR_B15 for 0 <= b < 256 (SGPU_CACHED_MAX_*: the host and
+	 * the device planners send longer packets to the plain general
+	 * kernels); b < 0 only ever lands in masked words. */
 	__device__ __forceinline__ void block(const uint8_t *smem, uint32_t lo,
 					      const uint32_t *rk, int32_t b,
 					      uint32_t ks[4]) const
@@ -163,6 +186,18 @@ struct CtrKs {
 			const uint32_t iv[4] = {t0 ^ rk[0], t1 ^ rk[1],
 						t2 ^ rk[2], t3c ^ rk[3]};
 			ctr_block<NR, T4>(smem, lo, rk, iv, b, ks);
+			return;
+		}
+		if (T4 && CTR_B15) {
+			const Tt4 T = {smem, lo, lo | 0x10000u};
+			const uint32_t s0 = A0 ^ lds_u32(smem, A1 ^
+					(((uint32_t)b & 255u) << 8));
+			uint32_t r0 = T.t0(s0) ^ R0;
+			uint32_t r1 = T.t3(s0) ^ C1a;
+			uint32_t r2 = T.t2(s0) ^ C2;
+			uint32_t r3 = T.t1(s0) ^ C3a;
+			aes4_rounds<NR, 3>(T, rk, r0, r1, r2, r3);
+			ks[0] = r0; ks[1] = r1; ks[2] = r2; ks[3] = r3;
 			return;
 		}
 		const uint32_t t3 = t3c ^ bswap32((uint32_t)b);

@@ -110,7 +110,7 @@ k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
 			f |= SPF_PARSE;
 		if (!in.prot && (int)seq - (int)sb > 32768)
 			f |= SPF_TIMEOUT;
-		if (end[i] - pos[i] >= (1u << 20) - 64u)
+		if (end[i] - pos[i] >= in.maxlen)
 			f |= SPF_SIZE;
 		if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
 		    (cap && (end[i] > cap[i] || cap[i] > asz)))

@@ -239,12 +239,24 @@ __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 			const uint32_t *__restrict__ pos,
 			const uint32_t *__restrict__ end,
 			struct sgpu_hdr *__restrict__ out,
-			uint32_t *__restrict__ eix, uint32_t n, int rtcp)
+			uint32_t *__restrict__ eix, uint32_t n, int rtcp,
+			struct sgpu_prologue pro)
 {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (blockIdx.x == 0) {
+		/* the batch prologue folded into the parse launch */
+		for (uint32_t k = threadIdx.x; k < pro.nz0; k += blockDim.x)
+			pro.z0[k] = 0;
+		for (uint32_t k = threadIdx.x; k < pro.nz1; k += blockDim.x)
+			pro.z1[k] = 0;
+		if (pro.cm_out && threadIdx.x == 0)
+			*pro.cm_out = pro.cm;
+	}
 	if (i >= n)
 		return;
 	const uint32_t p = pos[i], e = end[i];
+	if (pro.end_copy)
+		pro.end_copy[i] = e;
 	/* a window outside the arena is never read (the planner rejects it) */
 	const uint32_t left = (e > p && e <= asz) ? e - p : 0;
 	const uint8_t *b = arena + p;
@@ -369,7 +381,7 @@ k_plan_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 			f |= SPF_PARSE;
 		if (!in.prot && (int)seq - (int)sb > 32768)
 			f |= SPF_TIMEOUT;
-		if (end[i] - pos[i] >= (1u << 20) - 64u)
+		if (end[i] - pos[i] >= in.maxlen)
 			f |= SPF_SIZE;
 		if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
 		    (cap && (end[i] > cap[i] || cap[i] > asz)))
@@ -783,9 +795,24 @@ extern "C" int sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,
 {
 	if (!n)
 		return 0;
+	struct sgpu_prologue pro;
+	memset(&pro, 0, sizeof(pro));
+	return sgpu_parse_prologue(arena, arena_size, pos, end, out, eix, n,
+				   rtcp, &pro, stream);
+}
+
+extern "C" int sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
+				   const uint32_t *pos, const uint32_t *end,
+				   struct sgpu_hdr *out, uint32_t *eix,
+				   uint32_t n, int rtcp,
+				   const struct sgpu_prologue *pro,
+				   void *stream)
+{
+	if (!n)
+		return 0;
 	hipLaunchKernelGGL(k_parse, dim3((n + 255) / 256), dim3(256), 0,
 			   (hipStream_t)stream, arena, arena_size, pos, end, out,
-			   eix, n, rtcp);
+			   eix, n, rtcp, *pro);
 	return herr(hipGetLastError(), "k_parse launch");
 }
 
@@ -944,7 +971,8 @@ extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
 	const uint32_t nb = (in->n + PLAN_BLOCK - 1) / PLAN_BLOCK;
 	if (!in->n)
 		return EINVAL;
-	int e = herr(hipMemsetAsync(out, 0, sizeof(*out), st), "plan memset");
+	int e = in->zeroed ? 0 : herr(hipMemsetAsync(out, 0, sizeof(*out), st),
+				      "plan memset");
 	if (e)
 		return e;
 	hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(PLAN_BLOCK), 0, st,

@@ -1930,6 +1930,7 @@ static void plan_in(struct sgpu_plan_in *in, const struct srtp *s,
 	in->bitmap = st0 ? st0->replay_rtp.bitmap : 0;
 	in->tag = T;
 	in->need = need;
+	in->maxlen = SGPU_CACHED_MAX(s->rtp.mode);
 }
 
 /* stream state after an accepted device plan (old state kept for undo) */
@@ -1964,15 +1965,18 @@ static void plan_unapply(struct srtp *s, unsigned nstreams0,
 
 /* session states in (pinned) -> device; -1 if some session has 2+ streams */
 static int mplan_gather(struct srtp **sessv, size_t nsess,
-			struct sgpu_sstate *st)
+			struct sgpu_sstate *st, uint32_t *cm)
 {
+	const int suite = (int)sessv[0]->suite;
 	size_t k;
 	for (k = 0; k < nsess; k++) {
 		const struct srtp *s = sessv[k];
 		if (k + 16 < nsess)
 			__builtin_prefetch(sessv[k + 16], 0, 1);
-		if (s->nstreams > 1)
+		if (s->nstreams > 1 || (int)s->suite != suite)
 			return -1;
+		if (cm)
+			cm[k] = 2u * s->slot;           /* comp[0] = RTP */
 		memset(&st[k], 0, sizeof(st[k]));
 		if (s->nstreams) {
 			const struct srtp_stream *x = &s->streams[0];
@@ -2114,7 +2118,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	sin_d = (struct sgpu_sstate *)w->ms.d;
 	sout_h = sin_h + nsess;
 	sout_d = sin_d + nsess;
-	if (mplan_gather(sessv, nsess, sin_h))
+	if (mplan_gather(sessv, nsess, sin_h, NULL))
 		return -1;
 	order_d = (uint32_t *)(w->mscr.d + scr);
 
@@ -2124,6 +2128,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	in.prot = (uint32_t)prot;
 	in.tag = T;
 	in.need = need;
+	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	in.key_bits = bits;
 	memcpy(up_h, b->pos, n * 4);
 	memcpy(up_h + n, b->end, n * 4);
@@ -2625,29 +2630,31 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	return err;
 }
 
-#define FAST_MAX_PKT ((1u << 20) - 64u)
-
 static int run_batch(int op, struct srtp **sessv, size_t nsess,
 		     struct srtp_batch *b)
 {
 	size_t i;
+	uint32_t lim = UINT32_MAX;
 	int r, big = 0;
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && sessv && nsess && b &&
 	    b->arena && b->pos && b->end && b->cap && b->err &&
 	    b->n <= UINT32_MAX / 4 && b->arena_size <= UINT32_MAX &&
 	    !getenv("RE_SRTP_GENERAL")) {
-		for (i = 0; i < nsess; i++)
+		for (i = 0; i < nsess; i++) {
 			if (!sessv[i])
 				return EINVAL;
+			if (SGPU_CACHED_MAX(sessv[i]->rtp.mode) < lim)
+				lim = SGPU_CACHED_MAX(sessv[i]->rtp.mode);
+		}
 		for (i = 0; i < b->n; i++) {
 			if ((b->pos[i] & 3) || b->end[i] > b->cap[i] ||
 			    b->cap[i] > b->arena_size ||
 			    b->pos[i] > b->end[i] ||
 			    (b->sess && b->sess[i] >= nsess))
 				return EINVAL;
-			/* the compact kernels cache the CTR counter block
-			 * for payloads under 1 MiB (kern_common.h CtrKs) */
-			if (b->end[i] - b->pos[i] >= FAST_MAX_PKT)
+			/* the compact kernels cache the counter block for
+			 * packets under SGPU_CACHED_MAX (kern_common.h) */
+			if (b->end[i] - b->pos[i] >= lim)
 				big = 1;
 		}
 		r = big ? -1 : run_fast(op, sessv, nsess, b);
@@ -2712,15 +2719,16 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	es_d = (uint32_t *)w->es.d;
 
 	plan_in(&in, s, (uint32_t)n, prot, T, need);
-	*(uint32_t *)w->cm.h = cm;
-	err = sgpu_memcpy_h2d(w->cm.d, w->cm.h, 4, stream);
-	if (!err)
-		err = sgpu_memset(nfail_d, 0, 4, stream);
-	if (!err)
-		err = sgpu_memcpy_d2d(es_d, d->end, n * 4, stream);
-	if (!err)
-		err = sgpu_parse_headers(d->arena, d->arena_size, d->pos, es_d,
-					 hd_d, NULL, (uint32_t)n, 0, stream);
+	{
+		/* one launch: parse + end copy + zeroed counters + comp map */
+		struct sgpu_prologue pro = {
+			es_d, nfail_d, (uint32_t *)po_d, 1,
+			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm};
+		in.zeroed = 1;
+		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
+					  d->end, hd_d, NULL, (uint32_t)n, 0,
+					  &pro, stream);
+	}
 	if (!err)
 		err = sgpu_plan_rtp(&in, hd_d, d->pos, es_d, d->cap,
 				    d->arena_size, desc_d, scr, po_d, stream);
@@ -2790,16 +2798,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	uint64_t *desc_d;
 	uint32_t *es_d, *save_d, *nfail_d, *cm_h, *order_d, nfail = 0, bits = 1;
 	uint8_t *vd_d;
-	size_t scr, k;
+	size_t scr;
 	void *stream = d->stream;
 	struct ws *w = ws_get();
 	int err;
 
 	if (!w)
 		return ENOMEM;
-	for (k = 0; k < nsess; k++)
-		if (sessv[k]->suite != sessv[0]->suite)
-			return -1;
 	while (bits < 32 && ((size_t)1 << bits) < nsess)
 		bits++;
 	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
@@ -2835,10 +2840,9 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	sout_h = sin_h + nsess;
 	sout_d = sin_d + nsess;
 	order_d = (uint32_t *)(w->mscr.d + scr);
-	if (mplan_gather(sessv, nsess, sin_h))
+	/* one pass over the sessions: suite check, stream state, slot map */
+	if (mplan_gather(sessv, nsess, sin_h, cm_h))
 		return -1;
-	for (k = 0; k < nsess; k++)
-		cm_h[k] = 2u * sessv[k]->slot;          /* comp[0] = RTP */
 
 	memset(&in, 0, sizeof(in));
 	in.n = (uint32_t)n;
@@ -2846,18 +2850,20 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	in.prot = (uint32_t)prot;
 	in.tag = T;
 	in.need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
+	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	in.key_bits = bits;
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
 	if (!err)
 		err = sgpu_memcpy_h2d(sin_d, sin_h,
 				      nsess * sizeof(struct sgpu_sstate), stream);
-	if (!err)
-		err = sgpu_memset(nfail_d, 0, 4, stream);
-	if (!err)   /* the kernels keep reading the input windows */
-		err = sgpu_memcpy_d2d(es_d, d->end, n * 4, stream);
-	if (!err)
-		err = sgpu_parse_headers(d->arena, d->arena_size, d->pos, es_d,
-					 hd_d, NULL, (uint32_t)n, 0, stream);
+	if (!err) {
+		/* parse + end copy (the kernels keep reading the input
+		 * windows) + zeroed miss counter, one launch */
+		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0};
+		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
+					  d->end, hd_d, NULL, (uint32_t)n, 0,
+					  &pro, stream);
+	}
 	if (!err)
 		err = sgpu_mplan_rtp(&in, hd_d, d->pos, es_d, d->cap,
 				     d->arena_size, d->sess, sin_d, sout_d,

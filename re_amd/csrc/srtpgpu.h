@@ -180,8 +180,18 @@ struct sgpu_plan_in {
 	uint32_t tag;           /* bytes the tag adds / removes */
 	uint32_t ssrc_any;      /* no stream yet: take packet 0's SSRC */
 	uint32_t need;          /* protect: tag room end + need <= cap */
+	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
+	uint32_t zeroed;        /* out already zeroed (sgpu_parse_prologue) */
 	uint32_t pad;
 };
+
+/* compact (counter-cached) kernels take packets shorter than this:
+ * AES-CM caches rounds 1-2 for block indices < 256 (kern_common.h CtrKs,
+ * CTR_B15), GCM for counters < 65536 */
+#define SGPU_CACHED_MAX_CTR (4096u - 64u)
+#define SGPU_CACHED_MAX_GCM ((1u << 20) - 64u)
+#define SGPU_CACHED_MAX(mode) \
+	((mode) == SGPU_MODE_GCM ? SGPU_CACHED_MAX_GCM : SGPU_CACHED_MAX_CTR)
 
 enum {
 	SPF_PARSE   = 1u << 0,  /* EBADMSG / short packet */
@@ -247,6 +257,7 @@ struct sgpu_mplan_in {
 	uint32_t tag;
 	uint32_t need;
 	uint32_t key_bits;      /* bits of the session index */
+	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
 };
 
 /* device scratch needed by sgpu_mplan_rtp */
@@ -287,6 +298,22 @@ int   sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,
 			 const uint32_t *pos, const uint32_t *end,
 			 struct sgpu_hdr *out, uint32_t *eix, uint32_t n,
 			 int rtcp, void *stream);
+
+/* sgpu_parse_headers plus the per-call prologue of a device batch in the
+ * same launch: end_copy[i] = end[i] (if set), z0[0..nz0) and z1[0..nz1)
+ * zeroed, *cm_out = cm (if set) -- instead of separate copy/fill ops */
+struct sgpu_prologue {
+	uint32_t *end_copy;
+	uint32_t *z0, *z1;
+	uint32_t nz0, nz1;
+	uint32_t *cm_out;
+	uint32_t cm;
+};
+int   sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
+			  const uint32_t *pos, const uint32_t *end,
+			  struct sgpu_hdr *out, uint32_t *eix, uint32_t n,
+			  int rtcp, const struct sgpu_prologue *pro,
+			  void *stream);
 
 /* kernel timing (HIP events recorded on the launch stream) */
 void  sgpu_prof_enable(int on);

@@ -586,3 +586,49 @@ def test_device_resident_multi_session(suite, torch_cuda):
             for x, y in zip(ea + da, eb + db):
                 assert (x == y).all(), mode
         assert A[1] == B[1] and A[2] == B[2], mode
+
+
+@pytest.mark.parametrize("suite", [1, 2, 5])
+@pytest.mark.parametrize("big", [False, True])
+def test_cached_size_boundary(suite, big, torch_cuda):
+    """packets either side of the compact kernels' size bound
+    (SGPU_CACHED_MAX_CTR = 4032 B: AES-CM caches rounds 1-2 only while the
+    keystream block index stays < 256, kern_common.h CTR_B15).  big=False:
+    every packet just under the bound, so the whole batch takes the
+    device-planned compact kernels; big=True: packets up to 9000 B, so the
+    batch goes to the plain kernels.  Device-resident and host-array APIs
+    against the oracle, both directions."""
+    torch = torch_cuda
+    rng = np.random.default_rng(1300 + suite + 7 * big)
+    key = keys_for(suite, 1)[0]
+    lens = ([4031 - 12, 4030 - 12, 3800, 4000 - 12, 4016 - 12] if not big
+            else [4032 - 12, 4033 - 12, 4095 - 12, 4096 - 12, 4100, 9000])
+    pkts = [(0, rtp_packet(rng, (65530 + i) & 0xffff, 0x4242,
+                           plen=lens[i % len(lens)])) for i in range(24)]
+    arena, pos, end, cap, _ = to_arena(pkts)
+    txa, txb = P.Srtp(suite, key), P.Srtp(suite, key)
+    a = run_dev(torch, "srtp_encrypt", [txa], arena, pos, end, cap, None)
+    b = run(torch, "srtp_encrypt", [txb], arena, pos, end, cap, None, False)
+    for x, y in zip(a, b):
+        assert (x == y).all()
+    be = O.OracleBackend()
+    octx = be.alloc(suite, key, 0)[0]
+    prot = []
+    for i, (_, p) in enumerate(pkts):
+        e, po, en, _, buf = be.call(octx, "srtp_encrypt", len(p) + 64, 0,
+                                    len(p), p, len(p) + 16)
+        assert (int(a[3][i]), int(a[2][i] - pos[i])) == (e, en), i
+        assert a[0][pos[i]:a[2][i]].tobytes() == buf[:en], (i, len(p))
+        prot.append((0, bytes(buf[:en])))
+    be.free(octx)
+    a2, p2, e2, c2, _ = to_arena(prot)
+    rxa, rxb = P.Srtp(suite, key), P.Srtp(suite, key)
+    da = run_dev(torch, "srtp_decrypt", [rxa], a2, p2, e2, c2, None)
+    db = run(torch, "srtp_decrypt", [rxb], a2, p2, e2, c2, None, False)
+    for x, y in zip(da, db):
+        assert (x == y).all()
+    assert not da[3].any()
+    for i in range(len(pkts)):
+        assert da[0][p2[i]:da[2][i]].tobytes() == pkts[i][1], i
+    for c in (txa, txb, rxa, rxb):
+        c.close()

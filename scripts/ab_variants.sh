@@ -5,5 +5,4 @@ for so in re_amd/lib/variants/*.so; do
   name=$(basename $so .so)
   RE_SRTP_LIB=$PWD/$so timeout -k 10 200 python bench.py --no-cpu-baseline --no-verify --steps 10 > gpurun_out/var_${name}_$rep.json 2> gpurun_out/var_$name.err || exit $?
 done
-RE_SRTP_PERCLASS=1 RE_SRTP_LIB=$PWD/re_amd/lib/variants/b15_1024.so timeout -k 10 200 python bench.py --no-cpu-baseline --no-verify --steps 10 > gpurun_out/var_perclass_$rep.json 2> gpurun_out/var_perclass.err || exit $?
 done

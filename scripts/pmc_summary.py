@@ -45,8 +45,10 @@ def main():
             continue
         args = [x.strip() for x in
                 name[name.index("<") + 1:name.index(">")].split(",")]
-        # k_ctr_hmac<NR, SHIFT, PROT, COMPACT, UNI>, k_gcm<NR, PROT, ...>
-        prot = args[2] if "k_ctr_hmac" in name else args[1]
+        # k_ctr_hmac<NR, SHIFT, PROT, COMPACT, UNI>,
+        # k_ctr_hmac_any<NR, PROT, UNI>, k_gcm<NR, PROT, ...>
+        prot = args[2] if ("k_ctr_hmac" in name and
+                           "k_ctr_hmac_any" not in name) else args[1]
         d = "protect" if prot == "true" else "unprotect"
         fb = 2.0 * sum(fv) / len(fv)
         wb = sum(wv) / len(wv)

@@ -321,20 +321,79 @@ k_mp_final(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
 }
 
 /*
- * Launch order of the crypto kernels: packets by descending number of
- * 64-byte chunks (key 255 - chunks, stable), so a wave's lanes carry
- * packets of about the same length -- with mixed 200/1400-B traffic
- * (config 4) a wave otherwise runs as long as its longest packet.
+ * Launch order of the crypto kernels: packets grouped by descending number
+ * of 64-byte chunks, so a wave's lanes carry packets of about the same
+ * length -- with mixed 200/1400-B traffic (config 4) a wave otherwise runs
+ * as long as its longest packet.  Only the grouping matters (any order
+ * inside a group is a valid launch order), so this is a two-launch
+ * counting sort: per-block LDS histograms folded into MP_OBINS global
+ * counts, then each block scatters its packets behind a range reserved
+ * with one global atomic per (block, bin).  Packets of >= MP_OBINS-1
+ * chunks share the last group (the cached kernels take < 4032 B anyway).
  */
-__global__ void k_mp_lenkey(const uint32_t *pos, const uint32_t *end,
-			    uint32_t *key, uint32_t n)
+#define MP_OBINS 64
+#define MP_OBLOCK 1024
+#define MP_OPER 4
+
+__device__ __forceinline__ uint32_t mp_obin(const uint32_t *pos,
+					    const uint32_t *end, uint32_t i)
 {
-	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
-	if (i >= n)
-		return;
 	const uint32_t L = end[i] >= pos[i] ? end[i] - pos[i] : 0u;
 	const uint32_t ch = (L + 63u) >> 6;
-	key[i] = 255u - (ch < 255u ? ch : 255u);
+	return (MP_OBINS - 1u) - (ch < MP_OBINS - 1u ? ch : MP_OBINS - 1u);
+}
+
+__global__ void __launch_bounds__(MP_OBLOCK)
+k_mp_ocount(const uint32_t *pos, const uint32_t *end, uint32_t *ghist,
+	    uint32_t n)
+{
+	__shared__ uint32_t h[MP_OBINS];
+	const uint32_t t = threadIdx.x;
+	if (t < MP_OBINS)
+		h[t] = 0;
+	__syncthreads();
+	for (uint32_t j = 0; j < MP_OPER; j++) {
+		const uint32_t i = blockIdx.x * (MP_OBLOCK * MP_OPER) +
+				   j * MP_OBLOCK + t;
+		if (i < n)
+			atomicAdd(&h[mp_obin(pos, end, i)], 1u);
+	}
+	__syncthreads();
+	if (t < MP_OBINS && h[t])
+		atomicAdd(&ghist[t], h[t]);
+}
+
+__global__ void __launch_bounds__(MP_OBLOCK)
+k_mp_oscatter(const uint32_t *pos, const uint32_t *end,
+	      const uint32_t *ghist, uint32_t *gcur, uint32_t *order,
+	      uint32_t n)
+{
+	__shared__ uint32_t h[MP_OBINS], base[MP_OBINS];
+	const uint32_t t = threadIdx.x;
+	uint32_t bin[MP_OPER], rank[MP_OPER];
+	if (t < MP_OBINS)
+		h[t] = 0;
+	__syncthreads();
+	for (uint32_t j = 0; j < MP_OPER; j++) {
+		const uint32_t i = blockIdx.x * (MP_OBLOCK * MP_OPER) +
+				   j * MP_OBLOCK + t;
+		bin[j] = i < n ? mp_obin(pos, end, i) : 0u;
+		rank[j] = i < n ? atomicAdd(&h[bin[j]], 1u) : 0u;
+	}
+	__syncthreads();
+	if (t < MP_OBINS && h[t]) {
+		uint32_t pre = 0;
+		for (uint32_t q = 0; q < t; q++)
+			pre += ghist[q];
+		base[t] = pre + atomicAdd(&gcur[t], h[t]);
+	}
+	__syncthreads();
+	for (uint32_t j = 0; j < MP_OPER; j++) {
+		const uint32_t i = blockIdx.x * (MP_OBLOCK * MP_OPER) +
+				   j * MP_OBLOCK + t;
+		if (i < n)
+			order[base[bin[j]] + rank[j]] = i;
+	}
 }
 
 /* ---- host side ------------------------------------------------------ */
@@ -409,17 +468,18 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 			   (const uint32_t *)segf, (const uint32_t *)segl,
 			   st_out, out);
 	if (order) {
-		/* crypto launch order (k_mp_lenkey); pex and kout are free
-		 * once k_mp_final has run, vin is still the identity */
-		size_t tb8 = mp_cub_bytes(n, 8);
-		if (tb8 > tb)
-			return EINVAL;
-		hipLaunchKernelGGL(k_mp_lenkey, dim3(nb), dim3(MP_BLOCK), 0, st,
-				   pos, end, pex, n);
-		if (hipcub::DeviceRadixSort::SortPairs(p, tb8, pex, kout, vin,
-						       order, (int)n, 0, 8,
-						       st) != hipSuccess)
+		/* crypto launch order; pex and kout are free once k_mp_final
+		 * has run (each >= 256 B: bin counts and cursors) */
+		const uint32_t ob = (n + MP_OBLOCK * MP_OPER - 1) /
+				    (MP_OBLOCK * MP_OPER);
+		if (hipMemsetAsync(pex, 0, MP_OBINS * 4, st) != hipSuccess ||
+		    hipMemsetAsync(kout, 0, MP_OBINS * 4, st) != hipSuccess)
 			return EIO;
+		hipLaunchKernelGGL(k_mp_ocount, dim3(ob), dim3(MP_OBLOCK), 0,
+				   st, pos, end, pex, n);
+		hipLaunchKernelGGL(k_mp_oscatter, dim3(ob), dim3(MP_OBLOCK), 0,
+				   st, pos, end, (const uint32_t *)pex, kout,
+				   order, n);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

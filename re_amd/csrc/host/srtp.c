@@ -22,6 +22,7 @@
  */
 #include <errno.h>
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -31,6 +32,7 @@
 #include "re_srtp.h"
 #include "re_srtp_batch.h"
 #include "../srtpgpu.h"
+#include "pool.h"
 
 #ifndef EAUTH
 #define EAUTH 217               /* include/re_types.h:215-217 */
@@ -1963,47 +1965,74 @@ static void plan_unapply(struct srtp *s, unsigned nstreams0,
 
 /* ---- multi-session device plan ----------------------------------------- */
 
+/* session passes run on the host pool from this many sessions per part
+ * (RE_SRTP_PAR_MIN overrides: tests drive the pool with few sessions) */
+static size_t mplan_par(void)
+{
+	const char *e = getenv("RE_SRTP_PAR_MIN");
+	long v = e ? atol(e) : 0;
+	return v > 0 ? (size_t)v : 4096;
+}
+
+struct mpg {
+	struct srtp **sessv;
+	struct sgpu_sstate *st;
+	const struct sgpu_sstate *o;
+	uint32_t *cm;
+	int suite, prot;
+	atomic_int bad;
+};
+
+static void mplan_gather_part(void *arg, size_t a, size_t b)
+{
+	struct mpg *g = arg;
+	size_t k;
+	for (k = a; k < b; k++) {
+		const struct srtp *s = g->sessv[k];
+		struct sgpu_sstate *st = &g->st[k];
+		if (k + 16 < b)
+			__builtin_prefetch(g->sessv[k + 16], 0, 1);
+		if (s->nstreams > 1 || s->suite != g->suite) {
+			atomic_store(&g->bad, 1);
+			return;
+		}
+		if (g->cm)
+			g->cm[k] = 2u * s->slot;        /* comp[0] = RTP */
+		memset(st, 0, sizeof(*st));
+		if (s->nstreams) {
+			const struct srtp_stream *x = &s->streams[0];
+			st->ssrc = x->ssrc;
+			st->roc = x->roc;
+			st->s_l = x->s_l;
+			st->flags = SST_EXISTS | (x->s_l_set ? SST_SL_SET : 0);
+			st->lix = x->replay_rtp.lix;
+			st->bitmap = x->replay_rtp.bitmap;
+		}
+	}
+}
+
 /* session states in (pinned) -> device; -1 if some session has 2+ streams */
 static int mplan_gather(struct srtp **sessv, size_t nsess,
 			struct sgpu_sstate *st, uint32_t *cm)
 {
-	const int suite = (int)sessv[0]->suite;
-	size_t k;
-	for (k = 0; k < nsess; k++) {
-		const struct srtp *s = sessv[k];
-		if (k + 16 < nsess)
-			__builtin_prefetch(sessv[k + 16], 0, 1);
-		if (s->nstreams > 1 || (int)s->suite != suite)
-			return -1;
-		if (cm)
-			cm[k] = 2u * s->slot;           /* comp[0] = RTP */
-		memset(&st[k], 0, sizeof(st[k]));
-		if (s->nstreams) {
-			const struct srtp_stream *x = &s->streams[0];
-			st[k].ssrc = x->ssrc;
-			st[k].roc = x->roc;
-			st[k].s_l = x->s_l;
-			st[k].flags = SST_EXISTS | (x->s_l_set ? SST_SL_SET : 0);
-			st[k].lix = x->replay_rtp.lix;
-			st[k].bitmap = x->replay_rtp.bitmap;
-		}
-	}
-	return 0;
+	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0};
+	par_for(nsess, mplan_par(), mplan_gather_part, &g);
+	return atomic_load(&g.bad) ? -1 : 0;
 }
 
-/* device results -> sessions (touched ones only) */
-static void mplan_apply(struct srtp **sessv, size_t nsess,
-			const struct sgpu_sstate *o, int prot)
+static void mplan_apply_part(void *arg, size_t a, size_t b)
 {
+	struct mpg *g = arg;
+	const struct sgpu_sstate *o = g->o;
 	size_t k;
-	for (k = 0; k < nsess; k++) {
+	for (k = a; k < b; k++) {
 		struct srtp *s;
 		struct srtp_stream *x;
-		if (k + 16 < nsess && (o[k + 16].flags & SST_TOUCHED))
-			__builtin_prefetch(sessv[k + 16], 1, 1);
+		if (k + 16 < b && (o[k + 16].flags & SST_TOUCHED))
+			__builtin_prefetch(g->sessv[k + 16], 1, 1);
 		if (!(o[k].flags & SST_TOUCHED))
 			continue;
-		s = sessv[k];
+		s = g->sessv[k];
 		if (!s->nstreams) {
 			memset(&s->streams[0], 0, sizeof(s->streams[0]));
 			s->nstreams = 1;
@@ -2013,11 +2042,19 @@ static void mplan_apply(struct srtp **sessv, size_t nsess,
 		x->roc = o[k].roc;
 		x->s_l = (uint16_t)o[k].s_l;
 		x->s_l_set = 1;
-		if (!prot) {
+		if (!g->prot) {
 			x->replay_rtp.lix = o[k].lix;
 			x->replay_rtp.bitmap = o[k].bitmap;
 		}
 	}
+}
+
+/* device results -> sessions (touched ones only) */
+static void mplan_apply(struct srtp **sessv, size_t nsess,
+			const struct sgpu_sstate *o, int prot)
+{
+	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0};
+	par_for(nsess, mplan_par(), mplan_apply_part, &g);
 }
 
 /* undo mplan_apply from the gathered pre-call states */

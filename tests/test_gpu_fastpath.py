@@ -550,13 +550,17 @@ def test_device_resident_multi_session(suite, torch_cuda):
                                  plen=int(rng.integers(0, 400)))))
     batches.append(nb)
     res = {}
-    for mode in ("dev", "host", "general"):
+    # dev_par: the session gather/apply passes split over the host pool
+    # (RE_SRTP_PAR_MIN=4 -> parts of >= 4 sessions)
+    for mode in ("dev", "dev_par", "host", "general"):
         tx = [P.Srtp(suite, k) for k in keys]
         rx = [P.Srtp(suite, k) for k in keys]
         outs = []
+        if mode == "dev_par":
+            os.environ["RE_SRTP_PAR_MIN"] = "4"
         for bi, pk in enumerate(batches):
             arena, pos, end, cap, sess = to_arena(pk)
-            if mode == "dev":
+            if mode.startswith("dev"):
                 enc = run_dev(torch, "srtp_encrypt", tx, arena, pos, end,
                               cap, sess)
             else:
@@ -569,18 +573,19 @@ def test_device_resident_multi_session(suite, torch_cuda):
                 q[-2] ^= 0x08
                 prot[321] = (prot[321][0], bytes(q))
             a2, p2, e2, c2, s2 = to_arena(prot)
-            if mode == "dev":
+            if mode.startswith("dev"):
                 dec = run_dev(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2)
             else:
                 dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
                           mode == "general")
             outs.append((enc, dec))
+        os.environ.pop("RE_SRTP_PAR_MIN", None)
         res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
         for c in tx + rx:
             c.close()
     A = res["dev"]
     assert int(A[0][1][1][3][321]) == P.EAUTH
-    for mode in ("host", "general"):
+    for mode in ("dev_par", "host", "general"):
         B = res[mode]
         for (ea, da), (eb, db) in zip(A[0], B[0]):
             for x, y in zip(ea + da, eb + db):

@@ -70,11 +70,20 @@ __device__ __forceinline__ bool mp_first(const mp_ctx &c, uint32_t k)
 	return k == 0 || c.key[k - 1] != c.key[k];
 }
 
-__global__ void k_mp_iota(uint32_t *v, uint32_t n)
+/* sort input: identity values, and the session keys clamped -- an index
+ * >= nsess fails the plan (SPF_BAD) and is sorted as session nsess-1, so
+ * every later table access (st, segf, segl) stays in bounds */
+__global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, uint32_t *kin,
+			  uint32_t n, uint32_t nsess, struct sgpu_plan_out *out)
 {
 	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
-	if (i < n)
+	if (i < n) {
+		const uint32_t s = sess[i];
+		if (s >= nsess)
+			atomicOr(&out->fail, (uint32_t)SPF_BAD);
 		v[i] = i;
+		kin[i] = s < nsess ? s : nsess - 1u;
+	}
 }
 
 __global__ void __launch_bounds__(MP_BLOCK)
@@ -448,8 +457,10 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 	    hipMemsetAsync(segl, 0xff, (size_t)in->nsess * 4, st) !=
 	    hipSuccess)
 		return EIO;
-	hipLaunchKernelGGL(k_mp_iota, dim3(nb), dim3(MP_BLOCK), 0, st, vin, n);
-	if (hipcub::DeviceRadixSort::SortPairs(p, tb, sess, kout, vin, vout,
+	/* pex is free until k_mp_mark: the clamped keys */
+	hipLaunchKernelGGL(k_mp_iota, dim3(nb), dim3(MP_BLOCK), 0, st, vin, sess,
+			   pex, n, in->nsess, out);
+	if (hipcub::DeviceRadixSort::SortPairs(p, tb, pex, kout, vin, vout,
 					       (int)n, 0, (int)in->key_bits,
 					       st) != hipSuccess)
 		return EIO;

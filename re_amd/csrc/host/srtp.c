@@ -2838,6 +2838,8 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	size_t scr;
 	void *stream = d->stream;
 	struct ws *w = ws_get();
+	const int times = getenv("RE_SRTP_TIMES") != NULL;
+	double t[4];
 	int err;
 
 	if (!w)
@@ -2878,8 +2880,10 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	sout_d = sin_d + nsess;
 	order_d = (uint32_t *)(w->mscr.d + scr);
 	/* one pass over the sessions: suite check, stream state, slot map */
+	t[0] = times ? now_ms() : 0;
 	if (mplan_gather(sessv, nsess, sin_h, cm_h))
 		return -1;
+	t[1] = times ? now_ms() : 0;
 
 	memset(&in, 0, sizeof(in));
 	in.n = (uint32_t)n;
@@ -2925,13 +2929,20 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 				      nsess * sizeof(struct sgpu_sstate), stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+	t[2] = times ? now_ms() : 0;
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
 	if (po->fail)
 		return -1;
+	t[3] = times ? now_ms() : 0;
 	mplan_apply(sessv, nsess, sout_h, prot);
+	if (times)
+		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu: gather %.3f "
+			"submit %.3f wait %.3f apply %.3f ms\n", n, nsess,
+			t[1] - t[0], t[2] - t[1], t[3] - t[2],
+			now_ms() - t[3]);
 	if (!nfail)
 		return 0;
 	/* a forged packet: undo on the device, fold on the host engine */

@@ -637,3 +637,88 @@ def test_cached_size_boundary(suite, big, torch_cuda):
         assert da[0][p2[i]:da[2][i]].tobytes() == pkts[i][1], i
     for c in (txa, txb, rxa, rxb):
         c.close()
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+@pytest.mark.parametrize("shape", ["skewed", "few_sessions", "bad_session"])
+def test_multi_session_shapes(suite, shape, torch_cuda):
+    """multi-session device plan (plan_multi.hip) over session shapes:
+    one session far longer than the rest (skewed), few long sessions
+    (few_sessions) -- srtp_*_batch_dev results and final stream states
+    equal the general engine's -- and an out-of-range session index
+    (bad_session: the device plan fails with every sort key clamped in
+    bounds, the staged path rejects the call with EINVAL)"""
+    torch = torch_cuda
+    rng = np.random.default_rng(1234 + suite)
+    nsess = {"skewed": 64, "few_sessions": 3, "bad_session": 40}[shape]
+    n = {"skewed": 3000, "few_sessions": 1500, "bad_session": 800}[shape]
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    pk = multi_session_traffic(rng, n, nsess, s0=65300)
+    if shape == "skewed":     # session 5 gets 400 extra packets
+        for j in range(400):
+            pk.insert(int(rng.integers(0, len(pk))),
+                      (5, None))
+        out, seqs = [], {}
+        for s, p in pk:       # renumber every session in array order
+            q = seqs.get(s, 65300)
+            seqs[s] = (q + 1) & 0xffff
+            out.append((s, rtp_packet(rng, q, 0x7000 + s,
+                                      plen=int(rng.integers(0, 300)))))
+        pk = out
+    if shape == "bad_session":
+        # the device plan fails (SPF_BAD, every key clamped so the plan's
+        # reads stay in bounds) and the staged path rejects the call
+        # with EINVAL before touching any state -- for both sorts
+        for _ in range(2):
+            tx = [P.Srtp(suite, k) for k in keys]
+            arena, pos, end, cap, sess = to_arena(pk)
+            sess = sess.copy()
+            sess[17] = nsess + 3
+            dev = torch.from_numpy(arena.copy()).cuda()
+            i32 = lambda a: torch.from_numpy(
+                np.asarray(a, dtype=np.uint32).view(np.int32)).cuda()
+            p, e, c, sd = i32(pos), i32(end), i32(cap), i32(sess)
+            er = torch.full((len(pos),), -1, dtype=torch.int32,
+                            device="cuda")
+            torch.cuda.synchronize()
+            rc = P.device_batch_dev("srtp_encrypt", tx, dev.data_ptr(),
+                                    arena.nbytes, p.data_ptr(),
+                                    e.data_ptr(), c.data_ptr(),
+                                    er.data_ptr(), len(pos), sd.data_ptr())
+            torch.cuda.synchronize()
+            assert rc == errno.EINVAL, rc
+            assert (dev.cpu().numpy() == arena).all()
+            # no stream was created (export fails for every SSRC)
+            assert all(len(x) == 1 for x in states(tx, ssrcs))
+            for t in tx:
+                t.close()
+        return
+    res = {}
+    for mode in ("dev", "general"):
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        arena, pos, end, cap, sess = to_arena(pk)
+        if mode == "general":
+            enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap,
+                      sess, True)
+        else:
+            enc = run_dev(torch, "srtp_encrypt", tx, arena, pos, end, cap,
+                          sess)
+        prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
+                for i, (s, _) in enumerate(pk)]
+        a2, p2, e2, c2, s2 = to_arena(prot)
+        if mode == "general":
+            dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2, True)
+        else:
+            dec = run_dev(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2)
+        assert not dec[3].any()
+        res[mode] = ((enc, dec), states(tx, ssrcs), states(rx, ssrcs))
+        for c in tx + rx:
+            c.close()
+    A = res["general"]
+    for mode in ("dev",):
+        B = res[mode]
+        for x, y in zip(A[0][0] + A[0][1], B[0][0] + B[0][1]):
+            assert (x == y).all(), mode
+        assert A[1] == B[1] and A[2] == B[2], mode

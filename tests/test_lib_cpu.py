@@ -74,3 +74,26 @@ def test_mbuf_growth_policy():
     assert L.mbuf_write_mem(mb, b"\x03" * 30, 30) == 0
     assert mb.contents.size == 50          # MAX(50, 40)
     P.free_mbuf(mb)
+
+
+def test_host_pool_covers_every_range_once():
+    """par_for (re_amd/csrc/host/pool.c, the worker pool of the
+    multi-session gather/apply passes): over many back-to-back jobs of
+    varying size every index is visited exactly once"""
+    import numpy as np
+    L = P.load()
+    FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t,
+                          ctypes.c_size_t)
+    L.par_for.argtypes = [ctypes.c_size_t, ctypes.c_size_t, FN,
+                          ctypes.c_void_p]
+    L.par_for.restype = None
+    for n, min_per in ((1, 1), (7, 1), (100, 3), (5000, 64), (40000, 4096),
+                       (3, 0), (64, 8)):
+        seen = np.zeros(n, dtype=np.int64)
+
+        def part(_arg, a, b, seen=seen):
+            seen[a:b] += 1
+
+        cb = FN(part)
+        L.par_for(n, min_per, cb, None)
+        assert (seen == 1).all(), (n, min_per)

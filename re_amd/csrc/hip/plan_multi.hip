@@ -52,6 +52,9 @@ struct mp_ctx {
 	const struct sgpu_hdr *hdr;
 	const struct sgpu_sstate *st;
 	uint32_t n;
+	/* seq and SSRC in sorted order, written by k_mp_count: the later
+	 * passes read neighbours contiguously instead of through val[] */
+	uint32_t *sseq, *sssrc;
 };
 
 /* s_l seen by sorted position k of the segment starting at f */
@@ -60,9 +63,9 @@ __device__ __forceinline__ uint32_t mp_sb(const mp_ctx &c, uint32_t k,
 {
 	if (k == f) {
 		const struct sgpu_sstate &S = c.st[c.key[k]];
-		return (S.flags & SST_SL_SET) ? S.s_l : c.hdr[c.val[k]].seq;
+		return (S.flags & SST_SL_SET) ? S.s_l : c.sseq[k];
 	}
-	return c.hdr[c.val[k - 1]].seq;
+	return c.sseq[k - 1];
 }
 
 __device__ __forceinline__ bool mp_first(const mp_ctx &c, uint32_t k)
@@ -92,18 +95,32 @@ k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
 	   uint32_t *bcnt, struct sgpu_plan_out *out)
 {
 	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u;
 	bool wrap = false;
 	uint32_t f = 0;
+	/* the previous sorted position's header: from the lane below, a
+	 * gather only at lane 0 */
+	struct sgpu_hdr h = {0, 0, 0, 0};
+	if (k < in.n)
+		h = c.hdr[c.val[k]];
+	uint32_t pseq = (uint32_t)__shfl_up((int)h.seq, 1);
+	uint32_t pssrc = (uint32_t)__shfl_up((int)h.ssrc, 1);
+	if (lane == 0 && k > 0 && k < in.n) {
+		const struct sgpu_hdr hp = c.hdr[c.val[k - 1]];
+		pseq = hp.seq;
+		pssrc = hp.ssrc;
+	}
 	if (k < in.n) {
 		const uint32_t i = c.val[k], s = c.key[k];
 		const bool first = mp_first(c, k);
 		const bool last = k + 1 == in.n || c.key[k + 1] != s;
-		const struct sgpu_hdr h = c.hdr[i];
 		const uint32_t hl0 = c.hdr[0].hdr_len;
+		c.sseq[k] = h.seq;
+		c.sssrc[k] = h.ssrc;
 		const struct sgpu_sstate S = c.st[s];
 		const uint32_t seq = h.seq;
 		const uint32_t sb = first ? ((S.flags & SST_SL_SET) ? S.s_l : seq)
-					  : c.hdr[c.val[k - 1]].seq;
+					  : pseq;
 		if (s >= in.nsess)
 			f |= SPF_BAD;
 		if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
@@ -112,7 +129,7 @@ k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
 			f |= SPF_CLASS;
 		/* one SSRC per session: the stored one, or the segment's */
 		if (first ? ((S.flags & SST_EXISTS) && h.ssrc != S.ssrc)
-			  : h.ssrc != c.hdr[c.val[k - 1]].ssrc)
+			  : h.ssrc != pssrc)
 			f |= SPF_SSRC;
 		if (!in.prot && h.hdr_len != 0xffffffffu &&
 		    end[i] - pos[i] - h.hdr_len < in.tag)
@@ -179,9 +196,8 @@ k_mp_mark(mp_ctx c, const uint32_t *bpre, uint32_t *pex, uint32_t *segf,
 		first = mp_first(c, k);
 		last = k + 1 == c.n || c.key[k + 1] != c.key[k];
 		/* the segment start is only needed for k == f */
-		const uint32_t sb = first ? mp_sb(c, k, k)
-					  : c.hdr[c.val[k - 1]].seq;
-		wrap = mp_wrap(c.hdr[c.val[k]].seq, sb);
+		const uint32_t sb = first ? mp_sb(c, k, k) : c.sseq[k - 1];
+		wrap = mp_wrap(c.sseq[k], sb);
 	}
 	const uint64_t m = __ballot(wrap);
 	if (lane == 0)
@@ -208,10 +224,10 @@ __device__ __forceinline__ uint64_t mp_ix(const mp_ctx &c,
 					  uint32_t *sbp)
 {
 	const struct sgpu_sstate &S = c.st[c.key[k]];
-	const uint32_t seq = c.hdr[c.val[k]].seq;
+	const uint32_t seq = c.sseq[k];
 	const uint32_t sb = mp_sb(c, k, f);
 	const bool wrap = mp_wrap(seq, sb);
-	const uint32_t fseq = c.hdr[c.val[f]].seq;
+	const uint32_t fseq = c.sseq[f];
 	const bool wf = mp_wrap(fseq, mp_sb(c, f, f));
 	/* ROC after this packet's own rollover */
 	const uint32_t roc = S.roc + (pex[k] + (wrap ? 1u : 0u)) -
@@ -295,8 +311,8 @@ k_mp_final(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
 	uint32_t roc, sb;
 	bool wrap;
 	(void)mp_ix(c, in, pex, l, f, NULL, &roc, &wrap, &sb);
-	const uint32_t seq = c.hdr[c.val[l]].seq;
-	o.ssrc = (S.flags & SST_EXISTS) ? S.ssrc : c.hdr[c.val[f]].ssrc;
+	const uint32_t seq = c.sseq[l];
+	o.ssrc = (S.flags & SST_EXISTS) ? S.ssrc : c.sssrc[f];
 	o.roc = roc;
 	o.s_l = wrap ? seq : (seq > sb ? seq : sb);
 	o.flags = SST_EXISTS | SST_SL_SET | SST_TOUCHED;
@@ -425,7 +441,7 @@ static size_t mp_cub_bytes(uint32_t n, uint32_t bits)
 extern "C" size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess)
 {
 	const uint32_t nb = (n + MP_BLOCK - 1) / MP_BLOCK;
-	return 4 * mp_align((size_t)n * 4) + mp_align((size_t)nb * 4 + 64) +
+	return 6 * mp_align((size_t)n * 4) + mp_align((size_t)nb * 4 + 64) +
 	       2 * mp_align((size_t)nsess * 4) + mp_align(mp_cub_bytes(n, 32));
 }
 
@@ -446,6 +462,8 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 	uint32_t *vin = (uint32_t *)p;   p += mp_align((size_t)n * 4);
 	uint32_t *vout = (uint32_t *)p;  p += mp_align((size_t)n * 4);
 	uint32_t *pex = (uint32_t *)p;   p += mp_align((size_t)n * 4);
+	uint32_t *sseq = (uint32_t *)p;  p += mp_align((size_t)n * 4);
+	uint32_t *sssrc = (uint32_t *)p; p += mp_align((size_t)n * 4);
 	uint32_t *bcnt = (uint32_t *)p;  p += mp_align((size_t)nb * 4 + 64);
 	uint32_t *segf = (uint32_t *)p;  p += mp_align((size_t)in->nsess * 4);
 	uint32_t *segl = (uint32_t *)p;  p += mp_align((size_t)in->nsess * 4);
@@ -464,7 +482,7 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 					       (int)n, 0, (int)in->key_bits,
 					       st) != hipSuccess)
 		return EIO;
-	mp_ctx c = {kout, vout, hdr, st_in, n};
+	mp_ctx c = {kout, vout, hdr, st_in, n, sseq, sssrc};
 	hipLaunchKernelGGL(k_mp_count, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
 			   pos, end, cap, arena_size, bcnt, out);
 	hipLaunchKernelGGL(k_mp_scan, dim3(1), dim3(1024), 0, st, bcnt, nb);

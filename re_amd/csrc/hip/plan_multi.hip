@@ -76,7 +76,8 @@ __device__ __forceinline__ bool mp_first(const mp_ctx &c, uint32_t k)
 /* sort input: identity values, and the session keys clamped -- an index
  * >= nsess fails the plan (SPF_BAD) and is sorted as session nsess-1, so
  * every later table access (st, segf, segl) stays in bounds */
-__global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, uint32_t *kin,
+template <typename K>
+__global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, K *kin,
 			  uint32_t n, uint32_t nsess, struct sgpu_plan_out *out)
 {
 	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
@@ -85,8 +86,16 @@ __global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, uint32_t *kin,
 		if (s >= nsess)
 			atomicOr(&out->fail, (uint32_t)SPF_BAD);
 		v[i] = i;
-		kin[i] = s < nsess ? s : nsess - 1u;
+		kin[i] = (K)(s < nsess ? s : nsess - 1u);
 	}
+}
+
+/* sorted 16-bit keys -> the 32-bit key array the planner passes read */
+__global__ void k_mp_widen(const uint16_t *k16, uint32_t *k32, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (i < n)
+		k32[i] = k16[i];
 }
 
 __global__ void __launch_bounds__(MP_BLOCK)
@@ -428,14 +437,22 @@ static size_t mp_align(size_t x)
 	return (x + 255) & ~(size_t)255;
 }
 
+/* up to 65536 sessions the keys sort as uint16_t: rocPRIM then takes its
+ * onesweep radix sort for more than 100K items (device_radix_sort.hpp:
+ * 2-byte keys skip the merge-sort path, ~20 launches for 1M items) */
 static size_t mp_cub_bytes(uint32_t n, uint32_t bits)
 {
-	size_t tb = 0;
+	size_t tb = 0, t16 = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(
 		(void *)NULL, tb, (const uint32_t *)NULL, (uint32_t *)NULL,
 		(const uint32_t *)NULL, (uint32_t *)NULL, (int)n, 0,
 		(int)bits);
-	return tb;
+	if (bits <= 16)
+		(void)hipcub::DeviceRadixSort::SortPairs(
+			(void *)NULL, t16, (const uint16_t *)NULL,
+			(uint16_t *)NULL, (const uint32_t *)NULL,
+			(uint32_t *)NULL, (int)n, 0, (int)bits);
+	return tb > t16 ? tb : t16;
 }
 
 extern "C" size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess)
@@ -475,13 +492,29 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 	    hipMemsetAsync(segl, 0xff, (size_t)in->nsess * 4, st) !=
 	    hipSuccess)
 		return EIO;
-	/* pex is free until k_mp_mark: the clamped keys */
-	hipLaunchKernelGGL(k_mp_iota, dim3(nb), dim3(MP_BLOCK), 0, st, vin, sess,
-			   pex, n, in->nsess, out);
-	if (hipcub::DeviceRadixSort::SortPairs(p, tb, pex, kout, vin, vout,
-					       (int)n, 0, (int)in->key_bits,
-					       st) != hipSuccess)
-		return EIO;
+	/* pex is free until k_mp_mark (the clamped keys), sseq until
+	 * k_mp_count (sorted 16-bit keys) */
+	if (in->nsess <= 65536 && in->key_bits <= 16) {
+		uint16_t *k16 = (uint16_t *)pex, *o16 = (uint16_t *)sseq;
+		hipLaunchKernelGGL(k_mp_iota<uint16_t>, dim3(nb), dim3(MP_BLOCK),
+				   0, st, vin, sess, k16, n, in->nsess, out);
+		if (hipcub::DeviceRadixSort::SortPairs(p, tb, k16, o16, vin,
+						       vout, (int)n, 0,
+						       (int)in->key_bits,
+						       st) != hipSuccess)
+			return EIO;
+		hipLaunchKernelGGL(k_mp_widen, dim3(nb), dim3(MP_BLOCK), 0, st,
+				   (const uint16_t *)o16, kout, n);
+	}
+	else {
+		hipLaunchKernelGGL(k_mp_iota<uint32_t>, dim3(nb), dim3(MP_BLOCK),
+				   0, st, vin, sess, pex, n, in->nsess, out);
+		if (hipcub::DeviceRadixSort::SortPairs(p, tb, pex, kout, vin,
+						       vout, (int)n, 0,
+						       (int)in->key_bits,
+						       st) != hipSuccess)
+			return EIO;
+	}
 	mp_ctx c = {kout, vout, hdr, st_in, n, sseq, sssrc};
 	hipLaunchKernelGGL(k_mp_count, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
 			   pos, end, cap, arena_size, bcnt, out);

@@ -23,6 +23,7 @@ static pthread_mutex_t p_lock = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t p_wake = PTHREAD_COND_INITIALIZER;
 static pthread_once_t p_once = PTHREAD_ONCE_INIT;
 static int p_nthr;                      /* workers started */
+static long p_spin = 5000;              /* pause loops before sleeping */
 /* job parameters: written by par_for under p_lock while no worker is
  * inside a job (p_active == 0), read by workers that entered under
  * p_lock with the current generation */
@@ -59,8 +60,8 @@ static void *worker(void *arg)
 	unsigned long seen = 0;
 	for (;;) {
 		/* spin a little before sleeping: batches come back to back */
-		int spin;
-		for (spin = 0; spin < 100000 && atomic_load(&p_pub) == seen;
+		long spin;
+		for (spin = 0; spin < p_spin && atomic_load(&p_pub) == seen;
 		     spin++)
 			__builtin_ia32_pause();
 		pthread_mutex_lock(&p_lock);
@@ -78,8 +79,11 @@ static void *worker(void *arg)
 static void pool_start(void)
 {
 	const char *e = getenv("RE_SRTP_THREADS");
+	const char *sp = getenv("RE_SRTP_SPIN");
 	long want = e ? atol(e) : 8;
 	int i;
+	if (sp)
+		p_spin = atol(sp);
 	if (want > POOL_MAX)
 		want = POOL_MAX;
 	for (i = 0; i + 1 < want; i++) {

@@ -2879,6 +2879,16 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	sout_h = sin_h + nsess;
 	sout_d = sin_d + nsess;
 	order_d = (uint32_t *)(w->mscr.d + scr);
+	/* parse + end copy (the kernels keep reading the input windows) +
+	 * zeroed miss counter, one launch; it runs while the host gathers */
+	{
+		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0};
+		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
+					  d->end, hd_d, NULL, (uint32_t)n, 0,
+					  &pro, stream);
+		if (err)
+			return err;
+	}
 	/* one pass over the sessions: suite check, stream state, slot map */
 	t[0] = times ? now_ms() : 0;
 	if (mplan_gather(sessv, nsess, sin_h, cm_h))
@@ -2897,14 +2907,6 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (!err)
 		err = sgpu_memcpy_h2d(sin_d, sin_h,
 				      nsess * sizeof(struct sgpu_sstate), stream);
-	if (!err) {
-		/* parse + end copy (the kernels keep reading the input
-		 * windows) + zeroed miss counter, one launch */
-		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0};
-		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
-					  d->end, hd_d, NULL, (uint32_t)n, 0,
-					  &pro, stream);
-	}
 	if (!err)
 		err = sgpu_mplan_rtp(&in, hd_d, d->pos, es_d, d->cap,
 				     d->arena_size, d->sess, sin_d, sout_d,

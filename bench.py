@@ -137,6 +137,14 @@ def main():
                                     device_id=torch.device("cuda", gpu))
     dev = torch.device("cuda", gpu)
     P.load()
+    tstart = time.perf_counter()
+
+    def log(msg):
+        # phase progress on stderr (the JSON line stays alone on stdout)
+        print("[bench rank %d/%d %.1fs] %s" % (rank, world,
+                                              time.perf_counter() - tstart,
+                                              msg),
+              file=sys.stderr, flush=True)
 
     n, suite, nsess = cfg["n"], cfg["suite"], cfg["nsess"]
     s0 = 65000
@@ -146,6 +154,7 @@ def main():
     sess = W.random_sessions(n, nsess) if nsess > 1 else None
     arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
                                           sess=sess)
+    log("workload built (%d packets)" % n)
     arena = torch.from_numpy(arena_h).to(dev)
     plain = arena.clone() if not args.no_verify else None
     klen = P.key_len(suite) + P.salt_len(suite)
@@ -262,6 +271,7 @@ def main():
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
         return np.count_nonzero(err_e) + np.count_nonzero(err_d)
 
+    log("arena resident, warmup")
     # ---- warmup (untimed) ----
     for _ in range(args.warmup):
         tx, rx = make_sessions()
@@ -272,6 +282,7 @@ def main():
     # the C session pointer arrays are built once per set (not timed);
     # the Srtp handles stay alive until the end (they own the sessions)
     sess_objs = [make_sessions() for _ in range(args.steps)]
+    log("warmup done, timed steps")
     sess_sets = [(P.session_array(tx), P.session_array(rx))
                  for tx, rx in sess_objs]
     P.prof_enable(True)
@@ -297,6 +308,11 @@ def main():
     counters = torch.tensor([n * args.steps, rtp_bytes * args.steps, errors],
                             dtype=torch.float64, device=dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    log("timed steps done")
+    if os.environ.get("BENCH_WATCHDOG"):
+        import faulthandler
+        faulthandler.dump_traceback_later(
+            float(os.environ["BENCH_WATCHDOG"]), exit=False)
     S.reduce_results(dist if world > 1 else None, counters, tmax)
     tot_pkts, tot_bytes, tot_err = [float(x) for x in counters.tolist()]
     T = float(tmax.item())
@@ -309,9 +325,13 @@ def main():
         lens = torch.from_numpy((end - pos).astype(np.int64)).to(dev)
         win = torch.arange(slot, device=dev)[None, :] < lens[:, None]
         a2, p2 = arena.view(n, slot), plain.view(n, slot)
-        verified = bool(torch.equal(a2[win], p2[win])) and tot_err == 0
+        # elementwise compare + count: no boolean-mask gather (its
+        # index tensor is ~10 GB at 1M packets and slow to build)
+        bad = int(torch.count_nonzero((a2 != p2) & win).item())
+        verified = bad == 0 and tot_err == 0
         del win, a2, p2
 
+    log("verified")
     for tx, rx in sess_objs:
         for s in tx + rx:
             s.close()

@@ -2783,12 +2783,15 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 					prot ? (int32_t)T : -(int32_t)T, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	/* the miss count lands in pinned memory next to the plan (a
+	 * pageable destination would stage the copy through the runtime) */
 	if (!err)
-		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
+	nfail = *(const uint32_t *)(po + 1);
 	if (po->fail)
 		return -1;
 	plan_apply(s, po, prot, n, &old);
@@ -2855,7 +2858,8 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (!err)
 		err = pool_reserve(w, &w->cm, nsess * 4);
 	if (!err)
-		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out));
+		err = pool_reserve(w, &w->pl,
+				   sizeof(struct sgpu_plan_out) + 64);
 	if (!err)
 		err = pool_reserve(w, &w->es, n * 4);
 	if (!err)
@@ -2929,13 +2933,14 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (!err)
 		err = sgpu_memcpy_d2h(sout_h, sout_d,
 				      nsess * sizeof(struct sgpu_sstate), stream);
-	if (!err)
-		err = sgpu_memcpy_d2h(&nfail, nfail_d, 4, stream);
+	if (!err)   /* pinned, next to the plan (see dev_planned) */
+		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	t[2] = times ? now_ms() : 0;
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
+	nfail = *(const uint32_t *)(po + 1);
 	if (po->fail)
 		return -1;
 	t[3] = times ? now_ms() : 0;

@@ -1,0 +1,276 @@
+/*
+ * ref_digest.c -- whole-arena reference digests (TEST INFRASTRUCTURE ONLY).
+ *
+ * Linked against the reference src/srtp compiled by oracle/Makefile
+ * (target `ref`, the image's libcrypto).  For a BASELINE.json config it
+ * rebuilds the exact packet arena re_amd/workload.py builds (same
+ * xorshift64* generators, same slot layout), runs the reference
+ * srtp_encrypt (src/srtp/srtp.c:183-285) over every packet in array order,
+ * then srtp_decrypt (srtp.c:288-432) of the protected arena with fresh
+ * receiver contexts, and prints SHA-256 digests of the arena, the end
+ * array, the per-packet errnos and the final stream states after each
+ * direction.  tests/golden/fullsize_digests.json is this program's output
+ * for configs 1-4 (scripts/make_fullsize_digests.sh); the -m gpu tests
+ * compare the HIP path's full-size outputs with it.
+ *
+ *   ref_digest <config> [npkts]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <openssl/sha.h>
+#include <re.h>
+#include "srtp.h"               /* reference src/srtp/srtp.h (stream state) */
+
+#define GOLDEN 0x9E3779B97F4A7C15ull
+#define SEED_PAYLOAD 0x5EED5EEDull
+#define SEED_KEYS 0xC0FFEEull
+#define SSRC_BASE 0x01020304u
+#define BLOCK_PKTS 65536u
+
+static const size_t keylen[6]  = {16, 16, 32, 32, 16, 32};
+static const size_t saltlen[6] = {14, 14, 14, 14, 12, 12};
+
+static uint64_t xs(uint64_t *s)
+{
+	*s ^= *s >> 12;
+	*s ^= *s << 25;
+	*s ^= *s >> 27;
+	return *s * 0x2545F4914F6CDD1Dull;
+}
+
+static uint64_t xs_init(uint64_t seed, uint64_t i)
+{
+	uint64_t s = seed ^ (GOLDEN * (i + 1));
+	return s ? s : GOLDEN;
+}
+
+/* LE bytes of generator i's outputs (workload.py xs_bytes) */
+static void xs_fill(uint8_t *out, size_t n, uint64_t seed, uint64_t i)
+{
+	uint64_t s = xs_init(seed, i);
+	size_t o;
+	for (o = 0; o < n; o += 8) {
+		uint64_t v = xs(&s);
+		uint8_t b[8];
+		int k;
+		for (k = 0; k < 8; k++)
+			b[k] = (uint8_t)(v >> (8 * k));
+		memcpy(out + o, b, n - o < 8 ? n - o : 8);
+	}
+}
+
+struct cfg {
+	int suite;
+	size_t n;
+	size_t length;          /* 0: mixed 200/1400 */
+	size_t nsess;
+	unsigned s0;
+	int test_key;
+};
+
+static const struct cfg CFG[5] = {
+	{0, 0, 0, 0, 0, 0},
+	{1, 1024, 160, 1, 1, 1},
+	{1, 1u << 20, 1200, 1, 65000, 0},
+	{5, 1u << 20, 1200, 1, 65000, 0},
+	{1, 1u << 20, 0, 1u << 16, 65000, 0},
+};
+
+static void hex(const uint8_t *p, size_t n)
+{
+	size_t i;
+	putchar('"');
+	for (i = 0; i < n; i++)
+		printf("%02x", p[i]);
+	putchar('"');
+}
+
+static void sha(const void *p, size_t n)
+{
+	uint8_t md[32];
+	SHA256(p, n, md);
+	hex(md, 32);
+}
+
+/* per session: roc u32, s_l u32, replay_rtp lix u64, bitmap u64 (LE) */
+static void states(struct srtp **ctx, size_t nsess, uint32_t ssrc0,
+		   uint8_t *buf)
+{
+	size_t k;
+	for (k = 0; k < nsess; k++) {
+		struct srtp_stream *st = NULL;
+		uint8_t *o = buf + 24 * k;
+		struct le *le;
+		memset(o, 0, 24);
+		for (le = ctx[k]->streaml.head; le; le = le->next) {
+			struct srtp_stream *x = le->data;
+			if (x->ssrc == ssrc0 + (uint32_t)k)
+				st = x;
+		}
+		if (!st)
+			continue;
+		memcpy(o, &st->roc, 4);
+		{
+			uint32_t sl = st->s_l;
+			memcpy(o + 4, &sl, 4);
+		}
+		memcpy(o + 8, &st->replay_rtp.lix, 8);
+		memcpy(o + 16, &st->replay_rtp.bitmap, 8);
+	}
+}
+
+static void emit(const char *name, const uint8_t *arena, size_t n,
+		 size_t slot, const uint32_t *end, const int32_t *err,
+		 struct srtp **ctx, size_t nsess, uint8_t *stbuf)
+{
+	size_t b, nerr = 0, i;
+	for (i = 0; i < n; i++)
+		nerr += err[i] != 0;
+	printf(",\"%s\":{\"arena\":", name);
+	sha(arena, n * slot);
+	printf(",\"blocks\":[");
+	for (b = 0; b * BLOCK_PKTS < n; b++) {
+		size_t m = n - b * BLOCK_PKTS < BLOCK_PKTS ? n - b * BLOCK_PKTS
+							   : BLOCK_PKTS;
+		if (b)
+			putchar(',');
+		sha(arena + b * BLOCK_PKTS * slot, m * slot);
+	}
+	printf("],\"end\":");
+	sha(end, n * 4);
+	printf(",\"err\":");
+	sha(err, n * 4);
+	printf(",\"nerr\":%zu,\"states\":", nerr);
+	states(ctx, nsess, SSRC_BASE, stbuf);
+	sha(stbuf, 24 * nsess);
+	if (nsess == 1) {
+		printf(",\"state0\":");
+		hex(stbuf, 24);
+	}
+	printf(",\"pkt0\":");
+	hex(arena, end[0]);
+	printf(",\"pktN\":");
+	hex(arena + (n - 1) * slot, end[n - 1] - (n - 1) * slot);
+	printf("}");
+}
+
+int main(int argc, char **argv)
+{
+	int c = argc > 1 ? atoi(argv[1]) : 0;
+	struct cfg cf;
+	size_t n, slot, maxlen, i, klen;
+	uint8_t *arena, *keys, *stbuf;
+	uint32_t *pos, *end, *len, *sess, *cnt;
+	int32_t *err;
+	struct srtp **tx, **rx;
+
+	if (c < 1 || c > 4) {
+		fprintf(stderr, "usage: %s <config 1-4> [npkts]\n", argv[0]);
+		return 2;
+	}
+	cf = CFG[c];
+	n = argc > 2 ? (size_t)atol(argv[2]) : cf.n;
+	klen = keylen[cf.suite] + saltlen[cf.suite];
+	maxlen = cf.length ? cf.length : 1400;
+	slot = (maxlen + 16 + 15) & ~(size_t)15;
+
+	arena = calloc(n, slot);
+	pos = calloc(n, 4);
+	end = calloc(n, 4);
+	len = calloc(n, 4);
+	sess = calloc(n, 4);
+	err = calloc(n, 4);
+	cnt = calloc(cf.nsess, 4);
+	keys = calloc(cf.nsess, klen);
+	stbuf = calloc(cf.nsess, 24);
+	tx = calloc(cf.nsess, sizeof(*tx));
+	rx = calloc(cf.nsess, sizeof(*rx));
+	if (!arena || !pos || !end || !len || !sess || !err || !cnt || !keys ||
+	    !stbuf || !tx || !rx) {
+		fprintf(stderr, "out of memory\n");
+		return 1;
+	}
+
+	/* keys (workload.make_keys, or the test/srtp.c:524-528 key) */
+	for (i = 0; i < cf.nsess; i++) {
+		if (cf.test_key) {
+			memset(keys, 0x22, 16);
+			memset(keys + 16, 0x44, 14);
+		}
+		else {
+			xs_fill(keys + i * klen, klen, SEED_KEYS, i);
+		}
+		if (srtp_alloc(&tx[i], cf.suite, keys + i * klen, klen, 0) ||
+		    srtp_alloc(&rx[i], cf.suite, keys + i * klen, klen, 0)) {
+			fprintf(stderr, "srtp_alloc failed\n");
+			return 1;
+		}
+	}
+
+	/* arena (workload.make_arena) */
+	for (i = 0; i < n; i++) {
+		uint8_t *p = arena + i * slot;
+		uint32_t ssrc, ts = (uint32_t)(160u * (uint64_t)i);
+		uint16_t seq;
+		if (cf.length) {
+			len[i] = (uint32_t)cf.length;
+		}
+		else {
+			uint64_t s = xs_init(SEED_PAYLOAD + 1, i);
+			len[i] = (xs(&s) >> 63) ? 1400 : 200;
+		}
+		if (cf.nsess > 1) {
+			uint64_t s = xs_init(SEED_PAYLOAD + 2, i);
+			sess[i] = (uint32_t)((xs(&s) >> 32) % cf.nsess);
+		}
+		seq = (uint16_t)(cf.s0 + cnt[sess[i]]++);
+		ssrc = SSRC_BASE + sess[i];
+		p[0] = 0x80;
+		p[1] = 0;
+		p[2] = (uint8_t)(seq >> 8);
+		p[3] = (uint8_t)seq;
+		p[4] = (uint8_t)(ts >> 24); p[5] = (uint8_t)(ts >> 16);
+		p[6] = (uint8_t)(ts >> 8);  p[7] = (uint8_t)ts;
+		p[8] = (uint8_t)(ssrc >> 24); p[9] = (uint8_t)(ssrc >> 16);
+		p[10] = (uint8_t)(ssrc >> 8); p[11] = (uint8_t)ssrc;
+		xs_fill(p + 12, len[i] - 12, SEED_PAYLOAD, i);
+		pos[i] = (uint32_t)(i * slot);
+		end[i] = pos[i] + len[i];
+	}
+
+	printf("{\"config\":%d,\"suite\":%d,\"n\":%zu,\"slot\":%zu,"
+	       "\"nsess\":%zu,\"plain\":", c, cf.suite, n, slot, cf.nsess);
+	sha(arena, n * slot);
+
+	/* protect every packet in array order, in place (the slot has room
+	 * for the tag: mbuf_write_mem never reallocates) */
+	for (i = 0; i < n; i++) {
+		struct mbuf mb;
+		mb.buf = arena;
+		mb.size = pos[i] + slot;
+		mb.pos = pos[i];
+		mb.end = end[i];
+		err[i] = srtp_encrypt(tx[sess[i]], &mb);
+		end[i] = (uint32_t)mb.end;
+	}
+	emit("protect", arena, n, slot, end, err, tx, cf.nsess, stbuf);
+
+	for (i = 0; i < n; i++) {
+		struct mbuf mb;
+		mb.buf = arena;
+		mb.size = pos[i] + slot;
+		mb.pos = pos[i];
+		mb.end = end[i];
+		err[i] = srtp_decrypt(rx[sess[i]], &mb);
+		end[i] = (uint32_t)mb.end;
+	}
+	emit("unprotect", arena, n, slot, end, err, rx, cf.nsess, stbuf);
+	printf("}\n");
+
+	for (i = 0; i < cf.nsess; i++) {
+		mem_deref(tx[i]);
+		mem_deref(rx[i]);
+	}
+	return 0;
+}

@@ -1144,3 +1144,22 @@ long oracle_bench_pairs(int suite, size_t len, long n)
 	oracle_srtp_free(rx);
 	return ok;
 }
+
+/* stream state of ssrc (test helper: the state the reference keeps in
+ * struct srtp_stream, src/srtp/srtp.h:29-38); -1 if no such stream */
+int oracle_stream_state(const struct osrtp *s, uint32_t ssrc, uint32_t *roc,
+			uint32_t *s_l, uint64_t *lix, uint64_t *bitmap)
+{
+	int i;
+	for (i = 0; i < s->nstreams; i++) {
+		const struct ostream *st = &s->streams[i];
+		if (st->ssrc != ssrc)
+			continue;
+		*roc = st->roc;
+		*s_l = st->s_l;
+		*lix = st->replay_rtp.lix;
+		*bitmap = st->replay_rtp.bitmap;
+		return 0;
+	}
+	return -1;
+}

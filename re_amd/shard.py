@@ -13,7 +13,21 @@ srtp_stream_import().  RCCL (or gloo on CPU) only reduces the counters.
 def shard_state(rank, per_rank, s0, ssrc, receiver, state_cls=None):
     """Stream state after a sequential sender (receiver) processed packets
     0 .. rank*per_rank-1 with seq = (s0 + i) mod 2^16, starting from a
-    fresh stream.  Returns a StreamState (re_amd.srtp) or a dict."""
+    fresh stream.  Returns a StreamState (re_amd.srtp) or a dict.
+
+    Precondition (the only stream shape this closed form covers -- the
+    config-5 workload, re_amd/workload.py): ONE SSRC, a fresh stream at
+    packet 0, seq strictly +1 per packet (mod 2^16), every packet authentic
+    and none lost.  Other shapes (several SSRCs, reordering, loss, forged
+    packets) have no closed form: hand the state over with
+    srtp_stream_export() of the previous shard's contexts instead, which
+    serialises the shards.  tests/test_shard_cpu.py checks this function
+    against a sequential model, tests/test_gpu_shard.py against the library.
+    """
+    if not (isinstance(rank, int) and isinstance(per_rank, int) and
+            rank >= 0 and per_rank > 0 and 0 <= s0 <= 0xffff):
+        raise ValueError("shard_state: rank >= 0, per_rank > 0, "
+                         "0 <= s0 < 65536 (monotone single stream only)")
     k = rank * per_rank
     st = {"ssrc": ssrc, "roc": 0, "s_l": 0, "s_l_set": 0,
           "replay_rtp_lix": 0, "replay_rtp_bitmap": 0}

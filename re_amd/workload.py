@@ -1,61 +1,115 @@
 """Synthetic SRTP workloads (BASELINE.json configs).
 
 Packets are full RTP packets: 12-byte header (V=2, CC=0, X=0, PT=0),
-seq = (s0 + i) mod 2^16 with s0 = 65000 (ROC wraps every 65536 packets),
-ts = 160*i, one SSRC per session; payload bytes from a seeded generator.
-Each packet sits in a 16-byte aligned slot with room for the tag, so the
-arena can be handed to srtp_*_batch as-is.
+seq = (s0 + i) mod 2^16 (per session: s0 + the packet's ordinal in its
+session), ts = 160*i, SSRC = SSRC_BASE + session; each packet sits in a
+16-byte aligned slot with room for the tag, so the arena can be handed to
+srtp_*_batch as-is.
+
+Every random byte comes from xorshift64* (SURVEY.md 8(d)), one generator
+per packet / per session so the arena builds vectorised here and packet by
+packet in C (oracle/ref_digest.c rebuilds the identical arenas to compute
+the reference digests in tests/golden/fullsize_digests.json):
+
+  xs64(s):        s ^= s >> 12; s ^= s << 25; s ^= s >> 27;
+                  return s * 0x2545F4914F6CDD1D
+  state(seed, i): seed ^ (0x9E3779B97F4A7C15 * (i + 1))   (0 -> GOLDEN)
+  payload of packet i:  bytes [12, L) = LE bytes of xs64 outputs of
+                        state(SEED_PAYLOAD, i)
+  key of session k:     LE bytes of xs64 outputs of state(SEED_KEYS, k)
+  length (config 4):    first output of state(SEED_PAYLOAD + 1, i):
+                        top bit set -> 1400 B, else 200 B
+  session (config 4):   (first output of state(SEED_PAYLOAD + 2, i)
+                         >> 32) % nsess
 """
 import numpy as np
 
 SEED_PAYLOAD = 0x5EED5EED
 SEED_KEYS = 0xC0FFEE
 SSRC_BASE = 0x01020304
+GOLDEN = 0x9E3779B97F4A7C15
+XS_MUL = 0x2545F4914F6CDD1D
+
+# config 1: test/srtp.c:524-528 key, SSRC 0x01020304
+CONFIG1_KEY = b"\x22" * 16 + b"\x44" * 14
 
 
 def slot_size(max_len):
     return (max_len + 16 + 15) & ~15
 
 
+def xs_state(seed, idx):
+    """initial xorshift64* states of generators idx (uint64 array)"""
+    idx = np.asarray(idx, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed) ^ (np.uint64(GOLDEN) * (idx + np.uint64(1)))
+    s[s == 0] = np.uint64(GOLDEN)
+    return s
+
+
+def xs_next(s):
+    """advance states in place, return the xorshift64* outputs"""
+    s ^= s >> np.uint64(12)
+    s ^= s << np.uint64(25)
+    s ^= s >> np.uint64(27)
+    with np.errstate(over="ignore"):
+        return s * np.uint64(XS_MUL)
+
+
+def xs_bytes(seed, idx, nbytes):
+    """uint8[len(idx), nbytes]: LE bytes of each generator's outputs"""
+    s = xs_state(seed, idx)
+    nw = (nbytes + 7) // 8
+    out = np.empty((len(s), nw), dtype=np.uint64)
+    for w in range(nw):
+        out[:, w] = xs_next(s)
+    return out.view(np.uint8)[:, :nbytes]
+
+
 def make_keys(nsess, klen, seed=SEED_KEYS):
-    rng = np.random.default_rng(seed)
-    return rng.integers(0, 256, size=(nsess, klen), dtype=np.uint8)
+    return np.ascontiguousarray(xs_bytes(seed, np.arange(nsess), klen))
 
 
 def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
-               payload=True):
+               payload=True, first=0):
     """Returns (arena uint8[n*slot], pos, end, cap) numpy arrays.
 
     lengths: int or uint32 array (RTP packet length incl. 12-B header).
     sess: optional per-packet session index (SSRC = SSRC_BASE + sess).
+    first: global index of packet 0 (a shard of a longer stream: payload
+    generators and ts continue the stream).
     """
     lengths = np.broadcast_to(np.asarray(lengths, dtype=np.uint32),
                               (npkts,)).copy()
-    slot = slot_size(int(lengths.max()))
+    maxlen = int(lengths.max())
+    slot = slot_size(maxlen)
     arena = np.zeros((npkts, slot), dtype=np.uint8)
-    if payload:
-        rng = np.random.default_rng(seed)
-        arena[:, 12:int(lengths.max())] = rng.integers(
-            0, 256, size=(npkts, int(lengths.max()) - 12), dtype=np.uint8)
+    gidx = np.arange(first, first + npkts, dtype=np.uint64)
+    if payload and maxlen > 12:
+        # in chunks: the uint64 word matrix of 1M packets is ~1.2 GB
+        step = 1 << 16
+        for a in range(0, npkts, step):
+            b = min(npkts, a + step)
+            arena[a:b, 12:maxlen] = xs_bytes(seed, gidx[a:b], maxlen - 12)
         # zero bytes past each packet's end (mixed lengths)
-        if lengths.min() != lengths.max():
+        if lengths.min() != maxlen:
             col = np.arange(slot, dtype=np.uint32)[None, :]
             arena[col >= lengths[:, None]] = 0
-    i = np.arange(npkts, dtype=np.uint64)
     if sess is not None:
         # per-session sequence numbers: ordinal of the packet within its
         # session, so every SSRC sends seq s0, s0+1, ... in array order
         sarr = np.asarray(sess, dtype=np.int64)
         order = np.argsort(sarr, kind="stable")
         ss = sarr[order]
-        first = np.r_[0, np.flatnonzero(np.diff(ss)) + 1]
-        run_start = np.repeat(first, np.diff(np.r_[first, len(ss)]))
+        firsts = np.r_[0, np.flatnonzero(np.diff(ss)) + 1]
+        run_start = np.repeat(firsts, np.diff(np.r_[firsts, len(ss)]))
         ordinal = np.empty(npkts, dtype=np.uint64)
         ordinal[order] = (np.arange(npkts) - run_start).astype(np.uint64)
         seq = ((s0 + ordinal) & 0xffff).astype(np.uint16)
     else:
-        seq = ((s0 + i) & 0xffff).astype(np.uint16)
-    ts = (160 * i & 0xffffffff).astype(np.uint32)
+        seq = ((np.uint64(s0) + np.arange(npkts, dtype=np.uint64))
+               & np.uint64(0xffff)).astype(np.uint16)
+    ts = ((np.uint64(160) * gidx) & np.uint64(0xffffffff)).astype(np.uint32)
     ssrc = np.full(npkts, SSRC_BASE, dtype=np.uint32)
     if sess is not None:
         ssrc = (SSRC_BASE + np.asarray(sess, dtype=np.uint32)).astype(np.uint32)
@@ -74,11 +128,36 @@ def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
 
 def mixed_lengths(npkts, seed=SEED_PAYLOAD + 1):
     """config 4: Bernoulli(0.5) -> 200 or 1400 B"""
-    rng = np.random.default_rng(seed)
-    return np.where(rng.integers(0, 2, size=npkts) == 1, 1400,
-                    200).astype(np.uint32)
+    v = xs_next(xs_state(seed, np.arange(npkts)))
+    return np.where(v >> np.uint64(63), 1400, 200).astype(np.uint32)
 
 
 def random_sessions(npkts, nsess, seed=SEED_PAYLOAD + 2):
-    rng = np.random.default_rng(seed)
-    return rng.integers(0, nsess, size=npkts, dtype=np.uint32)
+    v = xs_next(xs_state(seed, np.arange(npkts)))
+    return ((v >> np.uint64(32)) % np.uint64(nsess)).astype(np.uint32)
+
+
+# BASELINE.json configs as workloads (oracle/ref_digest.c mirrors this)
+CONFIGS = {
+    1: dict(suite=1, n=1024, length=160, nsess=1, s0=1, key=CONFIG1_KEY),
+    2: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000),
+    3: dict(suite=5, n=1 << 20, length=1200, nsess=1, s0=65000),
+    4: dict(suite=1, n=1 << 20, length=None, nsess=1 << 16, s0=65000),
+}
+
+KEY_LEN = {0: 30, 1: 30, 2: 46, 3: 46, 4: 28, 5: 44}
+
+
+def build_config(cfg_id, n=None):
+    """(arena, pos, end, cap, sess or None, keys uint8[nsess, klen])"""
+    c = CONFIGS[cfg_id]
+    n = n or c["n"]
+    lengths = c["length"] if c["length"] else mixed_lengths(n)
+    sess = random_sessions(n, c["nsess"]) if c["nsess"] > 1 else None
+    arena, pos, end, cap = make_arena(n, lengths, s0=c["s0"], sess=sess)
+    klen = KEY_LEN[c["suite"]]
+    if c.get("key"):
+        keys = np.frombuffer(c["key"], dtype=np.uint8).reshape(1, klen)
+    else:
+        keys = make_keys(c["nsess"], klen)
+    return arena, pos, end, cap, sess, keys

@@ -1,0 +1,18 @@
+#!/bin/sh
+# Regenerate tests/golden/fullsize_digests.json: the reference src/srtp
+# (oracle/_ref/ref_digest, built by `make -C oracle ref` from the sources
+# under /root/reference) over the full BASELINE.json configs 1-4.
+# Build container only (needs /root/reference); ~15 s.
+set -e
+cd "$(dirname "$0")/.."
+make -s -C oracle ref
+{
+	echo '{"generator": "oracle/ref_digest.c (reference src/srtp + OpenSSL)",'
+	echo ' "configs": ['
+	oracle/_ref/ref_digest 1; echo ','
+	oracle/_ref/ref_digest 2; echo ','
+	oracle/_ref/ref_digest 3; echo ','
+	oracle/_ref/ref_digest 4
+	echo ']}'
+} > tests/golden/fullsize_digests.json
+python -c "import json; json.load(open('tests/golden/fullsize_digests.json'))"

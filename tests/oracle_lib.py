@@ -53,6 +53,10 @@ def _load():
     lib.oracle_bench_pairs.restype = ctypes.c_long
     lib.oracle_bench_pairs.argtypes = [ctypes.c_int, ctypes.c_size_t,
                                        ctypes.c_long]
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    lib.oracle_stream_state.argtypes = [vp, ctypes.c_uint32, u32p, u32p,
+                                        u64p, u64p]
     return lib
 
 
@@ -80,6 +84,16 @@ class OracleBackend:
 
     def free(self, ctx):
         self.l.oracle_srtp_free(ctx)
+
+    def export(self, ctx, ssrc):
+        """(roc, s_l, replay lix, replay bitmap) of ssrc, zeros if none"""
+        r, s = ctypes.c_uint32(), ctypes.c_uint32()
+        x, b = ctypes.c_uint64(), ctypes.c_uint64()
+        if self.l.oracle_stream_state(ctx, ssrc, ctypes.byref(r),
+                                      ctypes.byref(s), ctypes.byref(x),
+                                      ctypes.byref(b)):
+            return (0, 0, 0, 0)
+        return (r.value, s.value, x.value, b.value)
 
     def call(self, ctx, opname, size, pos, end, inb, nout):
         mb = OMbuf()

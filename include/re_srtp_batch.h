@@ -116,6 +116,18 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st);
 int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 		    const uint8_t *keys, size_t key_bytes, int flags);
 
+/**
+ * Diagnostics / tuning knobs (defaults from the environment, read once:
+ * RE_SRTP_NOPLAN, RE_SRTP_GENERAL, RE_SRTP_PERCLASS, RE_SRTP_TRACE,
+ * RE_SRTP_TIMES, RE_SRTP_CHUNK, RE_SRTP_PAR_MIN).  name is one of
+ * "noplan" (no device planners), "general" (general engine only),
+ * "perclass" (one CTR launch per header class), "trace", "times" (phase
+ * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
+ * (sessions per host-pool part); value 0 turns a switch off and restores
+ * a size's built-in default.  Results never depend on them.  0 or EINVAL.
+ */
+int srtp_gpu_tune(const char *name, long value);
+
 /** last HIP-level error text (diagnostics) */
 const char *srtp_gpu_error(void);
 

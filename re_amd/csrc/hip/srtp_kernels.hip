@@ -598,6 +598,8 @@ extern "C" int sgpu_table_reserve(uint32_t nsessions)
 	return e;
 }
 
+extern "C" uint32_t sgpu_table_capacity(void) { return g_table_cap; }
+
 extern "C" uint64_t sgpu_table_device_ptr(void) { return (uint64_t)(uintptr_t)g_table; }
 
 extern "C" int sgpu_setup_sessions(const struct sgpu_keyreq *req,

@@ -77,12 +77,83 @@ struct srtp {
 	struct srtp_stream streams[SRTP_MAX_STREAMS];
 	struct comp rtp, rtcp;
 	int dev;
+	uint32_t mp_epoch;      /* multi-session plan: call that gathered it
+				   (detects sessv entries aliasing one
+				   context) */
 };
+
+/* ------------------------------------------------------------------ */
+/* tuning / diagnostics switches, read once (not per batch)             */
+
+static struct {
+	int noplan;             /* RE_SRTP_NOPLAN: no device planners */
+	int general;            /* RE_SRTP_GENERAL: general engine only */
+	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
+	int trace;              /* RE_SRTP_TRACE: per-call phase times */
+	int times;              /* RE_SRTP_TIMES: multi-session phases */
+	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
+	size_t par_min;         /* RE_SRTP_PAR_MIN: sessions per pool part */
+} g_env;
+static pthread_once_t g_env_once = PTHREAD_ONCE_INIT;
+
+static void env_read(void)
+{
+	const char *e;
+	long v;
+	g_env.noplan = getenv("RE_SRTP_NOPLAN") != NULL;
+	g_env.general = getenv("RE_SRTP_GENERAL") != NULL;
+	g_env.perclass = getenv("RE_SRTP_PERCLASS") != NULL;
+	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
+	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
+	e = getenv("RE_SRTP_CHUNK");
+	v = e ? atol(e) : 0;
+	g_env.chunk = v >= 64 ? (size_t)v : (size_t)1 << 18;
+	e = getenv("RE_SRTP_PAR_MIN");
+	v = e ? atol(e) : 0;
+	g_env.par_min = v > 0 ? (size_t)v : 4096;
+}
+
+static void env_init(void)
+{
+	pthread_once(&g_env_once, env_read);
+}
+
+int srtp_gpu_tune(const char *name, long value)
+{
+	env_init();
+	if (!name)
+		return EINVAL;
+	if (!strcmp(name, "noplan"))
+		g_env.noplan = value > 0;
+	else if (!strcmp(name, "general"))
+		g_env.general = value > 0;
+	else if (!strcmp(name, "perclass"))
+		g_env.perclass = value > 0;
+	else if (!strcmp(name, "trace"))
+		g_env.trace = value > 0;
+	else if (!strcmp(name, "times"))
+		g_env.times = value > 0;
+	else if (!strcmp(name, "chunk"))
+		g_env.chunk = value >= 64 ? (size_t)value : (size_t)1 << 18;
+	else if (!strcmp(name, "par_min"))
+		g_env.par_min = value > 0 ? (size_t)value : 4096;
+	else
+		return EINVAL;
+	return 0;
+}
 
 /* ------------------------------------------------------------------ */
 /* device table slots                                                  */
 
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+/*
+ * The device session table may move when it grows (sgpu_table_reserve).
+ * Batch calls hold it read-locked for their whole duration (each call
+ * synchronises its stream before returning, so no kernel of it still reads
+ * the table afterwards); a growing allocation takes it write-locked.
+ * Lock order: g_table_rw, then g_lock.
+ */
+static pthread_rwlock_t g_table_rw = PTHREAD_RWLOCK_INITIALIZER;
 static uint32_t *g_free;
 static uint32_t g_nfree, g_free_cap, g_next_slot;
 static int g_gpu_state;         /* 0 unknown, 1 ok, -1 unavailable */
@@ -112,13 +183,35 @@ const char *srtp_gpu_error(void)
 static int slots_get(uint32_t *slots, size_t n)
 {
 	size_t i;
-	int err;
-	pthread_mutex_lock(&g_lock);
+	int err, held = 0;
+	/* growth moves the table: only under the write lock (re-checked
+	 * under g_lock, another allocation may have taken slots meanwhile) */
+	for (;;) {
+		pthread_mutex_lock(&g_lock);
+		if (held || (uint64_t)g_next_slot + n <= sgpu_table_capacity())
+			break;
+		pthread_mutex_unlock(&g_lock);
+		pthread_rwlock_wrlock(&g_table_rw);
+		held = 1;
+	}
 	for (i = 0; i < n; i++)
 		slots[i] = g_nfree ? g_free[--g_nfree] : g_next_slot++;
 	err = sgpu_table_reserve(g_next_slot);
 	pthread_mutex_unlock(&g_lock);
+	if (held)
+		pthread_rwlock_unlock(&g_table_rw);
 	return err;
+}
+
+static void table_rdlock(void)
+{
+	env_init();
+	pthread_rwlock_rdlock(&g_table_rw);
+}
+
+static void table_unlock(void)
+{
+	pthread_rwlock_unlock(&g_table_rw);
 }
 
 static void slot_put(uint32_t s)
@@ -1227,8 +1320,8 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 
 /* ---- host-resident front-end (mbufs) -------------------------------- */
 
-static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
-		     size_t n)
+static int run_mbufs_(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
+		      size_t n)
 {
 	const int prot = op == OP_RTP_ENC || op == OP_RTCP_ENC;
 	struct engine E;
@@ -1237,7 +1330,7 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 	uint8_t *keep = NULL;       /* per-packet copies across rounds */
 	uint32_t *soff = NULL;      /* staging offsets */
 	size_t *koff = NULL, i, round;
-	int err;
+	int err, snapped = 0;
 
 	if (!srtp || !mbv)
 		return EINVAL;
@@ -1272,6 +1365,7 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 	}
 
 	snap_take(&E);
+	snapped = 1;
 	for (round = 0;; round++) {
 		size_t need, bytes = 0;
 		uint32_t m;
@@ -1348,16 +1442,20 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 				outp[i] = w->stage.h + soff[i];
 	}
 
-	/* unpack: bytes, mbuf size growth (same policy), pos/end, errno */
+	/* mbuf size growth (same policy) first: a failed resize leaves
+	 * every mbuf's window and bytes, and the stream states, as before */
+	for (i = 0; i < n; i++) {
+		if (E.rec[i].size_o > mbv[i]->size) {
+			err = mbuf_resize(mbv[i], E.rec[i].size_o);
+			if (err)
+				goto out;
+		}
+	}
+	/* unpack: bytes, pos/end, errno */
 	for (i = 0; i < n; i++) {
 		const struct rec *r = &E.rec[i];
 		struct mbuf *mb = mbv[i];
 		const struct pinfo *pi = &E.pi[i];
-		if (r->size_o > mb->size) {
-			err = mbuf_resize(mb, r->size_o);
-			if (err)
-				goto out;
-		}
 		if (r->has_job && outp[i])
 			memcpy(mb->buf + pi->start, outp[i],
 			       r->ext_end - pi->start);
@@ -1367,11 +1465,24 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 			errv[i] = r->err;
 	}
  out:
+	/* a failed call leaves the stream states as it found them */
+	if (err && snapped)
+		snap_restore(&E);
 	free(outp);
 	free(keep);
 	free(soff);
 	free(koff);
 	engine_free(&E);
+	return err;
+}
+
+static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
+		     size_t n)
+{
+	int err;
+	table_rdlock();
+	err = run_mbufs_(op, srtp, mbv, errv, n);
+	table_unlock();
 	return err;
 }
 
@@ -1442,7 +1553,7 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 	uint32_t *pe_h;
 	struct sgpu_hdr *hd_h;
 	uint32_t *eix_h;
-	int err;
+	int err, snapped = 0;
 
 	if (!sessv || !nsess || !b || !b->arena || !b->pos || !b->end ||
 	    !b->cap || !b->err)
@@ -1512,6 +1623,7 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 
 	/* 2. plan / run rounds; in-place results */
 	snap_take(&E);
+	snapped = 1;
 	for (round = 0;; round++) {
 		size_t need;
 		uint32_t m = 0, mu = 0;
@@ -1596,6 +1708,8 @@ static int run_batch_general(int op, struct srtp **sessv, size_t nsess,
 		b->err[i] = r->err;
 	}
  out:
+	if (err && snapped)
+		snap_restore(&E);
 	engine_free(&E);
 	return err;
 }
@@ -1890,9 +2004,7 @@ static double now_ms(void)
 
 static size_t fast_chunk(void)
 {
-	const char *e = getenv("RE_SRTP_CHUNK");
-	long v = e ? atol(e) : 0;
-	return v >= 64 ? (size_t)v : (size_t)1 << 18;
+	return g_env.chunk;
 }
 
 /* replay state after the planned batch: the last <= 65 indices suffice
@@ -1969,9 +2081,7 @@ static void plan_unapply(struct srtp *s, unsigned nstreams0,
  * (RE_SRTP_PAR_MIN overrides: tests drive the pool with few sessions) */
 static size_t mplan_par(void)
 {
-	const char *e = getenv("RE_SRTP_PAR_MIN");
-	long v = e ? atol(e) : 0;
-	return v > 0 ? (size_t)v : 4096;
+	return g_env.par_min;
 }
 
 struct mpg {
@@ -1980,6 +2090,7 @@ struct mpg {
 	const struct sgpu_sstate *o;
 	uint32_t *cm;
 	int suite, prot;
+	uint32_t epoch;         /* this call (alias detection) */
 	atomic_int bad;
 };
 
@@ -1993,6 +2104,14 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 		if (k + 16 < b)
 			__builtin_prefetch(g->sessv[k + 16], 0, 1);
 		if (s->nstreams > 1 || s->suite != g->suite) {
+			atomic_store(&g->bad, 1);
+			return;
+		}
+		/* two sessv entries naming one context would plan the same
+		 * stream as two independent segments: not plannable (the
+		 * host engines work through the pointers) */
+		if (__atomic_exchange_n(&((struct srtp *)s)->mp_epoch, g->epoch,
+					__ATOMIC_RELAXED) == g->epoch) {
 			atomic_store(&g->bad, 1);
 			return;
 		}
@@ -2015,7 +2134,10 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 static int mplan_gather(struct srtp **sessv, size_t nsess,
 			struct sgpu_sstate *st, uint32_t *cm)
 {
-	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0};
+	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0};
+	do {
+		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
+	} while (!g.epoch);
 	par_for(nsess, mplan_par(), mplan_gather_part, &g);
 	return atomic_load(&g.bad) ? -1 : 0;
 }
@@ -2053,7 +2175,7 @@ static void mplan_apply_part(void *arg, size_t a, size_t b)
 static void mplan_apply(struct srtp **sessv, size_t nsess,
 			const struct sgpu_sstate *o, int prot)
 {
-	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0};
+	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0};
 	par_for(nsess, mplan_par(), mplan_apply_part, &g);
 }
 
@@ -2099,7 +2221,7 @@ static int run_classes(uint8_t *arena, uint64_t asz, struct sgpu_compact C,
 		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
 					0, prot, stream);
 	}
-	if (!C.undo && !getenv("RE_SRTP_PERCLASS")) {
+	if (!C.undo && !g_env.perclass) {
 		C.guard = po_d->skip;
 		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
 					-1, prot, stream);
@@ -2221,7 +2343,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
-	if (getenv("RE_SRTP_TRACE"))
+	if (g_env.trace)
 		fprintf(stderr, "re_srtp mplan %s n=%zu nsess=%zu: fail 0x%x "
 			"cap %d\n", prot ? "enc" : "dec", n, nsess, po->fail,
 			capok);
@@ -2265,12 +2387,13 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	void *stream, *entry_ev = NULL;
 	struct ws *w;
 	int err = 0, parsed = 0, planned = 0;
+	int touched = 0;        /* up_h holds every original window */
 	void *pst;
 	/* planned path: stream state before the call (undo) */
 	struct srtp *ps = sessv[0];
 	unsigned ps_n = ps->nstreams;
 	struct srtp_stream ps_old;
-	const int trace = getenv("RE_SRTP_TRACE") != NULL;
+	const int trace = g_env.trace;
 	double t0 = trace ? now_ms() : 0, t1 = 0, t2 = 0, tscan = 0, twait = 0;
 
 	if (n == 0)
@@ -2285,6 +2408,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	w = ws_get();
 	if (!w)
 		return ENOMEM;
+	w->ulog[0].n = 0;
 	if (!w->pstream) {
 		w->pstream = sgpu_stream_create();
 		if (!w->pstream)
@@ -2342,9 +2466,10 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	/* 0b. many sessions, at most one stream each: plan on the device
 	 *     (stable sort by session + per-session speculation); host work
 	 *     is O(sessions): gather the states, apply the results. */
-	if (b->sess && nsess > 1 && !t_noplan && !getenv("RE_SRTP_NOPLAN")) {
+	if (b->sess && nsess > 1 && !t_noplan && !g_env.noplan) {
 		int r = run_mplanned(op, sessv, nsess, b, w, stream, c0, T, fl,
 				     &nfl, &nfail);
+		touched = r != -1;
 		if (r == 0) {
 			planned = 2;
 			if (trace)
@@ -2368,7 +2493,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	 *    crypto launches are guarded on the device by the plan's verdict
 	 *    (sgpu_plan_out.skip), so a rejected plan modifies nothing. */
 	if (nsess == 1 && ps->nstreams <= 1 && !t_noplan &&
-	    !getenv("RE_SRTP_NOPLAN")) {
+	    !g_env.noplan) {
 		struct sgpu_plan_in in;
 		struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
 		struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
@@ -2384,6 +2509,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		plan_in(&in, ps, (uint32_t)n, prot, T, need);
 		memcpy(up_h, b->pos, n * 4);
 		memcpy(up_h + n, b->end, n * 4);
+		touched = 1;
 		err = sgpu_memcpy_h2d(w->cm.d, cm_h, 4, stream);
 		if (!err && !prot)
 			err = sgpu_memset(nfail_d, 0, 4, stream);
@@ -2513,6 +2639,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	}
 	if (err)
 		goto out;
+	touched = 1;
 	if (parsed && b->sess) {
 		memcpy(up_h + 2 * n, b->sess, n * 4);
 		err = sgpu_memcpy_h2d(up_d + 2 * n, up_h + 2 * n, n * 4,
@@ -2534,7 +2661,9 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	FT[0].cap = b->cap;
 	FT[0].err = b->err;
 	FT[0].epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
-	FT[0].log = !prot;
+	/* every first touch of a stream is logged (undo on a miss or a
+	 * failed call) */
+	FT[0].log = 1;
 	FT[0].mode = c0->mode;
 	FT[0].tag_len = c0->tag_len;
 	FT[0].log_v = &w->ulog[0];
@@ -2623,12 +2752,6 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			now_ms() - t0);
 	if (err)
 		goto out;
-	if (nfail && getenv("RE_SRTP_DEBUG_NOFOLD")) {
-		/* debugging aid: leave the speculative first pass in place */
-		fprintf(stderr, "re_srtp: %u speculation misses not folded\n",
-			nfail);
-		goto out;
-	}
 	if (nfail) {
 		/* speculation missed: undo and fold exactly */
 		for (k = 0; k < nfl && !err; k++) {
@@ -2663,6 +2786,17 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 		return run_batch_general(op, sessv, nsess, b);
 	}
  out:
+	if (err > 0 && touched) {
+		/* a failed call leaves the stream states and windows as it
+		 * found them (the arena may be partly processed: EIO) */
+		if (planned == 1)
+			plan_unapply(ps, ps_n, &ps_old);
+		else if (planned == 2)
+			mplan_unapply(sessv, nsess, w);
+		ulog_undo(&w->ulog[0]);
+		memcpy(b->pos, up_h, n * 4);
+		memcpy(b->end, up_h + n, n * 4);
+	}
 	free(fl);
 	return err;
 }
@@ -2676,7 +2810,7 @@ static int run_batch(int op, struct srtp **sessv, size_t nsess,
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && sessv && nsess && b &&
 	    b->arena && b->pos && b->end && b->cap && b->err &&
 	    b->n <= UINT32_MAX / 4 && b->arena_size <= UINT32_MAX &&
-	    !getenv("RE_SRTP_GENERAL")) {
+	    !g_env.general) {
 		for (i = 0; i < nsess; i++) {
 			if (!sessv[i])
 				return EINVAL;
@@ -2841,7 +2975,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	size_t scr;
 	void *stream = d->stream;
 	struct ws *w = ws_get();
-	const int times = getenv("RE_SRTP_TIMES") != NULL;
+	const int times = g_env.times;
 	double t[4];
 	int err;
 
@@ -3047,13 +3181,13 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 		return EINVAL;
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess == 1 &&
 	    !d->sess && sessv[0]->nstreams <= 1 &&
-	    !getenv("RE_SRTP_NOPLAN") && !getenv("RE_SRTP_GENERAL")) {
+	    !g_env.noplan && !g_env.general) {
 		int r = dev_planned(op, sessv[0], d);
 		if (r >= 0)
 			return r;
 	}
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess > 1 && d->sess &&
-	    !getenv("RE_SRTP_NOPLAN") && !getenv("RE_SRTP_GENERAL")) {
+	    !g_env.noplan && !g_env.general) {
 		int r = dev_mplanned(op, sessv, nsess, d);
 		if (r >= 0)
 			return r;
@@ -3061,52 +3195,66 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 	return dev_staged(op, sessv, nsess, d);
 }
 
+enum { HOSTW = 0, DEV = 1 };
+
+/* public batch entry: the device table stays in place for the call */
+static int locked(int kind, int op, struct srtp **sessv, size_t nsess,
+		  void *b)
+{
+	int err;
+	table_rdlock();
+	err = kind == DEV ? run_dev(op, sessv, nsess, b)
+			  : run_batch(op, sessv, nsess, b);
+	table_unlock();
+	return err;
+}
+
 int srtp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
 			   struct srtp_batch_dev *b)
 {
-	return run_dev(OP_RTP_ENC, sessv, nsess, b);
+	return locked(DEV, OP_RTP_ENC, sessv, nsess, b);
 }
 
 int srtp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
 			   struct srtp_batch_dev *b)
 {
-	return run_dev(OP_RTP_DEC, sessv, nsess, b);
+	return locked(DEV, OP_RTP_DEC, sessv, nsess, b);
 }
 
 int srtcp_encrypt_batch_dev(struct srtp **sessv, size_t nsess,
 			    struct srtp_batch_dev *b)
 {
-	return run_dev(OP_RTCP_ENC, sessv, nsess, b);
+	return locked(DEV, OP_RTCP_ENC, sessv, nsess, b);
 }
 
 int srtcp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
 			    struct srtp_batch_dev *b)
 {
-	return run_dev(OP_RTCP_DEC, sessv, nsess, b);
+	return locked(DEV, OP_RTCP_DEC, sessv, nsess, b);
 }
 
 int srtp_encrypt_batch(struct srtp **sessv, size_t nsess,
 		       struct srtp_batch *b)
 {
-	return run_batch(OP_RTP_ENC, sessv, nsess, b);
+	return locked(HOSTW, OP_RTP_ENC, sessv, nsess, b);
 }
 
 int srtp_decrypt_batch(struct srtp **sessv, size_t nsess,
 		       struct srtp_batch *b)
 {
-	return run_batch(OP_RTP_DEC, sessv, nsess, b);
+	return locked(HOSTW, OP_RTP_DEC, sessv, nsess, b);
 }
 
 int srtcp_encrypt_batch(struct srtp **sessv, size_t nsess,
 			struct srtp_batch *b)
 {
-	return run_batch(OP_RTCP_ENC, sessv, nsess, b);
+	return locked(HOSTW, OP_RTCP_ENC, sessv, nsess, b);
 }
 
 int srtcp_decrypt_batch(struct srtp **sessv, size_t nsess,
 			struct srtp_batch *b)
 {
-	return run_batch(OP_RTCP_DEC, sessv, nsess, b);
+	return locked(HOSTW, OP_RTCP_DEC, sessv, nsess, b);
 }
 
 /* ---- stream state export / import ------------------------------------ */

@@ -99,7 +99,10 @@ int   sgpu_init(void);                  /* 0, or ENODEV / ENOSYS */
 const char *sgpu_last_error(void);
 
 /* device session-context table: slots are allocated by the host */
-int   sgpu_table_reserve(uint32_t nsessions);      /* grow capacity */
+int   sgpu_table_reserve(uint32_t nsessions);      /* grow capacity (moves
+							   the table: callers
+							   exclude batches) */
+uint32_t sgpu_table_capacity(void);
 int   sgpu_setup_sessions(const struct sgpu_keyreq *req, const uint32_t *slot,
 			  uint32_t n);               /* KDF + key schedule */
 uint64_t sgpu_table_device_ptr(void);

@@ -98,7 +98,7 @@ EXPORTS = (
     "srtp_decrypt_batch_dev", "srtcp_encrypt_batch_dev",
     "srtcp_decrypt_batch_dev", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
-    "srtp_gpu_prof", "srtp_gpu_prof_read",
+    "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
 )
 
@@ -137,6 +137,7 @@ def load():
     L.srtp_alloc_many.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_int,
                                   ctypes.c_char_p, sz, ctypes.c_int]
     L.srtp_gpu_prof.argtypes = [ctypes.c_int]
+    L.srtp_gpu_tune.argtypes = [ctypes.c_char_p, ctypes.c_long]
     L.srtp_gpu_prof_read.argtypes = [ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64),
                                      ctypes.POINTER(ctypes.c_uint64)]
@@ -308,6 +309,25 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
     sv = session_array(sessions)
     return getattr(lib(), opname + "_batch_dev")(sv, len(sv),
                                                  ctypes.byref(b))
+
+
+class tune:
+    """srtp_gpu_tune as a context manager: with tune(general=1): ...
+    (knobs restored to their defaults on exit)"""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            if v is not None:
+                assert lib().srtp_gpu_tune(k.encode(), int(v)) == 0, k
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.knobs:
+            lib().srtp_gpu_tune(k.encode(), 0)
+        return False
 
 
 def prof_enable(on=True):

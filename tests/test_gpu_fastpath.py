@@ -1,7 +1,7 @@
 """GPU parity of the compact descriptor path (srtp_*_batch fast path).
 
 The fast path (re_amd/csrc/host/srtp.c run_fast) must give exactly the
-results of the general engine (RE_SRTP_GENERAL=1), which the golden
+results of the general engine (srtp_gpu_tune general), which the golden
 replays pin to the reference, and of the oracle called one packet at a
 time: same errno, pos/end, bytes and stream state.  Batches are adversarial:
 CSRC/extension headers (mixed kernel classes), 9 SSRCs in one session
@@ -11,7 +11,6 @@ and forged packets (EAUTH -> speculation miss -> undo + exact fold), with
 tiny chunks so the host/GPU pipeline crosses many chunk boundaries.
 """
 import errno
-import os
 
 import numpy as np
 import pytest
@@ -99,17 +98,7 @@ def to_arena(pkts, short_cap=()):
 
 def run(torch, opname, sessions, arena, pos, end, cap, sess, general,
         chunk=None):
-    env_old = {k: os.environ.get(k) for k in ("RE_SRTP_GENERAL",
-                                               "RE_SRTP_CHUNK")}
-    try:
-        if general:
-            os.environ["RE_SRTP_GENERAL"] = "1"
-        else:
-            os.environ.pop("RE_SRTP_GENERAL", None)
-        if chunk:
-            os.environ["RE_SRTP_CHUNK"] = str(chunk)
-        else:
-            os.environ.pop("RE_SRTP_CHUNK", None)
+    with P.tune(general=1 if general else 0, chunk=chunk or 0):
         dev = torch.from_numpy(arena.copy()).cuda()
         p, e = pos.copy(), end.copy()
         torch.cuda.synchronize()
@@ -117,12 +106,6 @@ def run(torch, opname, sessions, arena, pos, end, cap, sess, general,
                                  arena.nbytes, p, e, cap, sess)
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
         return dev.cpu().numpy(), p, e, err
-    finally:
-        for k, v in env_old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def states(sessions, ssrcs):
@@ -285,7 +268,7 @@ def test_device_planner_and_its_fallbacks(suite, torch_cuda):
     """Single-stream batches take the device planner; every broken
     speculation (reorder, replay, ETIMEDOUT, mixed header classes, second
     SSRC) must fall back with identical results.  Compared against the
-    host-planned fast path (RE_SRTP_NOPLAN) and the general engine, with
+    host-planned fast path (srtp_gpu_tune noplan) and the general engine, with
     state carried across consecutive batches."""
     torch = torch_cuda
     rng = np.random.default_rng(77 + suite)
@@ -310,13 +293,13 @@ def test_device_planner_and_its_fallbacks(suite, torch_cuda):
             tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
             outs = []
             for a, b in parts:
-                os.environ.pop("RE_SRTP_NOPLAN", None)
+                P.lib().srtp_gpu_tune(b"noplan", 0)
                 if mode == "noplan":
-                    os.environ["RE_SRTP_NOPLAN"] = "1"
+                    P.lib().srtp_gpu_tune(b"noplan", 1)
                 sl = slice(a, b)
                 enc = run(torch, "srtp_encrypt", [tx], arena, pos[sl],
                           end[sl], cap[sl], None, mode == "general")
-                os.environ.pop("RE_SRTP_NOPLAN", None)
+                P.lib().srtp_gpu_tune(b"noplan", 0)
                 outs.append(enc)
             # receive what was sent (protected windows), same split
             prot = []
@@ -330,11 +313,11 @@ def test_device_planner_and_its_fallbacks(suite, torch_cuda):
             douts = []
             for a, b in ((0, h), (h, len(prot))):
                 if mode == "noplan":
-                    os.environ["RE_SRTP_NOPLAN"] = "1"
+                    P.lib().srtp_gpu_tune(b"noplan", 1)
                 sl = slice(a, b)
                 douts.append(run(torch, "srtp_decrypt", [rx], a2, p2[sl],
                                  e2[sl], c2[sl], None, mode == "general"))
-                os.environ.pop("RE_SRTP_NOPLAN", None)
+                P.lib().srtp_gpu_tune(b"noplan", 0)
             res[mode] = (outs, douts, states([tx], [0x5151]),
                          states([rx], [0x5151]))
             tx.close()
@@ -430,7 +413,7 @@ def multi_session_traffic(rng, n, nsess, s0=None, forge=()):
 def test_multi_session_device_planner(suite, torch_cuda):
     """many sessions, one SSRC each: planned on the device (sort by
     session + per-session speculation); must equal the host scan
-    (RE_SRTP_NOPLAN) and the general engine, across two consecutive
+    (srtp_gpu_tune noplan) and the general engine, across two consecutive
     batches, with a forged packet forcing undo + exact fold"""
     torch = torch_cuda
     rng = np.random.default_rng(55 + suite)
@@ -456,10 +439,10 @@ def test_multi_session_device_planner(suite, torch_cuda):
         for bi, pk in enumerate(batches):
             arena, pos, end, cap, sess = to_arena(pk)
             if mode == "noplan":
-                os.environ["RE_SRTP_NOPLAN"] = "1"
+                P.lib().srtp_gpu_tune(b"noplan", 1)
             enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap, sess,
                       mode == "general")
-            os.environ.pop("RE_SRTP_NOPLAN", None)
+            P.lib().srtp_gpu_tune(b"noplan", 0)
             prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
                     for i, (s, _) in enumerate(pk)]
             if bi == 1:
@@ -468,10 +451,10 @@ def test_multi_session_device_planner(suite, torch_cuda):
                 prot[1234] = (prot[1234][0], bytes(q))
             a2, p2, e2, c2, s2 = to_arena(prot)
             if mode == "noplan":
-                os.environ["RE_SRTP_NOPLAN"] = "1"
+                P.lib().srtp_gpu_tune(b"noplan", 1)
             dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
                       mode == "general")
-            os.environ.pop("RE_SRTP_NOPLAN", None)
+            P.lib().srtp_gpu_tune(b"noplan", 0)
             outs.append((enc, dec))
         res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
         for c in tx + rx:
@@ -551,13 +534,13 @@ def test_device_resident_multi_session(suite, torch_cuda):
     batches.append(nb)
     res = {}
     # dev_par: the session gather/apply passes split over the host pool
-    # (RE_SRTP_PAR_MIN=4 -> parts of >= 4 sessions)
+    # (par_min 4 -> parts of >= 4 sessions)
     for mode in ("dev", "dev_par", "host", "general"):
         tx = [P.Srtp(suite, k) for k in keys]
         rx = [P.Srtp(suite, k) for k in keys]
         outs = []
         if mode == "dev_par":
-            os.environ["RE_SRTP_PAR_MIN"] = "4"
+            P.lib().srtp_gpu_tune(b"par_min", 4)
         for bi, pk in enumerate(batches):
             arena, pos, end, cap, sess = to_arena(pk)
             if mode.startswith("dev"):
@@ -579,7 +562,7 @@ def test_device_resident_multi_session(suite, torch_cuda):
                 dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
                           mode == "general")
             outs.append((enc, dec))
-        os.environ.pop("RE_SRTP_PAR_MIN", None)
+        P.lib().srtp_gpu_tune(b"par_min", 0)
         res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
         for c in tx + rx:
             c.close()

@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--host-arrays", action="store_true",
                     help="srtp_*_batch with host pos/end/err arrays instead "
                          "of the device-resident srtp_*_batch_dev")
+    ap.add_argument("--tune", action="append", default=[],
+                    help="name=value: srtp_gpu_tune knob (A/B runs)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary to attach (profiles/*.json)")
     args = ap.parse_args()
@@ -137,6 +139,9 @@ def main():
                                     device_id=torch.device("cuda", gpu))
     dev = torch.device("cuda", gpu)
     P.load()
+    for kv in args.tune:
+        k, v = kv.split("=")
+        assert P.lib().srtp_gpu_tune(k.encode(), int(v)) == 0, kv
     tstart = time.perf_counter()
 
     def log(msg):

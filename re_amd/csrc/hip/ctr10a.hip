@@ -4,6 +4,7 @@
  * parallel with the per-class instantiations.
  */
 #include "k_ctr.h"
+#include "k_ctr_fast.h"
 
 kfn_t sgpu_pick_ctr10_any(bool uni, int prot)
 {
@@ -11,4 +12,17 @@ kfn_t sgpu_pick_ctr10_any(bool uni, int prot)
 			   : k_ctr_hmac_any<10, false, true>)
 		   : (prot ? k_ctr_hmac_any<10, true, false>
 			   : k_ctr_hmac_any<10, false, false>);
+}
+
+/* lean kernels of device-planned single-key batches (k_ctr_fast.h) */
+kfn_t sgpu_pick_ctr10_fast(int prot, int refix)
+{
+	if (refix)
+		return k_ctr_fast_refix<10>;
+	return prot ? k_ctr_fast_any<10, true> : k_ctr_fast_any<10, false>;
+}
+
+unsigned sgpu_ctr_fast_block(void)
+{
+	return CTRF_BLOCK;
 }

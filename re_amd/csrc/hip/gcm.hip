@@ -234,8 +234,7 @@ k_gcm(const KArgs a)
 		for (int q = 0; q < 4; q++) {
 			uint32_t bp = 4u * q;
 			uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
-			uint32_t m = nbytes >= 4 ? 0xffffffffu
-				   : ((1u << (8 * nbytes)) - 1u);
+			uint32_t m = (uint32_t)((1ull << (8 * nbytes)) - 1ull);
 			const uint32_t o = (d[q] ^ ks[q]) & m;
 			ct[q] = PROT ? o : (d[q] & m);
 			if (nbytes == 4)
@@ -493,8 +492,7 @@ __device__ __forceinline__ uint8_t gcmu_packet(const uint8_t *smem, uint32_t lo,
 		for (int q = 0; q < 4; q++) {
 			const uint32_t bp = 4u * q;
 			const uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
-			const uint32_t mk = nbytes >= 4 ? 0xffffffffu
-					  : ((1u << (8 * nbytes)) - 1u);
+			const uint32_t mk = (uint32_t)((1ull << (8 * nbytes)) - 1ull);
 			const uint32_t o = (d[q] ^ ks[q]) & mk;
 			ct[q] = PROT ? o : (d[q] & mk);
 			if (nbytes == 4)

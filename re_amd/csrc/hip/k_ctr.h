@@ -29,6 +29,13 @@
 #ifndef CTR_PIPE_U
 #define CTR_PIPE_U 1
 #endif
+#ifndef CTR_SHAFIRST_U      /* unprotect steady chunk: MAC of the received
+			       ciphertext, then the keystream in place */
+#define CTR_SHAFIRST_U 0
+#endif
+#ifndef CTR_SCHED_BARRIER_U /* ... with a scheduling barrier between them */
+#define CTR_SCHED_BARRIER_U 0
+#endif
 #ifndef CTR_UNI_PROT_BLOCK  /* single-key protect block size */
 #define CTR_UNI_PROT_BLOCK 1024
 #endif
@@ -244,6 +251,9 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 			K1 = a1;
 		}
 	}
+	/* unprotect, SHA-first form: the keystream applied to bytes that
+	 * must stay ciphertext (no decryption) is masked to zero */
+	const uint32_t km = store_ct ? 0xffffffffu : 0u;
 	auto steady = [&](uint32_t k, auto coal) {
 		constexpr bool CO = decltype(coal)::value;
 		const uint32_t c0 = 64u * k;
@@ -258,6 +268,30 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 				d[4 * g] = v.x; d[4 * g + 1] = v.y;
 				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
 			}
+		}
+		if constexpr (!PROT && CTR_SHAFIRST_U && !PIPE) {
+			/* the MAC covers the received ciphertext: run it first,
+			 * then decrypt d in place -- only d, the schedule and
+			 * the SHA-1 state live at once */
+#pragma unroll
+			for (int jj = 0; jj < 16; jj++)
+				w[jj] = bswap32(d[jj]);
+			sha1_compress(h, w);
+			if (CTR_SCHED_BARRIER_U)
+				__builtin_amdgcn_sched_barrier(0);
+			ks_xor_km<NR, SHIFT>(smem, lo, rk, C,
+					     (int32_t)(4 * k) - cw4, carry, d, km);
+			if constexpr (CO) {
+				quad_store(arena, qb, c0, lane, d);
+			}
+			else {
+#pragma unroll
+				for (int g = 0; g < 4; g++)
+					*(uint4 *)(pkt + c0 + 16u * g) =
+						make_uint4(d[4 * g], d[4 * g + 1],
+							   d[4 * g + 2], d[4 * g + 3]);
+			}
+			return;
 		}
 		if constexpr (PIPE) {
 #pragma unroll

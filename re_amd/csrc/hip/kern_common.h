@@ -244,7 +244,9 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t gw, uint32_t data_be,
 	if (gw < aw)
 		return data_be;
 	if (gw == aw)
-		return (u ? (data_be & (0xFFFFFFFFu << (32 - 8 * u))) : 0u) |
+		/* 64-bit mask shift: a 32-bit shift by 32 (u = 0) is poison,
+		 * which LLVM may propagate past the select guarding it */
+		return (data_be & (uint32_t)(0xFFFFFFFF00000000ull >> (8 * u))) |
 		       (uint32_t)(X >> (32 + 8 * u));
 	if (gw == aw + 1)
 		return (uint32_t)(X >> (8 * u));
@@ -362,7 +364,9 @@ __device__ __forceinline__ uint32_t region_mask(uint32_t bpos, uint32_t c_off,
 {
 	const uint32_t nbytes = (bpos >= c_off && bpos < c_end) ?
 				min(c_end - bpos, 4u) : 0u;
-	return nbytes >= 4 ? 0xffffffffu : ((1u << (8 * nbytes)) - 1u);
+	/* no 32-bit shift by 32 (poison, which LLVM may carry past a select:
+	 * observed as whole-word tail stores, ROCm 7.2 -O3) */
+	return (uint32_t)((1ull << (8 * nbytes)) - 1ull);
 }
 
 /*
@@ -405,6 +409,40 @@ __device__ __forceinline__ void ks_xor(const uint8_t *smem, uint32_t lo,
 		}
 	}
 #undef KS_MASK
+}
+
+/* ks_xor (unmasked) with a per-lane keystream mask: d ^= ks & km, one
+ * v_bitop3 per word (a ^ (b & c): table 0x78) */
+template <int NR, int SHIFT, bool CACHED, bool T4>
+__device__ __forceinline__ void ks_xor_km(const uint8_t *smem, uint32_t lo,
+					  const uint32_t *rk,
+					  const CtrKs<NR, CACHED, T4> &C,
+					  int32_t blk0, uint32_t carry[4],
+					  uint32_t d[16], uint32_t km)
+{
+#pragma unroll
+	for (int q = 0; q < SHIFT; q++)
+		d[q] = __builtin_amdgcn_bitop3_b32(d[q], carry[4 - SHIFT + q], km,
+						   0x78);
+#pragma unroll
+	for (int m = 0; m < 4; m++) {
+		uint32_t B[4];
+		C.block(smem, lo, rk, blk0 + m, B);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const int jj = SHIFT + 4 * m + q;
+			if (jj < 16)
+				d[jj] = __builtin_amdgcn_bitop3_b32(d[jj], B[q], km,
+								   0x78);
+			else
+				carry[q] = B[q];
+		}
+		if (m == 3 && SHIFT == 0) {
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				carry[q] = B[q];
+		}
+	}
 }
 
 /*
@@ -584,4 +622,7 @@ kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr10_any(bool uni, int prot);
 kfn_t sgpu_pick_ctr14_any(bool uni, int prot);
 kfn_t sgpu_pick_gcm(bool compact, bool uni, int nr, int prot);
+kfn_t sgpu_pick_ctr10_fast(int prot, int refix);
+kfn_t sgpu_pick_ctr14_fast(int prot, int refix);
+unsigned sgpu_ctr_fast_block(void);
 unsigned sgpu_gcm_block(bool uni);

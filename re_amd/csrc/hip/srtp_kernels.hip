@@ -764,6 +764,30 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 {
 	if (!c->n)
 		return 0;
+	if (mode == SGPU_MODE_CTR && shift < 0 && c->uniform == 2 &&
+	    !c->undo && !c->idx) {
+		/* device-planned single-key batch: lean kernel (k_ctr_fast.h),
+		 * then the forged-packet restore behind it (unprotect) */
+		KArgs a;
+		memset(&a, 0, sizeof(a));
+		a.arena = arena;
+		a.asz = arena_size;
+		a.comps = (const struct sgpu_comp *)g_table;
+		a.t0 = g_T0_dev;
+		a.verdict = c->verdict;
+		a.save = c->save;
+		a.c = *c;
+		kfn_t ff = nr == 10 ? sgpu_pick_ctr10_fast(prot, 0)
+				    : sgpu_pick_ctr14_fast(prot, 0);
+		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
+			       (hipStream_t)stream, sgpu_ctr_fast_block());
+		if (!e && !prot)
+			e = launch(nr == 10 ? sgpu_pick_ctr10_fast(0, 1)
+					    : sgpu_pick_ctr14_fast(0, 1),
+				   a, c->n, -1, (hipStream_t)stream,
+				   sgpu_ctr_fast_block());
+		return e;
+	}
 	kfn_t f = mode == SGPU_MODE_GCM ?
 			  sgpu_pick_gcm(true, c->uniform != 0, nr, prot)
 		  : nr == 10 ? sgpu_pick_ctr10(true, c->uniform != 0, shift, prot)

@@ -89,6 +89,8 @@ static struct {
 	int noplan;             /* RE_SRTP_NOPLAN: no device planners */
 	int general;            /* RE_SRTP_GENERAL: general engine only */
 	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
+	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
+				   device-planned single-key batches */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
 	int times;              /* RE_SRTP_TIMES: multi-session phases */
 	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
@@ -103,6 +105,7 @@ static void env_read(void)
 	g_env.noplan = getenv("RE_SRTP_NOPLAN") != NULL;
 	g_env.general = getenv("RE_SRTP_GENERAL") != NULL;
 	g_env.perclass = getenv("RE_SRTP_PERCLASS") != NULL;
+	g_env.nolean = getenv("RE_SRTP_NOLEAN") != NULL;
 	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
 	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
 	e = getenv("RE_SRTP_CHUNK");
@@ -118,6 +121,29 @@ static void env_init(void)
 	pthread_once(&g_env_once, env_read);
 }
 
+/* diagnostics counters (srtp_gpu_counter) */
+static uint64_t g_cnt_misses;   /* MAC/tag speculation misses */
+static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
+static uint64_t g_cnt_rejects;  /* device plans rejected */
+
+static void count(uint64_t *c, uint64_t v)
+{
+	__atomic_add_fetch(c, v, __ATOMIC_RELAXED);
+}
+
+uint64_t srtp_gpu_counter(const char *name)
+{
+	if (!name)
+		return 0;
+	if (!strcmp(name, "misses"))
+		return __atomic_load_n(&g_cnt_misses, __ATOMIC_RELAXED);
+	if (!strcmp(name, "folds"))
+		return __atomic_load_n(&g_cnt_folds, __ATOMIC_RELAXED);
+	if (!strcmp(name, "rejects"))
+		return __atomic_load_n(&g_cnt_rejects, __ATOMIC_RELAXED);
+	return 0;
+}
+
 int srtp_gpu_tune(const char *name, long value)
 {
 	env_init();
@@ -129,6 +155,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.general = value > 0;
 	else if (!strcmp(name, "perclass"))
 		g_env.perclass = value > 0;
+	else if (!strcmp(name, "nolean"))
+		g_env.nolean = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -2223,6 +2251,9 @@ static int run_classes(uint8_t *arena, uint64_t asz, struct sgpu_compact C,
 	}
 	if (!C.undo && !g_env.perclass) {
 		C.guard = po_d->skip;
+		/* one key and the planner's packet shape: lean kernels */
+		if (C.uniform == 1 && !g_env.nolean)
+			C.uniform = 2;
 		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
 					-1, prot, stream);
 	}
@@ -2753,6 +2784,8 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	if (err)
 		goto out;
 	if (nfail) {
+		count(&g_cnt_misses, nfail);
+		count(&g_cnt_folds, 1);
 		/* speculation missed: undo and fold exactly */
 		for (k = 0; k < nfl && !err; k++) {
 			struct sgpu_compact C = {
@@ -2926,8 +2959,14 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (err)
 		return err;
 	nfail = *(const uint32_t *)(po + 1);
-	if (po->fail)
+	if (po->fail) {
+		count(&g_cnt_rejects, 1);
 		return -1;
+	}
+	if (nfail) {
+		count(&g_cnt_misses, nfail);
+		count(&g_cnt_folds, 1);
+	}
 	plan_apply(s, po, prot, n, &old);
 	if (!nfail)
 		return 0;
@@ -3075,8 +3114,14 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (err)
 		return err;
 	nfail = *(const uint32_t *)(po + 1);
-	if (po->fail)
+	if (po->fail) {
+		count(&g_cnt_rejects, 1);
 		return -1;
+	}
+	if (nfail) {
+		count(&g_cnt_misses, nfail);
+		count(&g_cnt_folds, 1);
+	}
 	t[3] = times ? now_ms() : 0;
 	mplan_apply(sessv, nsess, sout_h, prot);
 	if (times)

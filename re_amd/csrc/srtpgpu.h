@@ -154,7 +154,10 @@ struct sgpu_compact {
 	uint32_t *save;                 /* [packet] tag word under the ROC */
 	uint32_t *nfail;                /* +1 per speculation miss (device) */
 	int undo;                       /* restore the pre-call bytes */
-	int uniform;                    /* every packet: one session context */
+	int uniform;                    /* every packet: one session context;
+					   2: and the device planner's shape
+					   (SD_RUN | SD_CIPHER, [hl, A) --
+					   the lean CTR kernels) */
 	const uint32_t *guard;          /* device word; nonzero: do nothing
 					   (a rejected device plan) or NULL */
 };

@@ -98,7 +98,7 @@ EXPORTS = (
     "srtp_decrypt_batch_dev", "srtcp_encrypt_batch_dev",
     "srtcp_decrypt_batch_dev", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
-    "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune",
+    "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune", "srtp_gpu_counter",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
 )
 
@@ -138,6 +138,8 @@ def load():
                                   ctypes.c_char_p, sz, ctypes.c_int]
     L.srtp_gpu_prof.argtypes = [ctypes.c_int]
     L.srtp_gpu_tune.argtypes = [ctypes.c_char_p, ctypes.c_long]
+    L.srtp_gpu_counter.argtypes = [ctypes.c_char_p]
+    L.srtp_gpu_counter.restype = ctypes.c_uint64
     L.srtp_gpu_prof_read.argtypes = [ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64),
                                      ctypes.POINTER(ctypes.c_uint64)]
@@ -309,6 +311,11 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
     sv = session_array(sessions)
     return getattr(lib(), opname + "_batch_dev")(sv, len(sv),
                                                  ctypes.byref(b))
+
+
+def counter(name):
+    """srtp_gpu_counter: "misses", "folds", "rejects" since load"""
+    return int(lib().srtp_gpu_counter(name.encode()))
 
 
 class tune:

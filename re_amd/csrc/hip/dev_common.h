@@ -53,9 +53,22 @@ __device__ __forceinline__ uint32_t sha_maj(uint32_t b, uint32_t c, uint32_t d)
 	return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
 }
 
-/* LDS T-table address of byte k of x for this lane (laneoff = (lane&31)*4) */
-#define TT_ADDR(x, k, laneoff) \
-	__builtin_amdgcn_perm((x), (laneoff), 0x0C0C0000u | ((4u + (k)) << 8))
+/* LDS T-table address of byte k of x for this lane (laneoff = (lane&31)*4):
+ * ((byte k of x) << 8) | laneoff, one v_perm_b32.  TT_B1_BITOP3: byte 1,
+ * already in place, as one v_bitop3_b32 ((x & 0xff00) | laneoff), which
+ * issues at twice the v_perm rate (profiles/r01_ubench_valu_rates.log) --
+ * measured no faster in the kernels (same-box A/B): off */
+#ifndef TT_B1_BITOP3
+#define TT_B1_BITOP3 0
+#endif
+template <int K>
+__device__ __forceinline__ uint32_t tt_addr(uint32_t x, uint32_t laneoff)
+{
+	if (K == 1 && TT_B1_BITOP3)
+		return __builtin_amdgcn_bitop3_b32(x, 0xff00u, laneoff, 0xEA);
+	return __builtin_amdgcn_perm(x, laneoff, 0x0C0C0000u | ((4u + K) << 8));
+}
+#define TT_ADDR(x, k, laneoff) tt_addr<(k)>((x), (laneoff))
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t *smem, uint32_t a)
 {

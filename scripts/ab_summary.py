@@ -1,8 +1,8 @@
-"""Summarise gpurun_out/var_*.json (scripts/ab_variants.sh): value, step
-time and the per-direction crypto kernel times of each variant run."""
+"""Summarise gpurun_out/ab_*.json (scripts/gpu_ab.sh): value, step time
+and the per-direction crypto kernel times of each run."""
 import glob, json, sys
 for f in sorted(glob.glob((sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
-                          + "/var_*.json")):
+                          + "/ab_*.json")):
     try:
         d = json.loads(open(f).read().strip().splitlines()[-1])
     except Exception as e:      # a failed run: show why

@@ -103,6 +103,13 @@ def main():
                          "D2H per step, chunk-pipelined); reported, not "
                          "the headline value")
     ap.add_argument("--e2e-chunks", type=int, default=8)
+    ap.add_argument("--udp", action="store_true",
+                    help="socket to socket: GPU protect + sendmmsg on one "
+                         "loopback UDP socket, recvmmsg + GPU unprotect on "
+                         "another (include/re_srtp_udp.h); reported in "
+                         "DESIGN.md, not the headline value")
+    ap.add_argument("--udp-seconds", type=float, default=3.0)
+    ap.add_argument("--udp-batch", type=int, default=1024)
     ap.add_argument("--same-device", action="store_true",
                     help="testing only: all ranks on cuda:0, gloo counters")
     ap.add_argument("--host-arrays", action="store_true",
@@ -120,6 +127,8 @@ def main():
     from re_amd import shard as S
     from re_amd import workload as W
 
+    if args.udp:
+        return udp_bench(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -415,6 +424,84 @@ def main():
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def udp_bench(args):
+    """Socket-to-socket rate of the batched UDP helper: a sender thread
+    protects config-2 packets (1200 B, AES_CM_128_HMAC_SHA1_80) on the GPU
+    and sendmmsg()s them over loopback; the receiving thread recvmmsg()s,
+    unprotects on the GPU and counts the authentic packets.  Loopback drops
+    what the receiver cannot absorb, so the rate is the receiver's."""
+    import ctypes
+    import socket
+    import threading
+    import torch
+    import re_amd.srtp as P
+    from re_amd import workload as W
+
+    torch.cuda.set_device(0)
+    P.load()
+    n = args.packets or (1 << 20)
+    arena, pos, end, cap = W.make_arena(n, 1200, s0=65000)
+    key = W.make_keys(1, 30)[0].tobytes()
+    a = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    b = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    a.bind(("127.0.0.1", 0))
+    b.bind(("127.0.0.1", 0))
+    for sk in (a, b):
+        for opt in (socket.SO_RCVBUF, socket.SO_SNDBUF):
+            sk.setsockopt(socket.SOL_SOCKET, opt, 1 << 26)
+    tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+    B = args.udp_batch
+    st = P.SrtpUdp(a.fileno(), tx=tx, batch=B, slot=1280)
+    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=B, slot=1280)
+    assert st.err == 0 and sr.err == 0, P.lib().srtp_gpu_error()
+    base = arena.ctypes.data
+    mbs = []
+    for i in range(n):                  # mbuf views into the arena
+        m = P.Mbuf()
+        m.buf = ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8))
+        m.size, m.pos, m.end = int(cap[i]), int(pos[i]), int(end[i])
+        mbs.append(ctypes.pointer(m))
+    addr = P.sockaddr_in(*b.getsockname())
+    sent = [0]
+    t_end = [0.0]
+
+    def sender():
+        k = 0
+        deadline = time.perf_counter() + args.udp_seconds
+        while time.perf_counter() < deadline and k < n:
+            r, _ = st.send(addr, mbs[k:k + B])
+            sent[0] += max(r, 0)
+            k += B
+        t_end[0] = time.perf_counter()
+
+    th = threading.Thread(target=sender)
+    t0 = time.perf_counter()
+    th.start()
+    last = None
+    while True:
+        got = sr.recv(200)
+        if got > 0:
+            last = time.perf_counter()
+        elif not th.is_alive():
+            break
+    th.join()
+    rcv, ok, _ = sr.stats()
+    T = (last or t0) - t0
+    line = {"metric": "socket-to-socket SRTP protect+send / recv+unprotect "
+                      "over loopback UDP, 1200B RTP pkts (batched UDP helper)",
+            "value": round(ok * 1200 / T / 2**30, 4) if T > 0 else 0.0,
+            "unit": "GiB/s", "mpkt_s": round(ok / T / 1e6, 4) if T else 0.0,
+            "sent": sent[0], "received": rcv, "authentic": ok,
+            "seconds": round(T, 3), "batch": B,
+            "send_side_mpkt_s": round(sent[0] / (t_end[0] - t0) / 1e6, 4),
+            "data": "synthetic", "dtype": "u8",
+            "config": {"workload": "config2 packets over loopback",
+                       "suite": "AES_CM_128_HMAC_SHA1_80"}}
+    print(json.dumps(line))
+    st.close()
+    sr.close()
 
 
 def ctypes_stream(stream):

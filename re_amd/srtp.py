@@ -99,8 +99,14 @@ EXPORTS = (
     "srtcp_decrypt_batch_dev", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
     "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune", "srtp_gpu_counter",
+    "srtp_udp_alloc", "srtp_udp_recv", "srtp_udp_send", "srtp_udp_stats",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
 )
+
+# srtp_udp_recv_h (include/re_srtp_udp.h)
+UDP_RECV_H = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32,
+                              ctypes.POINTER(Mbuf), ctypes.c_int,
+                              ctypes.c_void_p)
 
 _lib = None
 
@@ -143,6 +149,14 @@ def load():
     L.srtp_gpu_prof_read.argtypes = [ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64),
                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.srtp_udp_alloc.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, vp,
+                                 sz, sz, UDP_RECV_H, vp]
+    L.srtp_udp_recv.argtypes = [vp, ctypes.c_int]
+    L.srtp_udp_send.argtypes = [vp, vp, ctypes.c_uint32,
+                                ctypes.POINTER(ctypes.POINTER(Mbuf)),
+                                ctypes.POINTER(ctypes.c_int), sz]
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.srtp_udp_stats.argtypes = [vp, u64p, u64p, u64p]
     L.mbuf_alloc.restype = ctypes.POINTER(Mbuf)
     L.mbuf_alloc.argtypes = [sz]
     L.mbuf_resize.argtypes = [ctypes.POINTER(Mbuf), sz]
@@ -222,6 +236,55 @@ def alloc_many(n, suite, keys, flags=0):
     if e:
         return e, []
     return 0, [Srtp.wrap(arr[i], suite) for i in range(n)]
+
+
+class SrtpUdp:
+    """struct srtp_udp (include/re_srtp_udp.h): GPU SRTP between a UDP
+    socket and the RTP layer.  handler(src_bytes, mbuf, err) per datagram;
+    the mbuf views the receive arena only during the call."""
+
+    def __init__(self, fd, rx=None, tx=None, batch=256, slot=1536,
+                 handler=None):
+        self._cb = UDP_RECV_H(self._recv)
+        self.handler = handler
+        self.ptr = ctypes.c_void_p()
+        self.err = lib().srtp_udp_alloc(
+            ctypes.byref(self.ptr), fd, rx.ptr if rx else None,
+            tx.ptr if tx else None, batch, slot, self._cb, None)
+
+    def _recv(self, src, srclen, mb, err, arg):
+        if self.handler:
+            self.handler(ctypes.string_at(src, srclen), mb, err)
+
+    def recv(self, timeout_ms=100):
+        return lib().srtp_udp_recv(self.ptr, timeout_ms)
+
+    def send(self, addr, mbufs):
+        """addr: bytes of a struct sockaddr; returns (sent, errs)"""
+        n = len(mbufs)
+        arr = (ctypes.POINTER(Mbuf) * n)(*mbufs)
+        errs = (ctypes.c_int * n)()
+        r = lib().srtp_udp_send(self.ptr, addr, len(addr), arr, errs, n)
+        return r, list(errs)
+
+    def stats(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib().srtp_udp_stats(self.ptr, ctypes.byref(a), ctypes.byref(b),
+                             ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def close(self):
+        if self.ptr:
+            lib().mem_deref(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+
+def sockaddr_in(host, port):
+    """struct sockaddr_in bytes (AF_INET) for srtp_udp_send"""
+    import socket
+    import struct
+    return struct.pack("<H", socket.AF_INET) + struct.pack(">H", port) + \
+        socket.inet_aton(host) + bytes(8)
 
 
 def new_mbuf(data, size, pos=0):

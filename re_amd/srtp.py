@@ -76,6 +76,13 @@ class SrtpBatchDev(ctypes.Structure):
                 ("stream", ctypes.c_void_p)]
 
 
+class DtlsSecret(ctypes.Structure):
+    """struct srtp_dtls_secret (include/re_srtp_keying.h)"""
+    _fields_ = [("master", ctypes.c_uint8 * 48),
+                ("client_random", ctypes.c_uint8 * 32),
+                ("server_random", ctypes.c_uint8 * 32)]
+
+
 class StreamState(ctypes.Structure):
     _fields_ = [("replay_rtp_bitmap", ctypes.c_uint64),
                 ("replay_rtp_lix", ctypes.c_uint64),
@@ -100,6 +107,8 @@ EXPORTS = (
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
     "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune", "srtp_gpu_counter",
     "srtp_udp_alloc", "srtp_udp_recv", "srtp_udp_send", "srtp_udp_stats",
+    "srtp_dtls_key_size", "srtp_keyinfo_split", "srtp_dtls_keying_many",
+    "srtp_alloc_dtls_many",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
 )
 
@@ -157,6 +166,18 @@ def load():
                                 ctypes.POINTER(ctypes.c_int), sz]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.srtp_udp_stats.argtypes = [vp, u64p, u64p, u64p]
+    L.srtp_dtls_key_size.argtypes = [ctypes.c_int]
+    L.srtp_dtls_key_size.restype = sz
+    L.srtp_keyinfo_split.argtypes = [ctypes.c_int, ctypes.c_char_p,
+                                     ctypes.c_char_p, sz, ctypes.c_char_p,
+                                     sz]
+    L.srtp_dtls_keying_many.argtypes = [ctypes.POINTER(DtlsSecret), sz,
+                                        ctypes.c_int, ctypes.c_char_p,
+                                        ctypes.c_char_p]
+    L.srtp_alloc_dtls_many.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                       sz, ctypes.c_int,
+                                       ctypes.POINTER(DtlsSecret),
+                                       ctypes.c_int, ctypes.c_int]
     L.mbuf_alloc.restype = ctypes.POINTER(Mbuf)
     L.mbuf_alloc.argtypes = [sz]
     L.mbuf_resize.argtypes = [ctypes.POINTER(Mbuf), sz]
@@ -285,6 +306,46 @@ def sockaddr_in(host, port):
     import struct
     return struct.pack("<H", socket.AF_INET) + struct.pack(">H", port) + \
         socket.inet_aton(host) + bytes(8)
+
+
+def dtls_secrets(items):
+    """[(master 48 B, client_random 32 B, server_random 32 B)] -> array"""
+    arr = (DtlsSecret * max(1, len(items)))()
+    for i, (m, c, r) in enumerate(items):
+        ctypes.memmove(arr[i].master, m, 48)
+        ctypes.memmove(arr[i].client_random, c, 32)
+        ctypes.memmove(arr[i].server_random, r, 32)
+    return arr
+
+
+def keyinfo_split(suite, keymat):
+    """srtp_keyinfo_split -> (err, cli_key, srv_key)"""
+    n = lib().srtp_dtls_key_size(suite)
+    cli, srv = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
+    e = lib().srtp_keyinfo_split(suite, keymat, cli, 64, srv, 64)
+    return e, cli.raw[:n], srv.raw[:n]
+
+
+def dtls_keying_many(suite, items):
+    """srtp_dtls_keying_many -> (err, [cli_key], [srv_key])"""
+    n, size = len(items), lib().srtp_dtls_key_size(suite)
+    cli = ctypes.create_string_buffer(max(1, n * size))
+    srv = ctypes.create_string_buffer(max(1, n * size))
+    e = lib().srtp_dtls_keying_many(dtls_secrets(items), n, suite, cli, srv)
+    return e, [cli.raw[i * size:(i + 1) * size] for i in range(n)], \
+        [srv.raw[i * size:(i + 1) * size] for i in range(n)]
+
+
+def alloc_dtls_many(suite, items, is_client, flags=0):
+    """srtp_alloc_dtls_many -> (err, [tx Srtp], [rx Srtp])"""
+    n = len(items)
+    tx, rx = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+    e = lib().srtp_alloc_dtls_many(tx, rx, n, suite, dtls_secrets(items),
+                                   1 if is_client else 0, flags)
+    if e:
+        return e, [], []
+    return 0, [Srtp.wrap(tx[i], suite) for i in range(n)], \
+        [Srtp.wrap(rx[i], suite) for i in range(n)]
 
 
 def new_mbuf(data, size, pos=0):

@@ -1,0 +1,62 @@
+"""DTLS-SRTP keying on the CPU side (no GPU): the split of
+tls_srtp_keyinfo (src/tls/openssl/tls.c:1140-1154) in the product library
+and a pure-Python restatement of the exporter PRF (RFC 5705 with the TLS 1.2
+PRF, RFC 5246 5: P_SHA256, label "EXTRACTOR-dtls_srtp") against the golden
+vectors OpenSSL's own PRF produced (tests/golden/dtls_srtp_keying.json,
+oracle/gen_dtls_prf.c)."""
+import errno
+import hashlib
+import hmac
+import json
+import os
+
+import pytest
+
+import re_amd.srtp as P
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def cases():
+    with open(os.path.join(ROOT, "tests", "golden",
+                           "dtls_srtp_keying.json")) as f:
+        return json.load(f)["cases"]
+
+
+def p_sha256(secret, seed, n):
+    """RFC 5246 5 -- test restatement, not the product (GPU, dtls_prf.hip)"""
+    out, a = b"", seed
+    while len(out) < n:
+        a = hmac.new(secret, a, hashlib.sha256).digest()
+        out += hmac.new(secret, a + seed, hashlib.sha256).digest()
+    return out[:n]
+
+
+def test_prf_restatement_vs_openssl(cases):
+    assert len(cases) == 32
+    for c in cases:
+        seed = b"EXTRACTOR-dtls_srtp" + bytes.fromhex(c["client_random"]) + \
+            bytes.fromhex(c["server_random"])
+        km = bytes.fromhex(c["keymat"])
+        assert p_sha256(bytes.fromhex(c["master"]), seed, len(km)) == km
+
+
+def test_split_vs_golden(cases):
+    for c in cases:
+        e, cli, srv = P.keyinfo_split(c["suite"], bytes.fromhex(c["keymat"]))
+        assert e == 0
+        assert (cli.hex(), srv.hex()) == (c["cli_key"], c["srv_key"])
+        assert len(cli) == P.key_len(c["suite"]) + P.salt_len(c["suite"])
+
+
+def test_split_errors():
+    L = P.lib()
+    km = bytes(88)
+    # AES_256_CM_* have no DTLS-SRTP profile in tls_srtp_keyinfo (ENOSYS)
+    for suite in (2, 3, 9):
+        assert P.keyinfo_split(suite, km)[0] == errno.ENOSYS
+        assert L.srtp_dtls_key_size(suite) == 0
+    out = P.ctypes.create_string_buffer(64)
+    assert L.srtp_keyinfo_split(1, km, out, 29, out, 64) == errno.EOVERFLOW
+    assert L.srtp_keyinfo_split(1, None, out, 64, out, 64) == errno.EINVAL

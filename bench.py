@@ -103,6 +103,9 @@ def main():
                          "D2H per step, chunk-pipelined); reported, not "
                          "the headline value")
     ap.add_argument("--e2e-chunks", type=int, default=8)
+    ap.add_argument("--rtcp", action="store_true",
+                    help="SRTCP: the same arena as RTCP packets through "
+                         "srtcp_*_batch_dev (device-planned SRTCP)")
     ap.add_argument("--udp", action="store_true",
                     help="socket to socket: GPU protect + sendmmsg on one "
                          "loopback UDP socket, recvmmsg + GPU unprotect on "
@@ -166,8 +169,14 @@ def main():
         s0 = S.shard_seq0(rank, n, 65000)   # this shard's first seq
     lengths = cfg["length"] if cfg["length"] else W.mixed_lengths(n)
     sess = W.random_sessions(n, nsess) if nsess > 1 else None
-    arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
-                                          sess=sess)
+    if args.rtcp:
+        assert nsess == 1 and cfg["length"], "--rtcp: configs 2 and 3"
+        arena_h, pos, end, cap = W.make_rtcp_arena(n, lengths)
+    else:
+        arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
+                                              sess=sess)
+    OPS = ("srtcp_encrypt", "srtcp_decrypt") if args.rtcp else \
+        ("srtp_encrypt", "srtp_decrypt")
     log("workload built (%d packets)" % n)
     arena = torch.from_numpy(arena_h).to(dev)
     plain = arena.clone() if not args.no_verify else None
@@ -180,7 +189,7 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = ctypes_stream(stream)
     L = cfg["length"] or 800
-    tag = P.tag_len(suite)
+    tag = P.tag_len(suite) + (4 if args.rtcp else 0)   # + E||index
     rtp_bytes = int(np.asarray(end - pos, dtype=np.int64).sum())
 
     def make_sessions():
@@ -259,14 +268,14 @@ def main():
         if args.e2e:
             p_d.copy_(pos_d)
             e_d.copy_(end_d)
-            e2e_pass("srtp_encrypt", tx, err_ed)
-            e2e_pass("srtp_decrypt", rx, err_dd)
+            e2e_pass(OPS[0], tx, err_ed)
+            e2e_pass(OPS[1], rx, err_dd)
             return 0
         if use_dev:
             p_d.copy_(pos_d)
             e_d.copy_(end_d)
-            for opname, ss, er in (("srtp_encrypt", tx, err_ed),
-                                   ("srtp_decrypt", rx, err_dd)):
+            for opname, ss, er in ((OPS[0], tx, err_ed),
+                                   (OPS[1], rx, err_dd)):
                 rc = P.device_batch_dev(opname, ss, arena.data_ptr(),
                                         arena.numel(), p_d.data_ptr(),
                                         e_d.data_ptr(), cap_d.data_ptr(),
@@ -277,10 +286,10 @@ def main():
             return 0
         np.copyto(p, pos)
         np.copyto(e, end)
-        rc, _ = P.device_batch("srtp_encrypt", tx, arena.data_ptr(),
+        rc, _ = P.device_batch(OPS[0], tx, arena.data_ptr(),
                                arena.numel(), p, e, cap, sess, sptr, err_e)
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
-        rc, _ = P.device_batch("srtp_decrypt", rx, arena.data_ptr(),
+        rc, _ = P.device_batch(OPS[1], rx, arena.data_ptr(),
                                arena.numel(), p, e, cap, sess, sptr, err_d)
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
         return np.count_nonzero(err_e) + np.count_nonzero(err_d)
@@ -394,8 +403,10 @@ def main():
                              for k, v in d.items()} for d in kern]}
     gib = tot_bytes / T / 2**30
     line = {
-        "metric": METRIC + (" [end-to-end: host pinned memory, incl. "
-                            "PCIe H2D/D2H]" if args.e2e else ""),
+        "metric": (METRIC.replace("SRTP", "SRTCP").replace("RTP", "RTCP")
+                   if args.rtcp else METRIC) +
+        (" [end-to-end: host pinned memory, incl. PCIe H2D/D2H]"
+         if args.e2e else ""),
         "value": round(gib, 4),
         "unit": "GiB/s",
         "mpkt_s": round(tot_pkts / T / 1e6, 4),

@@ -419,6 +419,8 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 		}
 		vd &= (uint8_t)~SV_CIPHERED;
 	}
+	if (undo && a.c.rtcp)
+		return;
 	if (undo) {
 		/* compact undo: the word under the ROC back (srtp.c:342-344) */
 		uint8_t *tp = pkt + j.tag_off;

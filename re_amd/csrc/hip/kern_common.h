@@ -269,6 +269,77 @@ struct KArgs {
 };
 
 /*
+ * SRTCP job of a device-planned packet, exactly as plan_rtcp_enc /
+ * plan_rtcp_dec (re_amd/csrc/host/srtp.c) build it (srtcp.c:31-140,
+ * 143-287 of the reference): cipher region from byte 8, E || index
+ * trailer, HMAC over the packet with the trailer (protect) or up to the
+ * tag (unprotect), GCM with the AAD forms of srtcp.c:82-102 / 239-262.
+ */
+template <int MODE, bool PROT>
+__device__ __forceinline__ bool rtcp_job(const KArgs &a,
+					 const struct sgpu_compact &c,
+					 uint32_t p, uint64_t d, uint8_t vd,
+					 struct sgpu_job &j)
+{
+	const uint32_t comp = c.compmap[0];
+	const struct sgpu_comp *cp = a.comps + comp;
+	const uint32_t off = c.pos[p];
+	const uint32_t L = c.end[p] - off;
+	const uint32_t ix = (uint32_t)d & 0x7fffffffu;
+	const uint32_t E = ((uint32_t)d >> 31) & 1u;
+	const uint32_t T = cp->tag_len;
+	const bool hmac = (cp->flags & 2u) != 0;
+	j.off = off;
+	j.comp = comp;
+	j.ssrc = ((const uint32_t *)(c.hdr + p))[0];
+	j.ixhi = ix >> 16;
+	j.ixlo = ix & 0xffffu;
+	j.trailer = E << 31 | ix;
+	j.c_off = 8;
+	j.t_off = 0;
+	if (PROT) {
+		if (MODE == SGPU_MODE_CTR) {
+			j.flags = SJ_PROTECT | SJ_STORE_TRAIL |
+				  (E ? SJ_CIPHER : 0u) |
+				  (hmac ? (SJ_HMAC | SJ_TRAILER) : 0u);
+			j.c_len = L - 8u;
+			j.t_off = L;
+			j.a_len = L;
+			j.tag_off = L + 4u;
+		}
+		else {
+			j.flags = SJ_PROTECT | SJ_GCM | SJ_TRAILER |
+				  SJ_STORE_TRAIL | (E ? SJ_CIPHER : 0u);
+			j.a_len = E ? 8u : L;
+			j.c_len = E ? L - 8u : 0u;
+			j.tag_off = L;
+			j.t_off = L + 16u;
+		}
+		return true;
+	}
+	if (MODE == SGPU_MODE_CTR) {
+		const uint32_t tag_start = L - T, eix_start = L - T - 4u;
+		j.c_len = eix_start - 8u;
+		j.a_len = tag_start;
+		j.tag_off = tag_start;
+		if (c.undo)
+			j.flags = (vd & SV_CIPHERED) ? SJ_CIPHER : 0u;
+		else
+			j.flags = SJ_HMAC | ((E && (cp->flags & 1u)) ?
+					     (SJ_CIPHER | SJ_CIPHER_IF_OK) : 0u);
+	}
+	else {
+		const uint32_t tag_start = L - 4u - 16u;
+		j.tag_off = tag_start;
+		j.a_len = E ? 8u : tag_start;
+		j.c_len = E ? tag_start - 8u : 0u;
+		j.flags = c.undo ? (SJ_GCM | SJ_CIPHER | SJ_UNDO)
+				 : (SJ_GCM | SJ_TRAILER | (E ? SJ_CIPHER : 0u));
+	}
+	return true;
+}
+
+/*
  * Job of thread t.  General path: jobs[t], results at slot t.  Compact
  * path: packet p = idx[base+t] (or base+t); the job is derived exactly as
  * plan_rtp_enc / plan_rtp_dec (re_amd/csrc/host/srtp.c) build it, from the
@@ -305,6 +376,8 @@ __device__ __forceinline__ bool get_job(const KArgs &a, uint32_t t,
 		if (MODE == SGPU_MODE_GCM && !(vd & SV_CIPHERED))
 			return true;
 	}
+	if (c.rtcp)
+		return rtcp_job<MODE, PROT>(a, c, p, d, vd, j);
 	const uint32_t comp = c.compmap[c.sess ? c.sess[p] : 0u];
 	const uint32_t off = c.pos[p];
 	const uint32_t L = c.end[p] - off;

@@ -499,6 +499,91 @@ k_plan_desc(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 		out->s_l_last = wrap ? seq : (seq > sb ? seq : sb);
 }
 
+/* ------------------------------------------------------------------ */
+/* Device-side planning of a single-stream SRTCP batch (srtpgpu.h).    */
+
+__device__ __forceinline__ uint32_t rplan_eix(const struct sgpu_rplan_in &in,
+					      const uint32_t *eix, uint32_t i)
+{
+	/* the E || index word at end - 4 - tag (k_parse, tl = 0, 4, 10) */
+	return eix[3 * i + (in.tag == 0 ? 0 : in.tag == 4 ? 1 : 2)];
+}
+
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_plan_rtcp(const struct sgpu_rplan_in in, const struct sgpu_hdr *hdr,
+	    const uint32_t *eix, const uint32_t *pos, const uint32_t *end,
+	    const uint32_t *cap, uint64_t asz, uint64_t *desc,
+	    struct sgpu_plan_out *out)
+{
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	if (i >= in.n)
+		return;
+	const struct sgpu_hdr h = hdr[i];
+	const uint32_t ssrc0 = in.ssrc_any ? hdr[0].ssrc : in.ssrc;
+	const uint32_t L = end[i] - pos[i];
+	uint32_t f = 0;
+	if (h.hdr_len == 0xffffffffu)
+		f |= SPF_PARSE;                 /* < 8 bytes: EBADMSG */
+	else if (h.ssrc != ssrc0)
+		f |= SPF_SSRC;
+	if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
+	    (cap && (end[i] > cap[i] || cap[i] > asz)))
+		f |= SPF_BAD;
+	uint32_t ix, E;
+	if (in.prot) {
+		if (cap && (uint64_t)end[i] + in.need > (uint64_t)cap[i])
+			f |= SPF_CAP;           /* ENOMEM (cap_short) */
+		ix = (in.rtcp_index + i + 1u) & 0x7fffffffu;    /* srtcp.c:54 */
+		E = in.encrypted;
+	}
+	else {
+		/* srtcp.c:166-172 (and 239-241 for GCM): room for E || index,
+		 * the tag, and the GCM tag before them */
+		if (L < 8u + 4u + in.tag + (in.gcm ? 16u : 0u))
+			f |= SPF_PARSE;
+		const uint32_t v = rplan_eix(in, eix, i);
+		ix = v & 0x7fffffffu;
+		E = v >> 31;
+		if (in.hmac) {
+			/* replay (srtcp.c:208-209), speculated: every index new
+			 * and increasing */
+			bool ok;
+			if (i == 0) {
+				if (ix > in.lix) {
+					ok = true;
+				}
+				else {
+					const uint64_t dl = in.lix - ix;
+					ok = dl < 64 && !(in.bitmap & (1ull << dl));
+				}
+			}
+			else {
+				ok = ix > (rplan_eix(in, eix, i - 1) & 0x7fffffffu);
+			}
+			if (!ok)
+				f |= SPF_REPLAY;
+		}
+	}
+	desc[i] = ((uint64_t)(ix & 0x7fffffffu)) | ((uint64_t)E << 31) |
+		  ((uint64_t)SD_RUN << 48);
+	const uint32_t t0 = in.n > SGPU_PLAN_TAIL ? in.n - SGPU_PLAN_TAIL : 0u;
+	if (i >= t0)
+		out->tail_ix[i - t0] = ix;
+	if (i == 0) {
+		out->ssrc0 = h.ssrc;
+		out->hl0 = 8;
+	}
+	if (f)
+		atomicOr(&out->fail, f);
+}
+
+extern "C" int sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
+			      const struct sgpu_hdr *hdr, const uint32_t *eix,
+			      const uint32_t *pos, const uint32_t *end,
+			      const uint32_t *cap, uint64_t arena_size,
+			      uint64_t *desc, struct sgpu_plan_out *out,
+			      void *stream);
+
 /* ================================================================== */
 /* C-ABI shim                                                          */
 
@@ -1009,6 +1094,25 @@ extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
 			   *in, hdr, (const uint32_t *)scratch, desc, out);
 	hipLaunchKernelGGL(k_plan_final, dim3(1), dim3(64), 0, st, out);
 	return herr(hipGetLastError(), "plan launch");
+}
+
+extern "C" int sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
+			      const struct sgpu_hdr *hdr, const uint32_t *eix,
+			      const uint32_t *pos, const uint32_t *end,
+			      const uint32_t *cap, uint64_t arena_size,
+			      uint64_t *desc, struct sgpu_plan_out *out,
+			      void *stream)
+{
+	hipStream_t st = (hipStream_t)stream;
+	if (!in->n)
+		return EINVAL;
+	hipLaunchKernelGGL(k_plan_rtcp, dim3((in->n + PLAN_BLOCK - 1) /
+					     PLAN_BLOCK), dim3(PLAN_BLOCK), 0,
+			   st, *in, hdr, eix, pos, end, cap, arena_size, desc,
+			   out);
+	/* guards: the SRTCP cipher region starts at byte 8 (class 2) */
+	hipLaunchKernelGGL(k_plan_final, dim3(1), dim3(64), 0, st, out);
+	return herr(hipGetLastError(), "rtcp plan launch");
 }
 
 __global__ void __launch_bounds__(256)

@@ -2349,7 +2349,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0};
 		err = run_classes(b->arena, b->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -2565,7 +2565,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			struct sgpu_compact C = {
 				up_d, up_d + n, hd_d, desc_d, NULL,
 				(const uint32_t *)w->cm.d, NULL, 0,
-				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL};
+				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL, 0};
 			err = run_classes(b->arena, b->arena_size, C, c0,
 					  po_d, prot, stream);
 		}
@@ -2761,7 +2761,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				(const uint32_t *)w->cm.d,
 				fl[q].has_idx ? idx_d : NULL, fl[q].base,
 				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1,
-				NULL};
+				NULL, 0};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[q].shift, prot, stream);
@@ -2798,7 +2798,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				c0->mode == SGPU_MODE_GCM ?
 				&((struct sgpu_plan_out *)w->pl.d)->fail :
 				&((struct sgpu_plan_out *)w->pl.d)->
-					  skip[fl[k].shift]};
+					  skip[fl[k].shift], 0};
 			C.uniform = planned != 2 && nsess == 1;
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
@@ -2940,7 +2940,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1, NULL};
+			save_d, nfail_d, 0, 1, NULL, 0};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -2975,7 +2975,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 1, NULL};
+			save_d, nfail_d, 1, 1, NULL, 0};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -2986,6 +2986,149 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (err)
 		return err;
 	plan_unapply(s, ns0, &old);
+	return -1;
+}
+
+/*
+ * Single-stream SRTCP batch planned and processed on the device (the
+ * SRTCP counterpart of dev_planned): k_parse (with the E || index words),
+ * k_plan_rtcp, the compact crypto launch, the per-packet results; one host
+ * synchronisation.  -1: not plannable or a forged packet (undone), else 0
+ * / errno.
+ */
+static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
+{
+	const int prot = op == OP_RTCP_ENC;
+	const struct comp *c0 = &s->rtcp;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const size_t n = d->n;
+	const uint32_t T = c0->tag_len;             /* 0 for GCM */
+	const uint32_t grow = 4u + T + (gcm ? 16u : 0u);
+	const unsigned ns0 = s->nstreams;
+	struct srtp_stream old;
+	struct sgpu_rplan_in in;
+	struct sgpu_plan_out *po, *po_d;
+	struct sgpu_hdr *hd_d;
+	uint64_t *desc_d;
+	uint32_t *es_d, *save_d, *nfail_d, *eix_d, nfail, cm = c0->dev;
+	uint8_t *vd_d;
+	void *stream = d->stream;
+	struct ws *w = ws_get();
+	int err;
+
+	if (!w)
+		return ENOMEM;
+	err = pool_reserve(w, &w->hd, n * (sizeof(struct sgpu_hdr) + 12));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 12);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out) + 64);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (err)
+		return err;
+	hd_d = (struct sgpu_hdr *)w->hd.d;
+	eix_d = (uint32_t *)(w->hd.d + n * sizeof(struct sgpu_hdr));
+	desc_d = (uint64_t *)w->dsc.d;
+	nfail_d = (uint32_t *)w->vs.d;
+	save_d = (uint32_t *)(w->vs.d + 64);
+	vd_d = w->vs.d + 64 + n * 4;
+	po = (struct sgpu_plan_out *)w->pl.h;
+	po_d = (struct sgpu_plan_out *)w->pl.d;
+	es_d = (uint32_t *)w->es.d;
+
+	memset(&in, 0, sizeof(in));
+	in.n = (uint32_t)n;
+	in.prot = (uint32_t)prot;
+	in.ssrc_any = !s->nstreams;
+	in.ssrc = s->nstreams ? s->streams[0].ssrc : 0;
+	in.rtcp_index = s->nstreams ? s->streams[0].rtcp_index : 0;
+	in.lix = s->nstreams ? s->streams[0].replay_rtcp.lix : 0;
+	in.bitmap = s->nstreams ? s->streams[0].replay_rtcp.bitmap : 0;
+	in.tag = T;
+	in.gcm = (uint32_t)gcm;
+	in.hmac = (uint32_t)c0->has_hmac;
+	in.encrypted = (uint32_t)(gcm ? c0->encrypted : c0->has_aes);
+	in.need = grow;
+	{
+		/* parse (+ E || index words) + end copy + zeroed counters and
+		 * plan + comp map, one launch */
+		struct sgpu_prologue pro = {
+			es_d, nfail_d, (uint32_t *)po_d, 1,
+			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm};
+		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
+					  d->end, hd_d, prot ? NULL : eix_d,
+					  (uint32_t)n, 1, &pro, stream);
+	}
+	if (!err)
+		err = sgpu_plan_rtcp(&in, hd_d, eix_d, d->pos, es_d, d->cap,
+				     d->arena_size, desc_d, po_d, stream);
+	if (!err) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, NULL,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 0, gcm ? 0 : 1,
+			gcm ? &po_d->fail : &po_d->skip[2], 1};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
+	}
+	if (!err)
+		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
+					(uint32_t)n,
+					prot ? (int32_t)grow : -(int32_t)grow,
+					stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)   /* pinned, next to the plan (see dev_planned) */
+		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	nfail = *(const uint32_t *)(po + 1);
+	if (po->fail) {
+		count(&g_cnt_rejects, 1);
+		return -1;
+	}
+	/* the stream (stream.c:45-67) and its SRTCP state after the batch */
+	if (!s->nstreams) {
+		memset(&s->streams[0], 0, sizeof(s->streams[0]));
+		s->streams[0].ssrc = po->ssrc0;
+		s->nstreams = 1;
+	}
+	old = s->streams[0];
+	if (prot)
+		s->streams[0].rtcp_index =
+			(s->streams[0].rtcp_index + (uint32_t)n) & 0x7fffffffu;
+	else if (c0->has_hmac)
+		s->streams[0].replay_rtcp =
+			plan_replay(&s->streams[0].replay_rtcp, po, n);
+	if (!nfail)
+		return 0;
+	count(&g_cnt_misses, nfail);
+	count(&g_cnt_folds, 1);
+	/* a forged packet: undo on the device, fold on the host engine */
+	{
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, NULL,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 1, gcm ? 0 : 1,
+			gcm ? &po_d->fail : &po_d->skip[2], 1};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, gcm ? 0 : 2, 0, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, es_d, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	s->streams[0] = old;
+	s->nstreams = ns0;
 	return -1;
 }
 
@@ -3093,7 +3236,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -3136,7 +3279,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 0, NULL};
+			save_d, nfail_d, 1, 0, NULL, 0};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -3228,6 +3371,13 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 	    !d->sess && sessv[0]->nstreams <= 1 &&
 	    !g_env.noplan && !g_env.general) {
 		int r = dev_planned(op, sessv[0], d);
+		if (r >= 0)
+			return r;
+	}
+	if ((op == OP_RTCP_ENC || op == OP_RTCP_DEC) && nsess == 1 &&
+	    !d->sess && sessv[0]->nstreams <= 1 &&
+	    !g_env.noplan && !g_env.general) {
+		int r = dev_planned_rtcp(op, sessv[0], d);
 		if (r >= 0)
 			return r;
 	}

@@ -160,7 +160,18 @@ struct sgpu_compact {
 					   the lean CTR kernels) */
 	const uint32_t *guard;          /* device word; nonzero: do nothing
 					   (a rejected device plan) or NULL */
+	int rtcp;                       /* SRTCP packets: descriptor = SRTCP
+					   index | E << 31 (sgpu_rdesc) */
 };
+
+/* SRTCP descriptor: bits 0..30 SRTCP index, bit 31 E, bits 48..63 SD_* */
+static inline uint64_t sgpu_rdesc(uint32_t index, uint32_t e, uint32_t flags)
+{
+	return (uint64_t)(index & 0x7fffffffu) | ((uint64_t)(e & 1u) << 31) |
+	       ((uint64_t)flags << 48);
+}
+
+
 
 /* launch the compact kernel of class (mode, nr, shift, prot) */
 int   sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
@@ -278,6 +289,35 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 		     void *scratch, size_t scratch_bytes,
 		     struct sgpu_plan_out *out, uint32_t *order,
 		     void *stream);
+
+/*
+ * Device-side planning of a single-stream SRTCP batch (srtcp_encrypt
+ * srtcp.c:31-140, srtcp_decrypt srtcp.c:143-287): protect numbers the
+ * packets rtcp_index + 1, + 2, ...; unprotect reads E || index from each
+ * packet and, for the HMAC suites, speculates every index new and
+ * increasing (replay_rtcp, replay.c:32-62) and every tag authentic.
+ * out->fail != 0 means "plan on the host"; skip[2] guards the launches
+ * (SRTCP's cipher region starts at byte 8: class 2).
+ */
+struct sgpu_rplan_in {
+	uint32_t n;
+	uint32_t prot;
+	uint32_t ssrc_any;      /* no stream yet: take packet 0's SSRC */
+	uint32_t ssrc;
+	uint32_t rtcp_index;    /* stream's index (protect) */
+	uint32_t tag;           /* HMAC tag length (0 for GCM) */
+	uint32_t gcm;
+	uint32_t hmac;          /* replay-checked (HMAC suites) */
+	uint32_t encrypted;     /* E for protect (has_aes / encrypted) */
+	uint32_t need;          /* protect: bytes appended */
+	uint64_t lix, bitmap;   /* replay_rtcp */
+};
+
+int   sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
+		     const struct sgpu_hdr *hdr, const uint32_t *eix,
+		     const uint32_t *pos, const uint32_t *end,
+		     const uint32_t *cap, uint64_t arena_size, uint64_t *desc,
+		     struct sgpu_plan_out *out, void *stream);
 
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */

@@ -126,6 +126,23 @@ def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
     return arena.reshape(-1), pos, end, cap
 
 
+def make_rtcp_arena(npkts, length, seed=SEED_PAYLOAD, first=0):
+    """SRTCP workload: RTCP packets of `length` bytes (one SR-typed message
+    header V=2, PT=200, length field = length/4 - 1, SSRC_BASE), payload
+    from the same generators as make_arena.  Returns (arena, pos, end, cap).
+    """
+    arena, pos, end, cap = make_arena(npkts, length, seed=seed, first=first)
+    a = arena.reshape(npkts, -1)
+    words = (int(length) // 4 - 1) & 0xffff
+    a[:, 0] = 0x80
+    a[:, 1] = 200
+    a[:, 2] = words >> 8
+    a[:, 3] = words & 0xff
+    for k in range(4):
+        a[:, 4 + k] = (SSRC_BASE >> (24 - 8 * k)) & 0xff
+    return arena, pos, end, cap
+
+
 def mixed_lengths(npkts, seed=SEED_PAYLOAD + 1):
     """config 4: Bernoulli(0.5) -> 200 or 1400 B"""
     v = xs_next(xs_state(seed, np.arange(npkts)))

@@ -47,33 +47,63 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(cfg):
-    """Reference src/srtp (oracle/_ref, OpenSSL) on the host cores, bounded
-    sample; falls back to the portable restatement (kind "port")."""
+def cpu_info():
+    """(nproc, usable cores, CPU model) of this host"""
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = nproc
+    return nproc, usable, model
+
+
+def cpu_baseline(cfg, rtcp=False):
+    """Reference src/srtp (oracle/_ref/ref_bench: the reference sources
+    compiled with the box's libcrypto) on the host cores, bounded sample,
+    on 1 core and on all usable cores (<= 16: the box's CPU quota), one
+    struct srtp pair per thread; falls back to the portable restatement
+    (kind "port").  A run with errors fails loudly."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
-    threads = max(1, min(16, os.cpu_count() or 1))
+    nproc, usable, model = cpu_info()
+    threads = max(1, min(16, usable))
     length = cfg["length"] or 0          # 0 = mixed 200/1400 in ref_bench
-    if os.path.exists(ref):
-        per = 60000 if cfg["suite"] < 4 else 150000
-        nsess = min(cfg["nsess"], 4096)
-        try:
+    if os.path.exists(ref) and not rtcp:
+        runs = {}
+        for t in sorted({1, threads}):
+            # ~1-4 s of CPU per run: CTR/HMAC ~0.2 Mpairs/s/core, GCM ~1
+            per = (60000 if cfg["suite"] < 4 else 150000) // (1 if t > 1
+                                                               else 2)
             out = subprocess.run(
-                [ref, str(cfg["suite"]), str(length), str(per), str(threads),
-                 str(nsess)], capture_output=True, text=True, timeout=300,
-                check=True).stdout
+                [ref, str(cfg["suite"]), str(length), str(per), str(t),
+                 str(cfg["nsess"])], capture_output=True, text=True,
+                timeout=600, check=True).stdout
             r = json.loads(out.strip().splitlines()[-1])
-            return {"value": round(r["gib_s"], 4), "unit": "GiB/s",
-                    "mpkt_s": round(r["mpairs_s"], 4), "cores": threads,
-                    "kind": "reference",
-                    "sample": "%d protect+unprotect pairs (%s B) on %d "
-                              "threads, one struct srtp pair per thread, "
-                              "reference src/srtp + OpenSSL %s" % (
-                                  r["pairs"], length or "200/1400",
-                                  threads, "libcrypto"),
-                    "seconds": round(r["seconds"], 3)}
-        except Exception as e:  # pragma: no cover
-            print("cpu_baseline: reference run failed: %s" % e,
-                  file=sys.stderr)
+            if r["errors"]:
+                raise RuntimeError("ref_bench: %d errors (%s)" %
+                                   (r["errors"], out.strip()))
+            runs[t] = r
+        r, r1 = runs[threads], runs[1]
+        return {"value": round(r["gib_s"], 4), "unit": "GiB/s",
+                "mpkt_s": round(r["mpairs_s"], 4), "cores": threads,
+                "value_1core": round(r1["gib_s"], 4),
+                "mpkt_s_1core": round(r1["mpairs_s"], 4),
+                "kind": "reference", "nproc": nproc, "usable_cores": usable,
+                "cpu_model": model, "openssl": r.get("openssl"),
+                "sample": "%d protect+unprotect pairs of %s-B RTP packets "
+                          "on %d threads (%d pairs on 1), %d session(s) "
+                          "per thread, reference src/srtp" % (
+                              r["pairs"], length or "200/1400", threads,
+                              r1["pairs"], cfg["nsess"]),
+                "seconds": round(r["seconds"] + r1["seconds"], 3)}
     from tests import oracle_lib as O
     n = 3000
     t0 = time.perf_counter()
@@ -82,6 +112,7 @@ def cpu_baseline(cfg):
     L = cfg["length"] or 800
     return {"value": round(ok * L / dt / 2**30, 5), "unit": "GiB/s",
             "mpkt_s": round(ok / dt / 1e6, 5), "cores": 1, "kind": "port",
+            "nproc": nproc, "cpu_model": model,
             "sample": "%d pairs through the portable C restatement" % n}
 
 
@@ -120,6 +151,11 @@ def main():
                          "of the device-resident srtp_*_batch_dev")
     ap.add_argument("--tune", action="append", default=[],
                     help="name=value: srtp_gpu_tune knob (A/B runs)")
+    ap.add_argument("--forge", type=float, default=0,
+                    help="adversarial receive: forge this many packets per "
+                         "batch (a fraction if < 1) between protect and "
+                         "unprotect, spread evenly (EAUTH expected for "
+                         "exactly those)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary to attach (profiles/*.json)")
     args = ap.parse_args()
@@ -262,6 +298,15 @@ def main():
                         arena[a * slot:b * slot], non_blocking=True)
             stream.wait_stream(s_dn)
 
+    nforge = int(args.forge * n) if 0 < args.forge < 1 else int(args.forge)
+    forge_idx = forge_pk = None
+    if nforge:
+        assert use_dev and not args.e2e and not args.rtcp
+        forge_pk = np.linspace(0, n - 1, nforge).astype(np.int64)
+        # one payload byte of each forged packet (past any header)
+        forge_idx = torch.from_numpy(pos[forge_pk].astype(np.int64) +
+                                     12 + 20).to(dev)
+
     def step(tx, rx, k=0):
         if use_dev:
             err_ed, err_dd = errbuf[0, k], errbuf[1, k]
@@ -276,6 +321,8 @@ def main():
             e_d.copy_(end_d)
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
+                if forge_idx is not None and opname == OPS[1]:
+                    arena.index_put_((forge_idx,), arena[forge_idx] ^ 0x40)
                 rc = P.device_batch_dev(opname, ss, arena.data_ptr(),
                                         arena.numel(), p_d.data_ptr(),
                                         e_d.data_ptr(), cap_d.data_ptr(),
@@ -327,6 +374,12 @@ def main():
     P.prof_enable(False)
     elapsed = t1 - t0
     if use_dev:
+        if forge_pk is not None:
+            # exactly the forged packets fail, with EAUTH
+            fp = torch.from_numpy(forge_pk).to(dev)
+            got = errbuf[1, :args.steps, fp]
+            assert bool((got == P.EAUTH).all()), "forged packets not EAUTH"
+            errbuf[1, :args.steps, fp] = 0
         errors += int(torch.count_nonzero(errbuf[:, :args.steps]).item())
     counters = torch.tensor([n * args.steps, rtp_bytes * args.steps, errors],
                             dtype=torch.float64, device=dev)
@@ -350,6 +403,9 @@ def main():
         a2, p2 = arena.view(n, slot), plain.view(n, slot)
         # elementwise compare + count: no boolean-mask gather (its
         # index tensor is ~10 GB at 1M packets and slow to build)
+        if forge_pk is not None:
+            # a forged packet keeps its ciphertext (srtp.c:358-359)
+            win[torch.from_numpy(forge_pk).to(dev)] = False
         bad = int(torch.count_nonzero((a2 != p2) & win).item())
         verified = bad == 0 and tot_err == 0
         del win, a2, p2
@@ -427,11 +483,14 @@ def main():
         "hbm_frac_e2e": round(tot_pkts / world * (4 * L + 2 * tag) /
                               (T / 1) / 1e9 / HBM_PEAK_GBS, 4),
         "errors": int(tot_err),
+        "forged_per_batch": nforge,
+        "folds": {"device": P.counter("devfolds"),
+                  "host": P.counter("folds")},
         "verified_roundtrip": verified,
         "roofline": roof,
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(cfg)
+        line["cpu_baseline"] = cpu_baseline(cfg, args.rtcp)
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

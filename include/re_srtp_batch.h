@@ -119,11 +119,12 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 /**
  * Diagnostics / tuning knobs (defaults from the environment, read once:
  * RE_SRTP_NOPLAN, RE_SRTP_GENERAL, RE_SRTP_PERCLASS, RE_SRTP_NOLEAN,
- * RE_SRTP_TRACE,
+ * RE_SRTP_NODEVFOLD, RE_SRTP_TRACE,
  * RE_SRTP_TIMES, RE_SRTP_CHUNK, RE_SRTP_PAR_MIN).  name is one of
  * "noplan" (no device planners), "general" (general engine only),
  * "perclass" (one CTR launch per header class), "nolean" (the general
- * CTR kernels for device-planned batches), "trace", "times" (phase
+ * CTR kernels for device-planned batches), "nodevfold" (forged packets
+ * of a device-planned batch fold on the host), "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores
  * a size's built-in default.  Results never depend on them.  0 or EINVAL.
@@ -133,8 +134,9 @@ int srtp_gpu_tune(const char *name, long value);
 /**
  * Diagnostics counters since load: "misses" (packets whose MAC/tag
  * speculation failed -- forged or mis-planned), "folds" (batches re-run to
- * fold such verdicts exactly), "rejects" (device plans rejected: the host
- * planned instead).  0 for an unknown name.
+ * fold such verdicts exactly on the host), "devfolds" (batches whose
+ * verdicts folded on the device, no re-run), "rejects" (device plans
+ * rejected: the host planned instead).  0 for an unknown name.
  */
 uint64_t srtp_gpu_counter(const char *name);
 

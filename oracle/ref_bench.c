@@ -17,6 +17,7 @@
 #include <pthread.h>
 #include <time.h>
 #include <re.h>
+#include <openssl/crypto.h>
 
 struct job {
 	int suite;
@@ -52,6 +53,7 @@ static void *worker(void *arg)
 {
 	struct job *j = arg;
 	struct srtp **tx, **rx;
+	uint32_t *cnt;          /* per-session packet ordinal (seq) */
 	struct mbuf *mb = mbuf_alloc(2048);
 	uint64_t s = 0xC0FFEEull + j->seed;
 	uint8_t key[46];
@@ -60,6 +62,7 @@ static void *worker(void *arg)
 
 	tx = calloc((size_t)j->nsess, sizeof(*tx));
 	rx = calloc((size_t)j->nsess, sizeof(*rx));
+	cnt = calloc((size_t)j->nsess, sizeof(*cnt));
 	for (k = 0; k < j->nsess; k++) {
 		size_t b;
 		for (b = 0; b < sizeof(key); b++)
@@ -76,7 +79,8 @@ static void *worker(void *arg)
 		int sess = j->nsess > 1 ? (int)(xs(&s) % (uint64_t)j->nsess)
 				        : 0;
 		size_t len = j->mixed ? ((xs(&s) & 1) ? 1400 : 200) : j->len;
-		uint16_t seq = (uint16_t)(65000 + i);
+		/* every session sends seq 65000, 65001, ... (workload.py) */
+		uint16_t seq = (uint16_t)(65000 + cnt[sess]++);
 		uint8_t *p = mb->buf;
 		size_t b;
 
@@ -103,6 +107,7 @@ static void *worker(void *arg)
 	}
 	free(tx);
 	free(rx);
+	free(cnt);
 	mem_deref(mb);
 	return NULL;
 }
@@ -151,9 +156,11 @@ int main(int argc, char **argv)
 			sec = jobs[t].sec;
 
 	printf("{\"pairs\":%zu,\"seconds\":%.6f,\"mpairs_s\":%.6f,"
-	       "\"gib_s\":%.6f,\"threads\":%d,\"errors\":%d}\n",
+	       "\"gib_s\":%.6f,\"threads\":%d,\"errors\":%d,"
+	       "\"openssl\":\"%s\"}\n",
 	       npkts * (size_t)threads, sec,
 	       (double)(npkts * (size_t)threads) / sec / 1e6,
-	       (double)bytes / sec / (1024.0 * 1024 * 1024), threads, errs);
+	       (double)bytes / sec / (1024.0 * 1024 * 1024), threads, errs,
+	       OpenSSL_version(OPENSSL_VERSION));
 	return 0;
 }

@@ -374,10 +374,71 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 				(uint32_t)tp[2] << 16 | (uint32_t)tp[3] << 24;
 	st_be32(tp, f.roc);
 	const uint8_t vd = (diff == 0 ? SV_TAG_OK : 0) | SV_CIPHERED;
-	if (!(vd & SV_TAG_OK))
-		atomicAdd(a.c.nfail, 1u);
+	if (!(vd & SV_TAG_OK)) {
+		const uint32_t q = atomicAdd(a.c.nfail, 1u);
+		if (a.c.flist)
+			a.c.flist[q] = f.p;
+	}
 	if (a.verdict)
 		a.verdict[f.p] = vd;
+}
+
+/*
+ * The same restore from the list of forged packets (a.c.flist, filled by
+ * the fast kernel): one packet per workgroup, one 16-byte keystream block
+ * per thread, so a few forged packets cost a few short blocks instead of
+ * a full-grid pass where each forged packet runs its whole keystream on
+ * one lane.  Bytes [hl, A) only: the ROC at A stays (srtp.c:342-344).
+ */
+template <int NR>
+__global__ void __launch_bounds__(256)
+k_ctr_refix_list(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	const uint32_t nf = *(volatile const uint32_t *)a.c.nfail;
+	if (blockIdx.x >= nf)
+		return;
+	tt4_fill(smem, a.t0);
+	__syncthreads();
+	uint32_t rk[4 * (NR + 1)];
+	const struct sgpu_comp *cp = fast_keys<NR>(a, rk);
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	const uint32_t T = __builtin_amdgcn_readfirstlane(cp->tag_len);
+	for (uint32_t q = blockIdx.x; q < nf; q += gridDim.x) {
+		const uint32_t p = a.c.flist[q];
+		FastPkt f;
+		if (!fast_pkt(a.c, p - a.c.base, f))
+			continue;
+		uint8_t *pkt = a.arena + f.off;
+		const uint32_t A = f.L - T;
+		uint32_t iv[4];
+		fast_iv(cp, f, iv);
+		CtrKs<NR, true, true> C;
+		C.init(smem, lo, rk, iv);
+		for (uint32_t b = threadIdx.x; f.hl + 16u * b < A;
+		     b += blockDim.x) {
+			uint32_t ks[4];
+			C.block(smem, lo, rk, (int32_t)b, ks);
+			const uint32_t p0 = f.hl + 16u * b;
+#pragma unroll
+			for (int w = 0; w < 4; w++) {
+				const uint32_t bp = p0 + 4u * w;
+				if (bp >= A)
+					break;
+				if (A - bp >= 4u) {
+					uint32_t *wp = (uint32_t *)(pkt + bp);
+					*wp = *wp ^ ks[w];
+				}
+				else {
+					for (uint32_t k = 0; k < A - bp; k++)
+						pkt[bp + k] ^= (uint8_t)(ks[w] >>
+									 (8 * k));
+				}
+			}
+		}
+		if (threadIdx.x == 0)
+			a.verdict[p] &= (uint8_t)~SV_CIPHERED;
+	}
 }
 
 /*
@@ -390,13 +451,17 @@ __device__ __forceinline__ void ctr_refix_body(const KArgs &a, uint8_t *smem)
 {
 	if (*(volatile const uint32_t *)a.c.nfail == 0)
 		return;
+	FastPkt f;
+	const bool live = fast_pkt(a.c, blockIdx.x * blockDim.x + threadIdx.x,
+				   f);
+	const uint8_t vd = live ? a.verdict[f.p] : (uint8_t)SV_TAG_OK;
+	const bool need = !(vd & SV_TAG_OK) && (vd & SV_CIPHERED);
+	/* only blocks holding a forged packet fill the 128 KiB table */
+	if (!__syncthreads_or(need))
+		return;
 	tt4_fill(smem, a.t0);
 	__syncthreads();
-	FastPkt f;
-	if (!fast_pkt(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
-		return;
-	const uint8_t vd = a.verdict[f.p];
-	if ((vd & SV_TAG_OK) || !(vd & SV_CIPHERED))
+	if (!need)
 		return;
 	uint32_t rk[4 * (NR + 1)];
 	const struct sgpu_comp *cp = fast_keys<NR>(a, rk);

@@ -695,6 +695,7 @@ kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr10_any(bool uni, int prot);
 kfn_t sgpu_pick_ctr14_any(bool uni, int prot);
 kfn_t sgpu_pick_gcm(bool compact, bool uni, int nr, int prot);
+/* refix: 0 the kernel, 1 full-grid restore, 2 list restore (c.flist) */
 kfn_t sgpu_pick_ctr10_fast(int prot, int refix);
 kfn_t sgpu_pick_ctr14_fast(int prot, int refix);
 unsigned sgpu_ctr_fast_block(void);

@@ -286,8 +286,10 @@ k_mp_desc(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pex,
 			}
 		}
 		else {
+			/* above the session's pre-batch lix as well (see
+			 * k_plan_desc, srtp_kernels.hip) */
 			ok = ix > mp_ix(c, in, pex, k - 1, f, NULL, NULL, NULL,
-					NULL);
+					NULL) && ix > c.st[s].lix;
 		}
 		if (!ok)
 			atomicOr(&out->fail, (uint32_t)SPF_REPLAY);

@@ -32,6 +32,10 @@
 #include "../srtpgpu.h"
 #include "kern_common.h"
 
+#ifndef EAUTH
+#define EAUTH 217               /* include/re_types.h:215-217 */
+#endif
+
 
 __device__ uint32_t g_T0[256];          /* T0 table (source of LDS image) */
 __device__ uint8_t g_sbox[256];
@@ -486,7 +490,11 @@ k_plan_desc(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 			const int32_t pv = plan_v(proc, pw ? 0u : psb, pseq);
 			const uint64_t pix = pseq +
 					     (uint64_t)(int64_t)pv * 65536ull;
-			ok = ix > pix;
+			/* above the pre-batch window too: a packet 0 below
+			 * lix leaves the window's bits in play (replay.c:53-61)
+			 * and the tail-based final window (plan_replay) holds
+			 * only for indices above it */
+			ok = ix > pix && ix > in.lix;
 		}
 		if (!ok)
 			atomicOr(&out->fail, (uint32_t)SPF_REPLAY);
@@ -866,7 +874,17 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				    : sgpu_pick_ctr14_fast(prot, 0);
 		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
 			       (hipStream_t)stream, sgpu_ctr_fast_block());
-		if (!e && !prot)
+		if (!e && !prot && c->flist) {
+			/* one workgroup per listed forged packet (grid-
+			 * strided past 1024); all exit at once if none */
+			const uint32_t g = c->n < 1024u ? c->n : 1024u;
+			hipLaunchKernelGGL(nr == 10 ? sgpu_pick_ctr10_fast(0, 2)
+						    : sgpu_pick_ctr14_fast(0, 2),
+					   dim3(g), dim3(256), 0,
+					   (hipStream_t)stream, a);
+			e = herr(hipGetLastError(), "refix launch");
+		}
+		else if (!e && !prot)
 			e = launch(nr == 10 ? sgpu_pick_ctr10_fast(0, 1)
 					    : sgpu_pick_ctr14_fast(0, 1),
 				   a, c->n, -1, (hipStream_t)stream,
@@ -1094,6 +1112,278 @@ extern "C" int sgpu_plan_rtp(const struct sgpu_plan_in *in,
 			   *in, hdr, (const uint32_t *)scratch, desc, out);
 	hipLaunchKernelGGL(k_plan_final, dim3(1), dim3(64), 0, st, out);
 	return herr(hipGetLastError(), "plan launch");
+}
+
+/* ------------------------------------------------------------------ */
+/* Verdict fold of a device-planned unprotect (srtpgpu.h sgpu_fold_rtp) */
+
+/* packet k changes s_l for the packets after it: authentic (s_l = seq)
+ * or a rollover (s_l = 0 when forged) -- srtp.c:318-321, 426-427 */
+__device__ __forceinline__ bool fold_event(const struct sgpu_plan_in &in,
+					   const struct sgpu_hdr *hdr,
+					   const uint8_t *vd, uint32_t k)
+{
+	return (vd[k] & SV_TAG_OK) ||
+	       plan_wrap(hdr[k].seq, plan_sb(in, hdr, k));
+}
+
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_fold_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
+	     const uint8_t *vd, int32_t *blast, int32_t *bred)
+{
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	int32_t last = -1, fok = 0x7fffffff, lok = -1;
+	bool ok = false;
+	if (i < in.n) {
+		if (fold_event(in, hdr, vd, i))
+			last = (int32_t)i;
+		ok = (vd[i] & SV_TAG_OK) != 0;
+		if (ok)
+			fok = lok = (int32_t)i;
+	}
+	/* block reductions (k_fold_scan folds the blocks: no same-address
+	 * atomics, which serialise at L2) */
+	const uint32_t cnt = (uint32_t)__popcll(__ballot(ok));
+	for (int o = 32; o > 0; o >>= 1) {
+		last = max(last, __shfl_xor(last, o));
+		fok = min(fok, __shfl_xor(fok, o));
+		lok = max(lok, __shfl_xor(lok, o));
+	}
+	__shared__ int32_t wl[PLAN_BLOCK / 64][4];
+	if ((threadIdx.x & 63u) == 0) {
+		wl[threadIdx.x >> 6][0] = last;
+		wl[threadIdx.x >> 6][1] = fok;
+		wl[threadIdx.x >> 6][2] = lok;
+		wl[threadIdx.x >> 6][3] = (int32_t)cnt;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int32_t m = -1, f = 0x7fffffff, l = -1, c = 0;
+		for (int w = 0; w < PLAN_BLOCK / 64; w++) {
+			m = max(m, wl[w][0]);
+			f = min(f, wl[w][1]);
+			l = max(l, wl[w][2]);
+			c += wl[w][3];
+		}
+		blast[blockIdx.x] = m;
+		bred[3 * blockIdx.x] = f;
+		bred[3 * blockIdx.x + 1] = l;
+		bred[3 * blockIdx.x + 2] = c;
+	}
+}
+
+/* exclusive prefix maximum of the block maxima (one workgroup) */
+__global__ void __launch_bounds__(1024)
+k_fold_scan(const int32_t *blast, const int32_t *bred, int32_t *bprev,
+	    uint32_t nb, struct sgpu_fold_out *out)
+{
+	__shared__ int32_t part[1024];
+	__shared__ int32_t red[3];
+	const uint32_t per = (nb + 1023u) / 1024u;
+	const uint32_t a = threadIdx.x * per;
+	int32_t m = -1, f = 0x7fffffff, l = -1, c = 0;
+	if (threadIdx.x == 0) {
+		red[0] = 0x7fffffff;
+		red[1] = -1;
+		red[2] = 0;
+	}
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
+		m = max(m, blast[k]);
+		f = min(f, bred[3 * k]);
+		l = max(l, bred[3 * k + 1]);
+		c += bred[3 * k + 2];
+	}
+	__syncthreads();
+	/* authentic-packet count and first / last (LDS atomics) */
+	if (c) {
+		atomicMin(&red[0], f);
+		atomicMax(&red[1], l);
+		atomicAdd(&red[2], c);
+	}
+	part[threadIdx.x] = m;
+	__syncthreads();
+	for (uint32_t d = 1; d < 1024; d <<= 1) {
+		int32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : -1;
+		__syncthreads();
+		part[threadIdx.x] = max(part[threadIdx.x], v);
+		__syncthreads();
+	}
+	int32_t run = threadIdx.x ? part[threadIdx.x - 1] : -1;
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
+		bprev[k] = run;
+		run = max(run, blast[k]);
+	}
+	if (threadIdx.x == 0) {
+		out->nok = (uint32_t)red[2];
+		out->first_ok = red[2] ? (uint32_t)red[0] : 0xffffffffu;
+		out->last_ok = red[2] ? (uint32_t)red[1] : 0xffffffffu;
+	}
+}
+
+/* s_l packet i really sees: after the last event before it */
+__device__ __forceinline__ uint32_t fold_sl(const struct sgpu_plan_in &in,
+					    const struct sgpu_hdr *hdr,
+					    const uint8_t *vd, int32_t k)
+{
+	if (k < 0)
+		return in.fresh ? hdr[0].seq : in.s_l;
+	return (vd[k] & SV_TAG_OK) ? hdr[k].seq : 0u;
+}
+
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_fold_check(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
+	     const uint8_t *vd, const int32_t *bprev,
+	     struct sgpu_fold_out *out)
+{
+	__shared__ int32_t sc[PLAN_BLOCK];
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	const bool ev = i < in.n && fold_event(in, hdr, vd, i);
+	/* inclusive prefix max of event indices inside the block */
+	sc[threadIdx.x] = ev ? (int32_t)i : -1;
+	__syncthreads();
+	for (uint32_t d = 1; d < PLAN_BLOCK; d <<= 1) {
+		int32_t v = threadIdx.x >= d ? sc[threadIdx.x - d] : -1;
+		__syncthreads();
+		sc[threadIdx.x] = max(sc[threadIdx.x], v);
+		__syncthreads();
+	}
+	if (i >= in.n)
+		return;
+	const int32_t k = max(bprev[blockIdx.x],
+			      threadIdx.x ? sc[threadIdx.x - 1] : -1);
+	const uint32_t seq = hdr[i].seq;
+	const uint32_t sb = plan_sb(in, hdr, i);        /* speculated */
+	const uint32_t sl = fold_sl(in, hdr, vd, k);    /* true */
+	const bool wrap = plan_wrap(seq, sb);
+	bool bad = plan_wrap(seq, sl) != wrap ||
+		   (int)seq - (int)sl > 32768;          /* ETIMEDOUT */
+	if (!bad && !wrap) {
+		/* same index estimate (misc.c:22-41): roc is the same */
+		bad = plan_v(in.roc, sl, seq) != plan_v(in.roc, sb, seq);
+		/* an authentic packet sets s_l = seq only if seq > s_l
+		 * (srtp.c:426-427); fold_sl assumes it does */
+		if ((vd[i] & SV_TAG_OK) && seq < sl)
+			bad = true;
+	}
+	if (bad)
+		atomicOr(&out->fail, 1u);
+}
+
+/* forged packets' results; the final s_l and replay window (one wave) */
+__global__ void k_fold_results(const struct sgpu_plan_in in,
+			       const struct sgpu_hdr *hdr, const uint8_t *vd,
+			       const uint64_t *desc, const uint32_t *end0,
+			       const int32_t *blast, const int32_t *bprev,
+			       uint32_t nb, uint32_t *pos, uint32_t *end,
+			       int32_t *err, int gcm, struct sgpu_fold_out *out)
+{
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	if (out->fail)
+		return;
+	if (i < in.n && !(vd[i] & SV_TAG_OK)) {
+		err[i] = EAUTH;
+		pos[i] += hdr[i].hdr_len;
+		if (gcm)
+			end[i] = end0[i];
+	}
+	if (blockIdx.x != 0 || threadIdx.x != 0)
+		return;
+	/* s_l after the last packet: the last event's value */
+	out->s_l = fold_sl(in, hdr, vd, max(bprev[nb - 1], blast[nb - 1]));
+	/* replay (replay.c:32-62) over the authentic packets: every index is
+	 * new and increasing, so the window after the last authentic packet
+	 * j holds the authentic packets j-63 .. j (and, if j < 64, the window
+	 * before the batch) */
+	uint64_t lix = in.lix, bm = in.bitmap;
+	if (out->last_ok != 0xffffffffu) {
+		const uint32_t j = out->last_ok;
+		uint32_t q = 0;
+		if (j >= 64) {
+			q = j - 63;
+			lix = (desc[j - 64] & 0xffffull) |
+			      ((desc[j - 64] >> 16) & 0xffffffffull) << 16;
+			bm = 0;
+		}
+		for (; q <= j; q++) {
+			if (!(vd[q] & SV_TAG_OK))
+				continue;
+			const uint64_t ix = (desc[q] & 0xffffull) |
+					    ((desc[q] >> 16) & 0xffffffffull) << 16;
+			if (ix > lix) {
+				const uint64_t dl = ix - lix;
+				bm = dl < 64 ? (bm << dl) | 1ull : 1ull;
+				lix = ix;
+			}
+			else {
+				bm |= 1ull << (lix - ix);
+			}
+		}
+	}
+	out->lix = lix;
+	out->bitmap = bm;
+}
+
+/* the first authentic packet against the window before the batch (the
+ * plan checked packet 0; a forged packet 0 leaves it to the next) */
+__global__ void k_fold_first(const struct sgpu_plan_in in,
+			     const uint64_t *desc, struct sgpu_fold_out *out)
+{
+	const uint32_t f = out->first_ok;
+	if (f == 0xffffffffu || f == 0)
+		return;
+	const uint64_t ix = (desc[f] & 0xffffull) |
+			    ((desc[f] >> 16) & 0xffffffffull) << 16;
+	bool ok;
+	if (ix > in.lix) {
+		ok = true;
+	}
+	else {
+		const uint64_t dl = in.lix - ix;
+		ok = dl < 64 && !(in.bitmap & (1ull << dl));
+	}
+	if (!ok)
+		atomicOr(&out->fail, 2u);
+}
+
+__global__ void k_fold_init(struct sgpu_fold_out *out)
+{
+	out->fail = 0;
+	out->nok = 0;
+	out->first_ok = 0xffffffffu;
+	out->last_ok = 0xffffffffu;
+	out->s_l = 0;
+	out->pad = 0;
+	out->lix = 0;
+	out->bitmap = 0;
+}
+
+extern "C" int sgpu_fold_rtp(const struct sgpu_plan_in *in,
+			     const struct sgpu_hdr *hdr, const uint64_t *desc,
+			     const uint8_t *verdict, const uint32_t *end0,
+			     uint32_t *pos, uint32_t *end, int32_t *err,
+			     int gcm, uint32_t *scratch,
+			     struct sgpu_fold_out *out, void *stream)
+{
+	hipStream_t st = (hipStream_t)stream;
+	const uint32_t nb = (in->n + PLAN_BLOCK - 1) / PLAN_BLOCK;
+	int32_t *blast = (int32_t *)scratch, *bprev = blast + nb + 2;
+	int32_t *bred = bprev + nb + 2;
+	if (!in->n)
+		return EINVAL;
+	hipLaunchKernelGGL(k_fold_init, dim3(1), dim3(1), 0, st, out);
+	hipLaunchKernelGGL(k_fold_count, dim3(nb), dim3(PLAN_BLOCK), 0, st,
+			   *in, hdr, verdict, blast, bred);
+	hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, blast,
+			   (const int32_t *)bred, bprev, nb, out);
+	hipLaunchKernelGGL(k_fold_check, dim3(nb), dim3(PLAN_BLOCK), 0, st, *in,
+			   hdr, verdict, (const int32_t *)bprev, out);
+	hipLaunchKernelGGL(k_fold_first, dim3(1), dim3(1), 0, st, *in, desc,
+			   out);
+	hipLaunchKernelGGL(k_fold_results, dim3(nb), dim3(PLAN_BLOCK), 0, st,
+			   *in, hdr, verdict, desc, end0,
+			   (const int32_t *)blast, (const int32_t *)bprev, nb,
+			   pos, end, err, gcm, out);
+	return herr(hipGetLastError(), "fold launch");
 }
 
 extern "C" int sgpu_plan_rtcp(const struct sgpu_rplan_in *in,

@@ -91,6 +91,8 @@ static struct {
 	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
 	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
 				   device-planned single-key batches */
+	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
+				   device-planned batch fold on the host */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
 	int times;              /* RE_SRTP_TIMES: multi-session phases */
 	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
@@ -106,6 +108,7 @@ static void env_read(void)
 	g_env.general = getenv("RE_SRTP_GENERAL") != NULL;
 	g_env.perclass = getenv("RE_SRTP_PERCLASS") != NULL;
 	g_env.nolean = getenv("RE_SRTP_NOLEAN") != NULL;
+	g_env.nodevfold = getenv("RE_SRTP_NODEVFOLD") != NULL;
 	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
 	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
 	e = getenv("RE_SRTP_CHUNK");
@@ -125,6 +128,7 @@ static void env_init(void)
 static uint64_t g_cnt_misses;   /* MAC/tag speculation misses */
 static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
+static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 
 static void count(uint64_t *c, uint64_t v)
 {
@@ -141,6 +145,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_folds, __ATOMIC_RELAXED);
 	if (!strcmp(name, "rejects"))
 		return __atomic_load_n(&g_cnt_rejects, __ATOMIC_RELAXED);
+	if (!strcmp(name, "devfolds"))
+		return __atomic_load_n(&g_cnt_devfolds, __ATOMIC_RELAXED);
 	return 0;
 }
 
@@ -157,6 +163,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.perclass = value > 0;
 	else if (!strcmp(name, "nolean"))
 		g_env.nolean = value > 0;
+	else if (!strcmp(name, "nodevfold"))
+		g_env.nodevfold = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -2349,7 +2357,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL, 0};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0, NULL};
 		err = run_classes(b->arena, b->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -2565,7 +2573,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			struct sgpu_compact C = {
 				up_d, up_d + n, hd_d, desc_d, NULL,
 				(const uint32_t *)w->cm.d, NULL, 0,
-				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL, 0};
+				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL, 0, NULL};
 			err = run_classes(b->arena, b->arena_size, C, c0,
 					  po_d, prot, stream);
 		}
@@ -2761,7 +2769,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				(const uint32_t *)w->cm.d,
 				fl[q].has_idx ? idx_d : NULL, fl[q].base,
 				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1,
-				NULL, 0};
+				NULL, 0, NULL};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[q].shift, prot, stream);
@@ -2798,7 +2806,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				c0->mode == SGPU_MODE_GCM ?
 				&((struct sgpu_plan_out *)w->pl.d)->fail :
 				&((struct sgpu_plan_out *)w->pl.d)->
-					  skip[fl[k].shift], 0};
+					  skip[fl[k].shift], 0, NULL};
 			C.uniform = planned != 2 && nsess == 1;
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
@@ -2889,10 +2897,12 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	struct sgpu_plan_out *po, *po_d;
 	struct sgpu_hdr *hd_d;
 	uint64_t *desc_d;
-	uint32_t *scr, *es_d, *save_d, *nfail_d, nfail = 0, cm = c0->dev;
+	uint32_t *scr, *es_d, *save_d, *nfail_d, *flist_d, nfail = 0;
+	uint32_t cm = c0->dev;
 	uint8_t *vd_d;
 	void *stream;
 	struct ws *w = ws_get();
+	size_t foff;
 	int err;
 
 	if (!w)
@@ -2902,12 +2912,13 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!err)
 		err = pool_reserve(w, &w->dsc, n * 12);
 	if (!err)
-		err = pool_reserve(w, &w->vs, n * 5 + 64);
+		err = pool_reserve(w, &w->vs, n * 9 + 72);
 	if (!err)
 		err = pool_reserve(w, &w->cm, 4);
+	/* pl: plan out | plan scratch | fold out | fold scratch */
+	foff = (sizeof(struct sgpu_plan_out) + (n / 256 + 8) * 4 + 63) & ~63ul;
 	if (!err)
-		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_plan_out) +
-				   (n / 256 + 8) * 4);
+		err = pool_reserve(w, &w->pl, foff + 64 + (n / 256 + 4) * 20);
 	if (!err)
 		err = pool_reserve(w, &w->es, n * 4);
 	if (err)
@@ -2917,6 +2928,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	nfail_d = (uint32_t *)w->vs.d;
 	save_d = (uint32_t *)(w->vs.d + 64);
 	vd_d = w->vs.d + 64 + n * 4;
+	flist_d = (uint32_t *)(w->vs.d + ((64 + n * 5 + 3) & ~(size_t)3));
 	po = (struct sgpu_plan_out *)w->pl.h;
 	po_d = (struct sgpu_plan_out *)w->pl.d;
 	scr = (uint32_t *)(w->pl.d + sizeof(*po));
@@ -2940,7 +2952,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1, NULL, 0};
+			save_d, nfail_d, 0, 1, NULL, 0, flist_d};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -2963,19 +2975,49 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
-	if (nfail) {
+	if (nfail)
 		count(&g_cnt_misses, nfail);
-		count(&g_cnt_folds, 1);
-	}
 	plan_apply(s, po, prot, n, &old);
 	if (!nfail)
 		return 0;
-	/* a forged packet: undo on the device, fold on the host engine */
+	/* a forged packet: fold the verdicts on the device.  The kernels
+	 * already left each forged packet as srtp_decrypt does (HMAC: the
+	 * ciphertext restored, the ROC over the tag; GCM: decrypted in
+	 * place); the fold checks that the speculated rollovers and indices
+	 * hold under the true s_l and writes the EAUTH results, s_l and the
+	 * replay window (sgpu_fold_rtp). */
+	if (!prot && !g_env.nodevfold) {
+		struct sgpu_fold_out *fo = (struct sgpu_fold_out *)(w->pl.h + foff);
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(w->pl.d + foff);
+		err = sgpu_fold_rtp(&in, hd_d, desc_d, vd_d, es_d, d->pos, d->end,
+				    d->err, c0->mode == SGPU_MODE_GCM,
+				    (uint32_t *)(w->pl.d + foff + 64), fo_d,
+				    stream);
+		if (!err)
+			err = sgpu_memcpy_d2h(fo, fo_d, sizeof(*fo), stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		if (err) {
+			plan_unapply(s, ns0, &old);
+			return err;
+		}
+		if (!fo->fail) {
+			struct srtp_stream *st = &s->streams[0];
+			st->s_l = (uint16_t)fo->s_l;
+			st->replay_rtp.lix = fo->lix;
+			st->replay_rtp.bitmap = fo->bitmap;
+			count(&g_cnt_devfolds, 1);
+			return 0;
+		}
+	}
+	count(&g_cnt_folds, 1);
+	/* undo on the device, fold on the host engine */
 	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 1, NULL, 0};
+			save_d, nfail_d, 1, 1, NULL, 0, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -3072,7 +3114,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
 			save_d, nfail_d, 0, gcm ? 0 : 1,
-			gcm ? &po_d->fail : &po_d->skip[2], 1};
+			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
 	}
@@ -3117,7 +3159,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
 			save_d, nfail_d, 1, gcm ? 0 : 1,
-			gcm ? &po_d->fail : &po_d->skip[2], 1};
+			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, 0, stream);
 	}
@@ -3236,7 +3278,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL, 0};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -3279,7 +3321,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 0, NULL, 0};
+			save_d, nfail_d, 1, 0, NULL, 0, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}

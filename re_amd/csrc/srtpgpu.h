@@ -162,6 +162,11 @@ struct sgpu_compact {
 					   (a rejected device plan) or NULL */
 	int rtcp;                       /* SRTCP packets: descriptor = SRTCP
 					   index | E << 31 (sgpu_rdesc) */
+	uint32_t *flist;                /* lean unprotect: forged packets are
+					   listed here (n words, device; slot =
+					   the nfail count) and restored by a
+					   packet-per-workgroup pass; NULL: a
+					   full-grid pass finds them */
 };
 
 /* SRTCP descriptor: bits 0..30 SRTCP index, bit 31 E, bits 48..63 SD_* */
@@ -318,6 +323,38 @@ int   sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
 		     const uint32_t *pos, const uint32_t *end,
 		     const uint32_t *cap, uint64_t arena_size, uint64_t *desc,
 		     struct sgpu_plan_out *out, void *stream);
+
+/*
+ * Verdict fold of a device-planned single-stream unprotect (srtp_decrypt,
+ * srtp.c:288-432) on the device.  The plan assumed every tag authentic;
+ * with the verdicts known, packet i really sees s_l = seq of the last
+ * earlier packet that authenticated, or 0 after a later forged rollover
+ * (the ROC is bumped before the MAC check, s_l updated only on success:
+ * srtp.c:318-321, 426-427).  If every packet's rollover, ETIMEDOUT status
+ * and index are unchanged under that s_l, the speculation's verdicts are
+ * the reference's and the fold is exact: forged packets get EAUTH
+ * (pos = payload, end = tag start; GCM: end untouched, srtp.c:404-411),
+ * the stream's s_l and replay window follow the authentic packets only.
+ * Otherwise out->fail is set and the host folds instead.
+ */
+struct sgpu_fold_out {
+	uint32_t fail;          /* speculation inconsistent with the verdicts */
+	uint32_t nok;           /* authentic packets */
+	uint32_t first_ok;      /* index of the first authentic packet */
+	uint32_t last_ok;       /* ... and of the last (0xffffffff: none) */
+	uint32_t s_l;           /* s_l after the batch */
+	uint32_t pad;
+	uint64_t lix, bitmap;   /* replay_rtp after the batch */
+};
+
+/* scratch: >= 5 * (n / 256 + 2) words.  gcm: EAUTH leaves end as is.
+ * Runs after the crypto kernels (verdict[] complete); results written
+ * only if the fold holds (out->fail == 0). */
+int   sgpu_fold_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
+		    const uint64_t *desc, const uint8_t *verdict,
+		    const uint32_t *end0, uint32_t *pos, uint32_t *end,
+		    int32_t *err, int gcm, uint32_t *scratch,
+		    struct sgpu_fold_out *out, void *stream);
 
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */

@@ -34,8 +34,10 @@ XS_MUL = 0x2545F4914F6CDD1D
 CONFIG1_KEY = b"\x22" * 16 + b"\x44" * 14
 
 
-def slot_size(max_len):
-    return (max_len + 16 + 15) & ~15
+def slot_size(max_len, room=16):
+    """packet slot: the packet, `room` bytes for what protect appends (the
+    SRTP tag: <= 16 B; SRTCP: E||index + tag, <= 20 B), 16-B aligned"""
+    return (max_len + room + 15) & ~15
 
 
 def xs_state(seed, idx):
@@ -71,7 +73,7 @@ def make_keys(nsess, klen, seed=SEED_KEYS):
 
 
 def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
-               payload=True, first=0):
+               payload=True, first=0, room=16):
     """Returns (arena uint8[n*slot], pos, end, cap) numpy arrays.
 
     lengths: int or uint32 array (RTP packet length incl. 12-B header).
@@ -82,7 +84,7 @@ def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
     lengths = np.broadcast_to(np.asarray(lengths, dtype=np.uint32),
                               (npkts,)).copy()
     maxlen = int(lengths.max())
-    slot = slot_size(maxlen)
+    slot = slot_size(maxlen, room)
     arena = np.zeros((npkts, slot), dtype=np.uint8)
     gidx = np.arange(first, first + npkts, dtype=np.uint64)
     if payload and maxlen > 12:
@@ -131,7 +133,8 @@ def make_rtcp_arena(npkts, length, seed=SEED_PAYLOAD, first=0):
     header V=2, PT=200, length field = length/4 - 1, SSRC_BASE), payload
     from the same generators as make_arena.  Returns (arena, pos, end, cap).
     """
-    arena, pos, end, cap = make_arena(npkts, length, seed=seed, first=first)
+    arena, pos, end, cap = make_arena(npkts, length, seed=seed, first=first,
+                                      room=20)
     a = arena.reshape(npkts, -1)
     words = (int(length) // 4 - 1) & 0xffff
     a[:, 0] = 0x80

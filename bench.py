@@ -156,6 +156,9 @@ def main():
                          "batch (a fraction if < 1) between protect and "
                          "unprotect, spread evenly (EAUTH expected for "
                          "exactly those)")
+    ap.add_argument("--sq-json", default=None,
+                    help="SQ-counter summary to attach as int_frac/lds_frac "
+                         "(scripts/pmc_sq_summary.py --json)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary to attach (profiles/*.json)")
     args = ap.parse_args()
@@ -438,19 +441,33 @@ def main():
     # scaled if this run's launches carry a different packet count
     traffic = None
     tj = args.traffic_json or os.path.join(ROOT, "profiles",
-                                           "r01_pmc_traffic.json")
+                                           "r02_pmc_traffic.json")
+    sq = None
     if dom and os.path.exists(tj):
         ent = json.load(open(tj)).get("config%d" % cfg_id, {}).get(dom["dir"])
         if ent:
             traffic = round(ent["traffic_bytes_per_launch"] *
                             dom["pkts_per_launch"] / ent["grid"])
+    # integer roofline of the same kernel (VALU issue, LDS array), from the
+    # committed SQ-counter passes of this configuration
+    sj = args.sq_json or os.path.join(ROOT, "profiles", "r02_pmc_sq.json")
+    if dom and os.path.exists(sj):
+        sq = json.load(open(sj)).get("config%d" % cfg_id, {}).get(dom["dir"])
     roof = None
     if dom:
         roof = {"bound": "hbm", "achieved": round(dom["gbs"], 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_ctr_hmac" if (dom["slot"] & 8) == 0 else "k_gcm",
+                "traffic_src": os.path.basename(tj) if traffic else None,
+                "int_frac": round(sq["valu_frac"], 4) if sq and
+                "valu_frac" in sq else None,
+                "lds_frac": round(sq["lds_frac"], 4) if sq and
+                "lds_frac" in sq else None,
+                "int_src": os.path.basename(sj) if sq else None,
+                "kernel": (("k_ctr_fast_any" if nsess == 1 else "k_ctr_hmac")
+                           if (dom["slot"] & 8) == 0 else
+                           ("k_gcmu" if nsess == 1 else "k_gcm")),
                 "dir": dom["dir"],
                 "avg_launch_ms": round(dom["avg_ms"], 4),
                 "pkts_per_launch": dom["pkts_per_launch"],

@@ -299,6 +299,9 @@ k_gcm(const KArgs a)
 #ifndef GCMU_COAL
 #define GCMU_COAL 1
 #endif
+#ifndef GCMU_ALIGNED        /* packet-aligned 64-byte chunks (gcma_packet) */
+#define GCMU_ALIGNED 1
+#endif
 
 /*
  * M8[b] = b * H for all bytes b (OpenSSL Htable convention, BE words),
@@ -535,6 +538,261 @@ __device__ __forceinline__ uint8_t gcmu_packet(const uint8_t *smem, uint32_t lo,
 	return vd;
 }
 
+/* one whole cipher block b of the per-block path (c_off-aligned, 16 B) */
+template <int NR, bool PROT>
+__device__ __forceinline__ void gcm_block16(const uint8_t *smem, uint32_t lo,
+					   uint32_t hi16, const uint32_t *rk,
+					   const CtrKs<NR, true> &C, uint8_t *pkt,
+					   uint64_t pasz, uint32_t c_off,
+					   uint32_t b, uint32_t X[4])
+{
+	const uint32_t p = c_off + 16u * b;
+	const uint4 v = ld16(pkt, pasz, p);
+	uint32_t ks[4];
+	C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
+	const uint32_t o0 = v.x ^ ks[0], o1 = v.y ^ ks[1];
+	const uint32_t o2 = v.z ^ ks[2], o3 = v.w ^ ks[3];
+	*(uint4 *)(pkt + p) = make_uint4(o0, o1, o2, o3);
+	X[0] ^= bswap32(PROT ? o0 : v.x); X[1] ^= bswap32(PROT ? o1 : v.y);
+	X[2] ^= bswap32(PROT ? o2 : v.z); X[3] ^= bswap32(PROT ? o3 : v.w);
+	ghash8_mul(X, smem, hi16);
+}
+
+/*
+ * gcmu_packet with packet-aligned memory traffic.  The GHASH / counter
+ * blocks start at c_off = 16 t + 4 S, so a 64-byte chunk k of the packet
+ * (bytes [64k, 64k + 64), the arena's own line grid when slots are
+ * 64-byte multiples) holds, for S > 0: the last S words of block
+ * beta - 1 (beta = 4k - t), blocks beta .. beta + 2 whole, and the first
+ * 4 - S words of block beta + 3, whose remaining keystream and ciphertext
+ * words are carried in registers to chunk k + 1 (S = 0: four whole
+ * blocks).  Chunks whose words all lie in whole cipher blocks run that
+ * branch-free body with aligned (quad-coalesced) 64-byte loads and stores;
+ * the blocks before them and after them take the per-block path, and the
+ * straddling block at either end is finished word by word.  Same
+ * results as gcmu_packet (SP 800-38D GCTR + GHASH, aes.c:136-249).
+ */
+template <int NR, bool PROT, int S>
+__device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
+					       uint32_t hi16, const uint32_t *rk,
+					       const CtrKs<NR, true> &C,
+					       uint8_t *arena, uint64_t asz,
+					       const struct sgpu_job &j,
+					       uint32_t lane)
+{
+	uint8_t *pkt = arena + j.off;
+	const uint64_t pasz = asz - j.off;
+	const uint32_t A = j.a_len;
+	const uint32_t c_off = j.c_off, c_len = j.c_len;
+	const uint32_t c_end = c_off + c_len;
+	const uint32_t t = c_off >> 4;
+	const uint32_t nfull = c_len / 16u;
+	uint32_t X[4] = {0, 0, 0, 0};
+	for (uint32_t p = 0; p < A; p += 16) {
+		uint32_t w[4];
+		aad_block(pkt, pasz, p, A, false, 0u, w);
+		X[0] ^= w[0]; X[1] ^= w[1]; X[2] ^= w[2]; X[3] ^= w[3];
+		ghash8_mul(X, smem, hi16);
+	}
+
+	/* steady chunks [k0, k1): block beta - 1 >= 0 (S > 0), the last
+	 * block touched (beta + 3) whole */
+	const uint32_t k0 = S ? (t + 4u) / 4u : (t + 3u) / 4u;
+	uint32_t k1 = (nfull + t) / 4u;
+	if (k1 < k0)
+		k1 = k0;
+	const uint32_t nst = k1 - k0;
+	/* per-block prologue: blocks [0, P) */
+	const uint32_t P = nst ? 4u * k0 - t - (S ? 1u : 0u) : nfull;
+	for (uint32_t b = 0; b < P; b++)
+		gcm_block16<NR, PROT>(smem, lo, hi16, rk, C, pkt, pasz, c_off, b,
+				      X);
+	uint32_t cks[4] = {0, 0, 0, 0};  /* keystream words S.. of the block */
+	uint32_t chd[4] = {0, 0, 0, 0};  /* its ciphertext words 0..3-S */
+	if (S && nst) {
+		/* head of block P: the last 4 - S words of chunk k0 - 1 */
+		uint32_t ks[4];
+		C.block(smem, lo, rk, (int32_t)(P + 2u), ks);
+		const uint32_t hp = 64u * k0 - 4u * (4 - S);
+#pragma unroll
+		for (int q = 0; q < 4 - S; q++) {
+			uint32_t *wp = (uint32_t *)(pkt + hp + 4u * q);
+			const uint32_t v = *wp, o = v ^ ks[q];
+			*wp = o;
+			chd[q] = PROT ? o : v;
+		}
+#pragma unroll
+		for (int q = 0; q < S; q++)
+			cks[q] = ks[4 - S + q];
+	}
+
+	uint32_t M1 = 0;
+	uint64_t qb[4];
+	if (GCMU_COAL) {
+		quad_offsets((uint64_t)j.off + 64u * k0, lane, qb);
+		const uint64_t act = __ballot(1);
+		uint32_t a1 = min(nst, qdpp<DPP_QXOR1>(nst));
+		a1 = min(a1, qdpp<DPP_QXOR2>(a1));
+		if (((act >> (lane & ~3u)) & 0xfull) == 0xfull)
+			M1 = a1;
+	}
+	auto chunk = [&](uint32_t m, auto coal) {
+		constexpr bool CO = decltype(coal)::value;
+		const uint32_t k = k0 + m;
+		const uint32_t beta = 4u * k - t;
+		uint32_t d[16], o[16];
+		if constexpr (CO) {
+			quad_load(arena, qb, 64u * m, lane, d);
+		}
+		else {
+#pragma unroll
+			for (int g = 0; g < 4; g++) {
+				const uint4 v = *(const uint4 *)(pkt + 64u * k +
+								 16u * g);
+				d[4 * g] = v.x; d[4 * g + 1] = v.y;
+				d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+			}
+		}
+		uint32_t hb[4];         /* block beta - 1 (S > 0) */
+		if (S) {
+#pragma unroll
+			for (int q = 0; q < S; q++)
+				o[q] = d[q] ^ cks[q];
+#pragma unroll
+			for (int q = 0; q < 4 - S; q++)
+				hb[q] = chd[q];
+#pragma unroll
+			for (int q = 0; q < S; q++)
+				hb[4 - S + q] = PROT ? o[q] : d[q];
+		}
+#pragma unroll
+		for (int mm = 0; mm < (S ? 3 : 4); mm++) {
+			uint32_t ks[4];
+			C.block(smem, lo, rk, (int32_t)(beta + mm + 2u), ks);
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				o[S + 4 * mm + q] = d[S + 4 * mm + q] ^ ks[q];
+		}
+		if (S) {
+			uint32_t ks[4];
+			C.block(smem, lo, rk, (int32_t)(beta + 5u), ks);
+#pragma unroll
+			for (int q = 0; q < 4 - S; q++) {
+				o[12 + S + q] = d[12 + S + q] ^ ks[q];
+				chd[q] = PROT ? o[12 + S + q] : d[12 + S + q];
+			}
+#pragma unroll
+			for (int q = 0; q < S; q++)
+				cks[q] = ks[4 - S + q];
+		}
+		if constexpr (CO) {
+			quad_store(arena, qb, 64u * m, lane, o);
+		}
+		else {
+#pragma unroll
+			for (int g = 0; g < 4; g++)
+				*(uint4 *)(pkt + 64u * k + 16u * g) =
+					make_uint4(o[4 * g], o[4 * g + 1],
+						   o[4 * g + 2], o[4 * g + 3]);
+		}
+		if (S) {
+			X[0] ^= bswap32(hb[0]); X[1] ^= bswap32(hb[1]);
+			X[2] ^= bswap32(hb[2]); X[3] ^= bswap32(hb[3]);
+			ghash8_mul(X, smem, hi16);
+		}
+#pragma unroll
+		for (int mm = 0; mm < (S ? 3 : 4); mm++) {
+			const uint32_t *c = (PROT ? o : d) + S + 4 * mm;
+			X[0] ^= bswap32(c[0]); X[1] ^= bswap32(c[1]);
+			X[2] ^= bswap32(c[2]); X[3] ^= bswap32(c[3]);
+			ghash8_mul(X, smem, hi16);
+		}
+	};
+	uint32_t m = 0;
+	if (GCMU_COAL)
+		for (; m < M1; m++)
+			chunk(m, std::true_type());
+	for (; m < nst; m++)
+		chunk(m, std::false_type());
+
+	uint32_t b = P;
+	if (nst) {
+		b = 4u * k1 - t;
+		if (S) {
+			/* tail of block b - 1: the first S words of chunk k1 */
+			uint32_t hb[4];
+#pragma unroll
+			for (int q = 0; q < 4 - S; q++)
+				hb[q] = chd[q];
+#pragma unroll
+			for (int q = 0; q < S; q++) {
+				uint32_t *wp = (uint32_t *)(pkt + 64u * k1 + 4u * q);
+				const uint32_t v = *wp, o = v ^ cks[q];
+				*wp = o;
+				hb[4 - S + q] = PROT ? o : v;
+			}
+			X[0] ^= bswap32(hb[0]); X[1] ^= bswap32(hb[1]);
+			X[2] ^= bswap32(hb[2]); X[3] ^= bswap32(hb[3]);
+			ghash8_mul(X, smem, hi16);
+		}
+	}
+	for (; b < nfull; b++)
+		gcm_block16<NR, PROT>(smem, lo, hi16, rk, C, pkt, pasz, c_off, b,
+				      X);
+	if (c_len > 16u * nfull) {
+		const uint32_t bb = nfull, p = c_off + 16u * bb;
+		const uint4 v = ld16(pkt, pasz, p);
+		const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+		uint32_t ks[4], ct[4];
+		C.block(smem, lo, rk, (int32_t)(bb + 2u), ks);
+		const uint32_t rem = c_end - p;
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t bp = 4u * q;
+			const uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
+			const uint32_t mk = (uint32_t)((1ull << (8 * nbytes)) - 1ull);
+			const uint32_t o = (d[q] ^ ks[q]) & mk;
+			ct[q] = PROT ? o : (d[q] & mk);
+			if (nbytes == 4)
+				*(uint32_t *)(pkt + p + bp) = o;
+			else if (nbytes)
+				st_partial(pkt + p + bp, o, nbytes);
+		}
+		X[0] ^= bswap32(ct[0]); X[1] ^= bswap32(ct[1]);
+		X[2] ^= bswap32(ct[2]); X[3] ^= bswap32(ct[3]);
+		ghash8_mul(X, smem, hi16);
+	}
+
+	/* length block: bitlen(AAD) || bitlen(C) */
+	{
+		const uint64_t al = (uint64_t)A * 8u, cl = (uint64_t)c_len * 8u;
+		X[0] ^= (uint32_t)(al >> 32); X[1] ^= (uint32_t)al;
+		X[2] ^= (uint32_t)(cl >> 32); X[3] ^= (uint32_t)cl;
+		ghash8_mul(X, smem, hi16);
+	}
+	/* tag = GHASH ^ E(K, J0) */
+	uint32_t e0[4];
+	C.block(smem, lo, rk, 1, e0);
+	const uint32_t tg[4] = {X[0] ^ bswap32(e0[0]), X[1] ^ bswap32(e0[1]),
+				X[2] ^ bswap32(e0[2]), X[3] ^ bswap32(e0[3])};
+	uint8_t *tp = pkt + j.tag_off;
+	uint8_t vd = SV_CIPHERED;
+	if (PROT) {
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+			st_be32(tp + 4 * q, tg[q]);
+	}
+	else {
+		uint32_t diff = 0;
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			diff |= tp[q] ^ (uint8_t)(tg[q >> 2] >> (24 - 8 * (q & 3)));
+		if (diff == 0)
+			vd |= SV_TAG_OK;
+	}
+	return vd;
+}
+
 template <int NR, bool PROT>
 __global__ void
 __attribute__((amdgpu_flat_work_group_size(1, GCMU_BLOCK)))
@@ -632,8 +890,31 @@ k_gcmu(const KArgs a)
 		return;
 	}
 	const uint32_t hi16 = ((lane & 15u) << 4) | 0x10000u;
-	const uint8_t vd = gcmu_packet<NR, PROT>(smem, lo, hi16, rk, C, a.arena,
-						 a.asz, j, lane);
+	uint8_t vd;
+	if (GCMU_ALIGNED) {
+		switch ((j.c_off >> 2) & 3u) {
+		case 0:
+			vd = gcma_packet<NR, PROT, 0>(smem, lo, hi16, rk, C,
+						      a.arena, a.asz, j, lane);
+			break;
+		case 1:
+			vd = gcma_packet<NR, PROT, 1>(smem, lo, hi16, rk, C,
+						      a.arena, a.asz, j, lane);
+			break;
+		case 2:
+			vd = gcma_packet<NR, PROT, 2>(smem, lo, hi16, rk, C,
+						      a.arena, a.asz, j, lane);
+			break;
+		default:
+			vd = gcma_packet<NR, PROT, 3>(smem, lo, hi16, rk, C,
+						      a.arena, a.asz, j, lane);
+			break;
+		}
+	}
+	else {
+		vd = gcmu_packet<NR, PROT>(smem, lo, hi16, rk, C, a.arena,
+					   a.asz, j, lane);
+	}
 	if (!PROT && !(vd & SV_TAG_OK))
 		atomicAdd(a.c.nfail, 1u);
 	if (verdict)

@@ -11,6 +11,10 @@ import csv
 import json
 import sys
 
+# the crypto kernels: k_ctr_fast_any (lean, device-planned single key),
+# k_ctr_hmac / k_ctr_hmac_any (general compact), k_gcmu / k_gcm
+CRYPTO = ("k_ctr_fast_any", "k_ctr_hmac", "k_gcm")
+
 
 def per_kernel(path, counter):
     rows = list(csv.DictReader(open(path + "/run_counter_collection.csv")))
@@ -19,7 +23,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        if "k_ctr_hmac" not in name and "k_gcm" not in name:
+        if not any(k in name for k in CRYPTO):
             continue
         v = float(r["Counter_Value"]) * 1024.0
         if v <= 0:

@@ -474,6 +474,27 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 			      struct sgpu_plan_out *out, uint32_t *order,
 			      void *stream)
 {
+	int e = sgpu_mplan_rtp_phase(1, in, hdr, pos, end, cap, arena_size,
+				     sess, st_in, st_out, desc, scratch,
+				     scratch_bytes, out, order, stream);
+	if (!e)
+		e = sgpu_mplan_rtp_phase(2, in, hdr, pos, end, cap, arena_size,
+					 sess, st_in, st_out, desc, scratch,
+					 scratch_bytes, out, order, stream);
+	return e;
+}
+
+extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
+				    const struct sgpu_hdr *hdr,
+				    const uint32_t *pos, const uint32_t *end,
+				    const uint32_t *cap, uint64_t arena_size,
+				    const uint32_t *sess,
+				    const struct sgpu_sstate *st_in,
+				    struct sgpu_sstate *st_out, uint64_t *desc,
+				    void *scratch, size_t scratch_bytes,
+				    struct sgpu_plan_out *out, uint32_t *order,
+				    void *stream)
+{
 	hipStream_t st = (hipStream_t)stream;
 	const uint32_t n = in->n, nb = (n + MP_BLOCK - 1) / MP_BLOCK;
 	uint8_t *p = (uint8_t *)scratch;
@@ -490,6 +511,8 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 	if (!n || !in->nsess ||
 	    (size_t)(p - (uint8_t *)scratch) + tb > scratch_bytes)
 		return EINVAL;
+	if (phase == 2)
+		goto plan;
 	if (hipMemsetAsync(out, 0, sizeof(*out), st) != hipSuccess ||
 	    hipMemsetAsync(segl, 0xff, (size_t)in->nsess * 4, st) !=
 	    hipSuccess)
@@ -517,6 +540,9 @@ extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 						       st) != hipSuccess)
 			return EIO;
 	}
+	if (phase == 1)
+		return hipGetLastError() == hipSuccess ? 0 : EIO;
+ plan:;
 	mp_ctx c = {kout, vout, hdr, st_in, n, sseq, sssrc};
 	hipLaunchKernelGGL(k_mp_count, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
 			   pos, end, cap, arena_size, bcnt, out);

@@ -598,6 +598,8 @@ extern "C" int sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
 static char g_err[256];
 static int g_inited;
 static struct sgpu_session *g_table;
+static struct sgpu_sstate *g_sst;       /* per slot: RTP stream 0 state of
+					   resident multi-session batches */
 static uint32_t g_table_cap;
 static struct sgpu_keyreq *g_req_dev;
 static uint32_t *g_slot_dev;
@@ -676,18 +678,137 @@ extern "C" int sgpu_table_reserve(uint32_t nsessions)
 	while (cap < nsessions)
 		cap *= 2;
 	struct sgpu_session *nt = NULL;
+	struct sgpu_sstate *ns = NULL;
 	int e = herr(hipMalloc(&nt, (size_t)cap * sizeof(*nt)), "table alloc");
-	if (e)
+	if (!e)
+		e = herr(hipMalloc(&ns, (size_t)cap * sizeof(*ns)),
+			 "state table alloc");
+	if (e) {
+		(void)hipFree(nt);
 		return e;
+	}
 	if (g_table) {
 		e = herr(hipMemcpy(nt, g_table,
 				   (size_t)g_table_cap * sizeof(*nt),
 				   hipMemcpyDeviceToDevice), "table grow");
+		if (!e)
+			e = herr(hipMemcpy(ns, g_sst,
+					   (size_t)g_table_cap * sizeof(*ns),
+					   hipMemcpyDeviceToDevice),
+				 "state table grow");
 		(void)hipDeviceSynchronize();
 		(void)hipFree(g_table);
+		(void)hipFree(g_sst);
 	}
 	g_table = nt;
+	g_sst = ns;
 	g_table_cap = cap;
+	return e;
+}
+
+/* ---- resident RTP stream states (srtpgpu.h sgpu_sst_*) ---------------- */
+
+__global__ void k_sst_zero(const uint32_t *slot, uint32_t n,
+			   struct sgpu_sstate *sst)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n)
+		sst[slot[i]] = sgpu_sstate{};
+}
+
+__global__ void k_sst_load(const uint32_t *cm, const uint8_t *need,
+			   const struct sgpu_sstate *up, uint32_t nsess,
+			   struct sgpu_sstate *sst, struct sgpu_sstate *st_in)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= nsess)
+		return;
+	const uint32_t slot = cm[k] >> 1;
+	struct sgpu_sstate S;
+	if (need && need[k]) {
+		S = up[k];
+		sst[slot] = S;
+	}
+	else {
+		S = sst[slot];
+	}
+	st_in[k] = S;
+}
+
+__global__ void k_sst_commit(const uint32_t *cm,
+			     const struct sgpu_sstate *st_out, uint32_t nsess,
+			     const uint32_t *fail, const uint32_t *nfail,
+			     struct sgpu_sstate *sst)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= nsess || *fail || *nfail)
+		return;
+	struct sgpu_sstate o = st_out[k];
+	if (!(o.flags & SST_TOUCHED))
+		return;
+	o.flags &= ~(uint32_t)SST_TOUCHED;
+	sst[cm[k] >> 1] = o;
+}
+
+__global__ void k_sst_read(const uint32_t *slot, uint32_t n,
+			   const struct sgpu_sstate *sst,
+			   struct sgpu_sstate *out)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n)
+		out[i] = sst[slot[i]];
+}
+
+extern "C" int sgpu_sst_load(const uint32_t *cm, const uint8_t *need,
+			     const struct sgpu_sstate *up, uint32_t nsess,
+			     struct sgpu_sstate *st_in, void *stream)
+{
+	if (!nsess)
+		return 0;
+	hipLaunchKernelGGL(k_sst_load, dim3((nsess + 255) / 256), dim3(256), 0,
+			   (hipStream_t)stream, cm, need, up, nsess, g_sst,
+			   st_in);
+	return herr(hipGetLastError(), "k_sst_load launch");
+}
+
+extern "C" int sgpu_sst_commit(const uint32_t *cm,
+			       const struct sgpu_sstate *st_out, uint32_t nsess,
+			       const uint32_t *fail, const uint32_t *nfail,
+			       void *stream)
+{
+	if (!nsess)
+		return 0;
+	hipLaunchKernelGGL(k_sst_commit, dim3((nsess + 255) / 256), dim3(256),
+			   0, (hipStream_t)stream, cm, st_out, nsess, fail, nfail,
+			   g_sst);
+	return herr(hipGetLastError(), "k_sst_commit launch");
+}
+
+extern "C" int sgpu_sst_read(const uint32_t *slot, uint32_t n,
+			     struct sgpu_sstate *out)
+{
+	uint32_t *sd = NULL;
+	struct sgpu_sstate *od = NULL;
+	int e;
+	if (!n)
+		return 0;
+	e = herr(hipMalloc(&sd, (size_t)n * 4), "sst read alloc");
+	if (!e)
+		e = herr(hipMalloc(&od, (size_t)n * sizeof(*od)),
+			 "sst read alloc");
+	if (!e)
+		e = herr(hipMemcpy(sd, slot, (size_t)n * 4,
+				   hipMemcpyHostToDevice), "sst read h2d");
+	if (!e) {
+		hipLaunchKernelGGL(k_sst_read, dim3((n + 255) / 256), dim3(256),
+				   0, 0, sd, n, g_sst, od);
+		e = herr(hipGetLastError(), "k_sst_read launch");
+	}
+	if (!e)
+		e = herr(hipMemcpy(out, od, (size_t)n * sizeof(*od),
+				   hipMemcpyDeviceToHost), "sst read d2h");
+	(void)hipFree(sd);
+	(void)hipFree(od);
 	return e;
 }
 
@@ -724,6 +845,12 @@ extern "C" int sgpu_setup_sessions(const struct sgpu_keyreq *req,
 	hipLaunchKernelGGL(k_setup, dim3((nthreads + thr - 1) / thr), dim3(thr),
 			   0, 0, g_req_dev, g_slot_dev, n, g_table);
 	e = herr(hipGetLastError(), "k_setup launch");
+	if (!e) {
+		/* a new session has no stream yet (resident state table) */
+		hipLaunchKernelGGL(k_sst_zero, dim3((n + 255) / 256), dim3(256),
+				   0, 0, g_slot_dev, n, g_sst);
+		e = herr(hipGetLastError(), "k_sst_zero launch");
+	}
 	if (!e)
 		e = herr(hipDeviceSynchronize(), "k_setup");
 	return e;

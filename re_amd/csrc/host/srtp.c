@@ -80,7 +80,17 @@ struct srtp {
 	uint32_t mp_epoch;      /* multi-session plan: call that gathered it
 				   (detects sessv entries aliasing one
 				   context) */
+	int dres;               /* where stream 0's RTP state lives: DRES_* */
 };
+
+/*
+ * Resident state (sgpu_sst_*): multi-session device batches keep each
+ * session's RTP stream-0 state in HBM across calls.  DRES_BOTH: host and
+ * device copies agree (a new session, no stream); DRES_DEV: the device
+ * copy is newer (after a multi-session device batch); DRES_HOST: the host
+ * copy is newer.  Host-side paths call sess_host() first.
+ */
+enum { DRES_HOST = 0, DRES_BOTH = 1, DRES_DEV = 2, DRES_LISTED = 3 };
 
 /* ------------------------------------------------------------------ */
 /* tuning / diagnostics switches, read once (not per batch)             */
@@ -370,6 +380,7 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 			goto out;
 		}
 		s->slot = slots[i];
+		s->dres = DRES_BOTH;    /* sgpu_setup_sessions zeroed it */
 		s->suite = (int)suite;
 		s->dev = sgpu_get_device();
 		comp_set(&s->rtp, &p, 1, 2 * slots[i]);
@@ -1356,6 +1367,76 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 
 /* ---- host-resident front-end (mbufs) -------------------------------- */
 
+/*
+ * Bring the host copy of every session's state up to date before a
+ * host-side path reads or changes it: sessions whose device copy is newer
+ * (DRES_DEV) are read back in one transfer; all end up DRES_HOST (the
+ * path may change them).  Needs the table read lock.
+ */
+static int sess_host(struct srtp **sessv, size_t nsess)
+{
+	struct srtp **lst = NULL;
+	uint32_t *slots = NULL;
+	struct sgpu_sstate *st = NULL;
+	size_t k, m = 0;
+	int err = 0;
+
+	for (k = 0; k < nsess; k++)
+		if (sessv[k] && sessv[k]->dres == DRES_DEV)
+			m++;
+	if (m) {
+		lst = malloc(m * sizeof(*lst));
+		slots = malloc(m * sizeof(*slots));
+		st = malloc(m * sizeof(*st));
+		if (!lst || !slots || !st) {
+			err = ENOMEM;
+			goto out;
+		}
+		m = 0;
+		for (k = 0; k < nsess; k++) {
+			struct srtp *s = sessv[k];
+			if (!s || s->dres != DRES_DEV)
+				continue;
+			s->dres = DRES_LISTED;          /* aliases: once */
+			lst[m] = s;
+			slots[m++] = s->slot;
+		}
+		err = sgpu_sst_read(slots, (uint32_t)m, st);
+		for (k = 0; k < m; k++) {
+			struct srtp *s = lst[k];
+			struct srtp_stream *x;
+			if (err) {
+				s->dres = DRES_DEV;
+				continue;
+			}
+			if (st[k].flags & SST_EXISTS) {
+				if (!s->nstreams) {
+					memset(&s->streams[0], 0,
+					       sizeof(s->streams[0]));
+					s->nstreams = 1;
+				}
+				x = &s->streams[0];
+				x->ssrc = st[k].ssrc;
+				x->roc = st[k].roc;
+				x->s_l = (uint16_t)st[k].s_l;
+				x->s_l_set = (st[k].flags & SST_SL_SET) ? 1 : 0;
+				x->replay_rtp.lix = st[k].lix;
+				x->replay_rtp.bitmap = st[k].bitmap;
+			}
+			s->dres = DRES_HOST;
+		}
+	}
+ out:
+	if (!err)
+		for (k = 0; k < nsess; k++)
+			if (sessv[k])
+				sessv[k]->dres = DRES_HOST;
+	free(lst);
+	free(slots);
+	free(st);
+	return err;
+}
+
 static int run_mbufs_(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 		      size_t n)
 {
@@ -1517,7 +1598,9 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 {
 	int err;
 	table_rdlock();
-	err = run_mbufs_(op, srtp, mbv, errv, n);
+	err = srtp ? sess_host(&srtp, 1) : 0;
+	if (!err)
+		err = run_mbufs_(op, srtp, mbv, errv, n);
 	table_unlock();
 	return err;
 }
@@ -2128,6 +2211,8 @@ struct mpg {
 	int suite, prot;
 	uint32_t epoch;         /* this call (alias detection) */
 	atomic_int bad;
+	uint8_t *need;          /* resident: st[k] is to be uploaded */
+	atomic_uint nup;        /* ... how many */
 };
 
 static void mplan_gather_part(void *arg, size_t a, size_t b)
@@ -2153,6 +2238,19 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 		}
 		if (g->cm)
 			g->cm[k] = 2u * s->slot;        /* comp[0] = RTP */
+		if (g->need) {
+			/* resident states: upload only what the host changed
+			 * since the device last held it */
+			if (s->dres == DRES_HOST) {
+				g->need[k] = 1;
+				atomic_fetch_add(&g->nup, 1);
+			}
+			else {
+				g->need[k] = 0;
+				((struct srtp *)s)->dres = DRES_DEV;
+				continue;
+			}
+		}
 		memset(st, 0, sizeof(*st));
 		if (s->nstreams) {
 			const struct srtp_stream *x = &s->streams[0];
@@ -2170,12 +2268,44 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 static int mplan_gather(struct srtp **sessv, size_t nsess,
 			struct sgpu_sstate *st, uint32_t *cm)
 {
-	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0};
+	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, NULL,
+			0};
 	do {
 		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
 	} while (!g.epoch);
 	par_for(nsess, mplan_par(), mplan_gather_part, &g);
 	return atomic_load(&g.bad) ? -1 : 0;
+}
+
+/*
+ * The same pass for resident states: sessions whose device copy is
+ * current are only mapped (and marked DRES_DEV); host-newer ones are
+ * copied to st[k] with need[k] = 1 for sgpu_sst_load.  *nup = how many.
+ * -1: not plannable (the caller uploads nothing: need[] is ignored and
+ * the marks are undone).
+ */
+static int mplan_gather_res(struct srtp **sessv, size_t nsess,
+			    struct sgpu_sstate *st, uint32_t *cm,
+			    uint8_t *need, uint32_t *nup)
+{
+	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, need,
+			0};
+	size_t k;
+	do {
+		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
+	} while (!g.epoch);
+	par_for(nsess, mplan_par(), mplan_gather_part, &g);
+	*nup = atomic_load(&g.nup);
+	if (atomic_load(&g.bad)) {
+		/* the device copies of sessions marked DEV here were current
+		 * already (DRES_BOTH or DRES_DEV): DEV is still true */
+		return -1;
+	}
+	if (*nup)
+		for (k = 0; k < nsess; k++)
+			if (need[k])
+				sessv[k]->dres = DRES_DEV;
+	return 0;
 }
 
 static void mplan_apply_part(void *arg, size_t a, size_t b)
@@ -2211,7 +2341,7 @@ static void mplan_apply_part(void *arg, size_t a, size_t b)
 static void mplan_apply(struct srtp **sessv, size_t nsess,
 			const struct sgpu_sstate *o, int prot)
 {
-	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0};
+	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0, NULL, 0};
 	par_for(nsess, mplan_par(), mplan_apply_part, &g);
 }
 
@@ -3190,12 +3320,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
 	const int gcm = c0->mode == SGPU_MODE_GCM;
 	struct sgpu_plan_out *po, *po_d;
-	struct sgpu_sstate *sin_h, *sin_d, *sout_h, *sout_d;
+	struct sgpu_sstate *up_h, *up_d, *sin_d, *sout_d;
 	struct sgpu_mplan_in in;
 	struct sgpu_hdr *hd_d;
 	uint64_t *desc_d;
 	uint32_t *es_d, *save_d, *nfail_d, *cm_h, *order_d, nfail = 0, bits = 1;
-	uint8_t *vd_d;
+	uint32_t nup = 0;
+	uint8_t *vd_d, *need_h, *need_d;
 	size_t scr;
 	void *stream = d->stream;
 	struct ws *w = ws_get();
@@ -3222,7 +3353,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		err = pool_reserve(w, &w->es, n * 4);
 	if (!err)
 		err = pool_reserve(w, &w->ms,
-				   nsess * 2 * sizeof(struct sgpu_sstate));
+				   nsess * (3 * sizeof(struct sgpu_sstate) + 1));
 	if (!err)   /* scratch, then the launch order (n words) */
 		err = pool_reserve(w, &w->mscr, scr + n * 4);
 	if (err)
@@ -3236,10 +3367,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	po_d = (struct sgpu_plan_out *)w->pl.d;
 	es_d = (uint32_t *)w->es.d;
 	cm_h = (uint32_t *)w->cm.h;
-	sin_h = (struct sgpu_sstate *)w->ms.h;
+	/* ms: st_in | st_out | uploads | need (device; host: the uploads) */
 	sin_d = (struct sgpu_sstate *)w->ms.d;
-	sout_h = sin_h + nsess;
 	sout_d = sin_d + nsess;
+	up_d = sout_d + nsess;
+	need_d = (uint8_t *)(up_d + nsess);
+	up_h = (struct sgpu_sstate *)w->ms.h + 2 * nsess;
+	need_h = (uint8_t *)(up_h + nsess);
 	order_d = (uint32_t *)(w->mscr.d + scr);
 	/* parse + end copy (the kernels keep reading the input windows) +
 	 * zeroed miss counter, one launch; it runs while the host gathers */
@@ -3251,12 +3385,6 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		if (err)
 			return err;
 	}
-	/* one pass over the sessions: suite check, stream state, slot map */
-	t[0] = times ? now_ms() : 0;
-	if (mplan_gather(sessv, nsess, sin_h, cm_h))
-		return -1;
-	t[1] = times ? now_ms() : 0;
-
 	memset(&in, 0, sizeof(in));
 	in.n = (uint32_t)n;
 	in.nsess = (uint32_t)nsess;
@@ -3265,15 +3393,37 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	in.need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
 	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	in.key_bits = bits;
+	/* the sort by session needs no session state: it runs while the
+	 * host walks the sessions */
+	err = sgpu_mplan_rtp_phase(1, &in, hd_d, d->pos, es_d, d->cap,
+				   d->arena_size, d->sess, sin_d, sout_d,
+				   desc_d, w->mscr.d, scr, po_d, order_d,
+				   stream);
+	if (err)
+		return err;
+	/* one pass over the sessions: suite check, slot map, and the states
+	 * the device does not hold yet (none once sessions are resident) */
+	t[0] = times ? now_ms() : 0;
+	if (mplan_gather_res(sessv, nsess, up_h, cm_h, need_h, &nup)) {
+		/* the queued sort only wrote scratch */
+		err = sgpu_stream_sync(stream);
+		return err ? err : -1;
+	}
+	t[1] = times ? now_ms() : 0;
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
+	if (!err && nup)
+		err = sgpu_memcpy_h2d(up_d, up_h,
+				      nsess * (sizeof(struct sgpu_sstate) + 1),
+				      stream);
 	if (!err)
-		err = sgpu_memcpy_h2d(sin_d, sin_h,
-				      nsess * sizeof(struct sgpu_sstate), stream);
+		err = sgpu_sst_load((const uint32_t *)w->cm.d,
+				    nup ? need_d : NULL, up_d, (uint32_t)nsess,
+				    sin_d, stream);
 	if (!err)
-		err = sgpu_mplan_rtp(&in, hd_d, d->pos, es_d, d->cap,
-				     d->arena_size, d->sess, sin_d, sout_d,
-				     desc_d, w->mscr.d, scr, po_d, order_d,
-				     stream);
+		err = sgpu_mplan_rtp_phase(2, &in, hd_d, d->pos, es_d, d->cap,
+					   d->arena_size, d->sess, sin_d,
+					   sout_d, desc_d, w->mscr.d, scr, po_d,
+					   order_d, stream);
 	if (!err) {
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
@@ -3286,11 +3436,14 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
 					(uint32_t)n,
 					prot ? (int32_t)T : -(int32_t)T, stream);
+	/* the new states replace the resident ones if the plan held and every
+	 * tag verified (a forged packet: the host folds from the old ones) */
+	if (!err)
+		err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
+				      (uint32_t)nsess, &po_d->fail, nfail_d,
+				      stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
-	if (!err)
-		err = sgpu_memcpy_d2h(sout_h, sout_d,
-				      nsess * sizeof(struct sgpu_sstate), stream);
 	if (!err)   /* pinned, next to the plan (see dev_planned) */
 		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	t[2] = times ? now_ms() : 0;
@@ -3308,12 +3461,10 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		count(&g_cnt_folds, 1);
 	}
 	t[3] = times ? now_ms() : 0;
-	mplan_apply(sessv, nsess, sout_h, prot);
 	if (times)
-		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu: gather %.3f "
-			"submit %.3f wait %.3f apply %.3f ms\n", n, nsess,
-			t[1] - t[0], t[2] - t[1], t[3] - t[2],
-			now_ms() - t[3]);
+		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu up=%u: gather "
+			"%.3f submit %.3f wait %.3f ms\n", n, nsess, nup,
+			t[1] - t[0], t[2] - t[1], t[3] - t[2]);
 	if (!nfail)
 		return 0;
 	/* a forged packet: undo on the device, fold on the host engine */
@@ -3331,8 +3482,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
-	mplan_unapply(sessv, nsess, w);
-	return -1;
+	return -1;      /* resident states untouched: the host folds */
 }
 
 /* any other batch: stage the device arrays through the host engine */
@@ -3409,6 +3559,18 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 		return 0;
 	if (d->n > UINT32_MAX / 4 || d->arena_size > UINT32_MAX)
 		return EINVAL;
+	/* many sessions: planned on the device against the resident states */
+	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess > 1 && d->sess &&
+	    !g_env.noplan && !g_env.general) {
+		int r = dev_mplanned(op, sessv, nsess, d);
+		if (r >= 0)
+			return r;
+	}
+	{
+		int err = sess_host(sessv, nsess);
+		if (err)
+			return err;
+	}
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess == 1 &&
 	    !d->sess && sessv[0]->nstreams <= 1 &&
 	    !g_env.noplan && !g_env.general) {
@@ -3423,12 +3585,6 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 		if (r >= 0)
 			return r;
 	}
-	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess > 1 && d->sess &&
-	    !g_env.noplan && !g_env.general) {
-		int r = dev_mplanned(op, sessv, nsess, d);
-		if (r >= 0)
-			return r;
-	}
 	return dev_staged(op, sessv, nsess, d);
 }
 
@@ -3440,8 +3596,14 @@ static int locked(int kind, int op, struct srtp **sessv, size_t nsess,
 {
 	int err;
 	table_rdlock();
-	err = kind == DEV ? run_dev(op, sessv, nsess, b)
-			  : run_batch(op, sessv, nsess, b);
+	if (kind == DEV) {
+		err = run_dev(op, sessv, nsess, b);
+	}
+	else {
+		err = sessv ? sess_host(sessv, nsess) : 0;
+		if (!err)
+			err = run_batch(op, sessv, nsess, b);
+	}
 	table_unlock();
 	return err;
 }
@@ -3500,8 +3662,15 @@ int srtp_stream_export(const struct srtp *srtp, uint32_t ssrc,
 		       struct srtp_stream_state *st)
 {
 	unsigned i;
+	struct srtp *sp = (struct srtp *)srtp;  /* state cache refresh */
+	int err;
 	if (!srtp || !st)
 		return EINVAL;
+	table_rdlock();
+	err = sess_host(&sp, 1);
+	table_unlock();
+	if (err)
+		return err;
 	for (i = 0; i < srtp->nstreams; i++) {
 		const struct srtp_stream *s = &srtp->streams[i];
 		if (s->ssrc != ssrc)
@@ -3527,6 +3696,11 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 	int err;
 	if (!srtp || !st)
 		return EINVAL;
+	table_rdlock();
+	err = sess_host(&srtp, 1);
+	table_unlock();
+	if (err)
+		return err;
 	err = stream_get(&s, srtp, st->ssrc);
 	if (err)
 		return err;

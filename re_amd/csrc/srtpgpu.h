@@ -282,6 +282,40 @@ struct sgpu_mplan_in {
 	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
 };
 
+/* the same in two launch groups: phase 1 sorts the packets by session
+ * (needs neither st_in nor the session map), phase 2 plans; the host
+ * prepares the session states in between (same arguments to both) */
+int   sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
+			   const struct sgpu_hdr *hdr, const uint32_t *pos,
+			   const uint32_t *end, const uint32_t *cap,
+			   uint64_t arena_size, const uint32_t *sess,
+			   const struct sgpu_sstate *st_in,
+			   struct sgpu_sstate *st_out, uint64_t *desc,
+			   void *scratch, size_t scratch_bytes,
+			   struct sgpu_plan_out *out, uint32_t *order,
+			   void *stream);
+
+/*
+ * Resident stream states: the device keeps one sgpu_sstate per table slot
+ * (stream 0 of the session's RTP direction), zeroed by
+ * sgpu_setup_sessions.  Multi-session device batches read and update it
+ * in place, so session state does not cross PCIe per call; the host
+ * reads it back (sgpu_sst_read) before any host-side path touches the
+ * session.  cm: session index -> comp index (2 * slot), device.
+ *   load:   st_in[k] = need && need[k] ? (table[slot] = up[k]) : table[slot]
+ *   commit: table[slot] = st_out[k] (touched ones, SST_TOUCHED cleared)
+ *           unless *fail or *nfail (device words, read when it runs)
+ *   read:   out[i] = table[slot[i]] (host arrays, synchronous)
+ */
+int   sgpu_sst_load(const uint32_t *cm, const uint8_t *need,
+		    const struct sgpu_sstate *up, uint32_t nsess,
+		    struct sgpu_sstate *st_in, void *stream);
+int   sgpu_sst_commit(const uint32_t *cm, const struct sgpu_sstate *st_out,
+		      uint32_t nsess, const uint32_t *fail,
+		      const uint32_t *nfail, void *stream);
+int   sgpu_sst_read(const uint32_t *slot, uint32_t n,
+		    struct sgpu_sstate *out);
+
 /* device scratch needed by sgpu_mplan_rtp */
 size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess);
 

@@ -705,3 +705,95 @@ def test_multi_session_shapes(suite, shape, torch_cuda):
         for x, y in zip(A[0][0] + A[0][1], B[0][0] + B[0][1]):
             assert (x == y).all(), mode
         assert A[1] == B[1] and A[2] == B[2], mode
+
+
+def next_batch(rng, last, n, nsess, plen=None):
+    """continue every session's sequence (ROC wraps inside)"""
+    out = []
+    for _ in range(n):
+        s = int(rng.integers(0, nsess))
+        last[s] = (last.get(s, 0) + 1) & 0xffff
+        out.append((s, rtp_packet(rng, last[s], 0x7000 + s,
+                                  plen=int(rng.integers(0, 300))
+                                  if plen is None else plen)))
+    return out
+
+
+@pytest.mark.parametrize("suite", [1, 4])
+def test_resident_state_across_paths(suite, torch_cuda):
+    """Multi-session device batches keep stream states in HBM across calls
+    (sgpu_sst_*); any host-side path reads them back first.  Sessions
+    driven through: device multi-session batch, per-packet srtp_encrypt /
+    srtp_decrypt on some sessions, another device batch, export + import
+    of one session, a host-array batch, a device batch, a forged packet in
+    a device batch, and again a device batch -- against twin sessions
+    driven only by the general engine (golden-pinned)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4242 + suite)
+    nsess = 24
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    last = {s: 65400 + 7 * s for s in range(nsess)}
+    plan = [("dev", next_batch(rng, last, 900, nsess)),
+            ("one", next_batch(rng, last, 40, 5)),
+            ("dev", next_batch(rng, last, 900, nsess)),
+            ("xport", None),
+            ("host", next_batch(rng, last, 600, nsess)),
+            ("dev", next_batch(rng, last, 900, nsess)),
+            ("forge", next_batch(rng, last, 900, nsess)),
+            ("dev", next_batch(rng, last, 900, nsess))]
+    res = {}
+    for mode in ("resident", "general"):
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        outs = []
+        for kind, pk in plan:
+            if kind == "xport":
+                for ctx in (tx[3], rx[3]):
+                    e, st = ctx.export(0x7000 + 3)
+                    assert e == 0
+                    assert ctx.import_(st) == 0
+                continue
+            if kind == "one":
+                for s, p in pk:
+                    mb = P.new_mbuf(p, len(p) + 64)
+                    e1 = tx[s].encrypt(mb)
+                    q = P.mbuf_bytes(mb)
+                    P.free_mbuf(mb)
+                    mb = P.new_mbuf(q, len(q) + 64)
+                    e2 = rx[s].decrypt(mb)
+                    outs.append((e1, q, e2, P.mbuf_bytes(mb)))
+                    P.free_mbuf(mb)
+                continue
+            arena, pos, end, cap, sess = to_arena(pk)
+            dev = mode == "resident" and kind != "host"
+            if dev:
+                enc = run_dev(torch, "srtp_encrypt", tx, arena, pos, end,
+                              cap, sess)
+            else:
+                enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap,
+                          sess, mode == "general")
+            prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
+                    for i, (s, _) in enumerate(pk)]
+            if kind == "forge":
+                q = bytearray(prot[77][1])
+                q[-1] ^= 0x01
+                prot[77] = (prot[77][0], bytes(q))
+            a2, p2, e2, c2, s2 = to_arena(prot)
+            if dev:
+                dec = run_dev(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2)
+            else:
+                dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
+                          mode == "general")
+            outs.append((enc, dec))
+        res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs))
+        for c in tx + rx:
+            c.close()
+    A, B = res["resident"], res["general"]
+    for x, y in zip(A[0], B[0]):
+        if isinstance(x[0], int):
+            assert x == y
+            continue
+        for u, v in zip(x[0] + x[1], y[0] + y[1]):
+            assert (u == v).all()
+    assert A[1] == B[1] and A[2] == B[2]

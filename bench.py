@@ -146,6 +146,11 @@ def main():
     ap.add_argument("--udp-batch", type=int, default=1024)
     ap.add_argument("--same-device", action="store_true",
                     help="testing only: all ranks on cuda:0, gloo counters")
+    ap.add_argument("--sync", action="store_true",
+                    help="synchronous srtp_*_batch_dev calls instead of the "
+                         "asynchronous srtp_*_batch_dev_async + "
+                         "srtp_batch_wait pair (protect and unprotect "
+                         "queued back to back on the stream)")
     ap.add_argument("--host-arrays", action="store_true",
                     help="srtp_*_batch with host pos/end/err arrays instead "
                          "of the device-resident srtp_*_batch_dev")
@@ -246,6 +251,8 @@ def main():
     # Default: srtp_*_batch_dev -- windows and results resident in HBM like
     # the packets; --host-arrays: srtp_*_batch with host windows.
     use_dev = not args.host_arrays
+    # asynchronous pair (srtp_*_batch_dev_async) for the RTP device path
+    use_async = use_dev and not args.sync and not args.e2e and not args.rtcp
     sess_d = None
     if use_dev:
         i32 = lambda a: torch.from_numpy(
@@ -322,16 +329,25 @@ def main():
         if use_dev:
             p_d.copy_(pos_d)
             e_d.copy_(end_d)
+            pend = []
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
                 if forge_idx is not None and opname == OPS[1]:
+                    if pend:    # the forgery reads protect's output
+                        assert P.batch_wait(pend.pop()[0]) == 0
                     arena.index_put_((forge_idx,), arena[forge_idx] ^ 0x40)
-                rc = P.device_batch_dev(opname, ss, arena.data_ptr(),
-                                        arena.numel(), p_d.data_ptr(),
-                                        e_d.data_ptr(), cap_d.data_ptr(),
-                                        er.data_ptr(), n,
-                                        sess_d.data_ptr() if sess_d
-                                        is not None else None, sptr)
+                a = (opname, ss, arena.data_ptr(), arena.numel(),
+                     p_d.data_ptr(), e_d.data_ptr(), cap_d.data_ptr(),
+                     er.data_ptr(), n,
+                     sess_d.data_ptr() if sess_d is not None else None, sptr)
+                if use_async:
+                    rc, t, keep = P.device_batch_dev_async(*a)
+                    pend.append((t, keep))
+                else:
+                    rc = P.device_batch_dev(*a)
+                assert rc == 0, (rc, P.lib().srtp_gpu_error())
+            for t, _ in pend:
+                rc = P.batch_wait(t)
                 assert rc == 0, (rc, P.lib().srtp_gpu_error())
             return 0
         np.copyto(p, pos)
@@ -496,7 +512,9 @@ def main():
                    "packets_per_gpu": n, "pkt_len": cfg["length"] or
                    "200/1400", "suite": P.suite_name(suite),
                    "sessions": nsess, "parallelism": "shard%d" % world,
-                   "api": "srtp_*_batch_dev" if use_dev else "srtp_*_batch"},
+                   "api": ("srtp_*_batch_dev_async" if use_async else
+                           "srtp_*_batch_dev") if use_dev else
+                   "srtp_*_batch"},
         "hbm_frac_e2e": round(tot_pkts / world * (4 * L + 2 * tag) /
                               (T / 1) / 1e9 / HBM_PEAK_GBS, 4),
         "errors": int(tot_err),

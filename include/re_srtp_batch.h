@@ -93,6 +93,38 @@ int srtcp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
 			    struct srtp_batch_dev *b);
 
 /**
+ * Asynchronous device-resident RTP batches: the call is queued on
+ * b->stream and returns without waiting for the GPU; srtp_batch_wait()
+ * completes it and returns what srtp_*_batch_dev would have returned.
+ * Calls issued one after another on the same stream run back to back on
+ * the GPU (e.g. protect on one context set, then unprotect of the same
+ * arena on another): each is planned against the states the calls
+ * before it leave, and a call queued behind one that must be completed on
+ * the host (a rejected device plan, a forged packet needing the host
+ * fold) does nothing on the GPU and is re-run when waited for -- results
+ * are always those of the synchronous calls in issue order.
+ *
+ * Until the ticket is waited for, sessv, the session contexts and the
+ * device arrays in *b (b itself is copied) must stay valid and unused by
+ * other calls; tickets are waited for on the issuing thread.  Any other
+ * call of this API on that thread first completes its pending tickets
+ * (their results stay in the tickets).  At most 4 calls are pending per
+ * thread (a fifth completes the oldest first).  Returns 0 with *tp set
+ * (the call may already have completed), or EINVAL / ENOMEM.
+ */
+struct srtp_batch_ticket;
+
+int srtp_encrypt_batch_dev_async(struct srtp **sessv, size_t nsess,
+				 struct srtp_batch_dev *b,
+				 struct srtp_batch_ticket **tp);
+int srtp_decrypt_batch_dev_async(struct srtp **sessv, size_t nsess,
+				 struct srtp_batch_dev *b,
+				 struct srtp_batch_ticket **tp);
+
+/** complete an asynchronous call: its result; frees the ticket */
+int srtp_batch_wait(struct srtp_batch_ticket *t);
+
+/**
  * Stream state export/import (checkpoint/resume and multi-GPU hand-off:
  * lets a second context continue an SSRC exactly where another left it).
  * Layout follows struct srtp_stream (src/srtp/srtp.h:29-38).

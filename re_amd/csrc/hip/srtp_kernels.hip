@@ -706,6 +706,36 @@ extern "C" int sgpu_table_reserve(uint32_t nsessions)
 	return e;
 }
 
+/* ---- asynchronous batch chains (srtpgpu.h sgpu_gate_*) --------------- */
+
+__global__ void k_gate_pred(const uint32_t *pred, uint32_t *fail)
+{
+	if (*pred)
+		atomicOr(fail, (uint32_t)SPF_PRED);
+}
+
+__global__ void k_gate_set(const uint32_t *fail, const uint32_t *nfail,
+			   uint32_t *gate)
+{
+	*gate = (*fail || (nfail && *nfail)) ? 1u : 0u;
+}
+
+extern "C" int sgpu_gate_pred(const uint32_t *pred, uint32_t *fail,
+			      void *stream)
+{
+	hipLaunchKernelGGL(k_gate_pred, dim3(1), dim3(1), 0,
+			   (hipStream_t)stream, pred, fail);
+	return herr(hipGetLastError(), "k_gate_pred launch");
+}
+
+extern "C" int sgpu_gate_set(const uint32_t *fail, const uint32_t *nfail,
+			     uint32_t *gate, void *stream)
+{
+	hipLaunchKernelGGL(k_gate_set, dim3(1), dim3(1), 0,
+			   (hipStream_t)stream, fail, nfail, gate);
+	return herr(hipGetLastError(), "k_gate_set launch");
+}
+
 /* ---- resident RTP stream states (srtpgpu.h sgpu_sst_*) ---------------- */
 
 __global__ void k_sst_zero(const uint32_t *slot, uint32_t n,

@@ -81,6 +81,9 @@ struct srtp {
 				   (detects sessv entries aliasing one
 				   context) */
 	int dres;               /* where stream 0's RTP state lives: DRES_* */
+	uint64_t pend_p;        /* async: last pending single-stream call on
+				   it (issuing thread's sequence number) */
+	uint64_t pend_m;        /* ... last pending multi-session call */
 };
 
 /*
@@ -279,9 +282,12 @@ static void slot_put(uint32_t s)
 /* ------------------------------------------------------------------ */
 /* srtp_alloc (srtp.c:88-180)                                          */
 
+static void tk_drain(void);
+
 static void destructor(void *arg)
 {
 	struct srtp *srtp = arg;
+	tk_drain();     /* a pending call of this thread may still use it */
 	slot_put(srtp->slot);
 }
 
@@ -341,6 +347,9 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 		return EINVAL;
 	if (!gpu_ready())
 		return ENOSYS;
+	/* this thread's pending calls hold the table (growth waits for
+	 * them) */
+	tk_drain();
 
 	req = calloc(n ? n : 1, sizeof(*req));
 	slots = calloc(n ? n : 1, sizeof(*slots));
@@ -1157,18 +1166,23 @@ struct ws {
 
 static __thread struct ws *t_ws;
 
+static struct ws *ws_new(void)
+{
+	struct ws *w = calloc(1, sizeof(*w));
+	if (!w)
+		return NULL;
+	w->stream = sgpu_stream_create();
+	if (!w->stream) {
+		free(w);
+		return NULL;
+	}
+	return w;
+}
+
 static struct ws *ws_get(void)
 {
-	if (!t_ws) {
-		t_ws = calloc(1, sizeof(*t_ws));
-		if (!t_ws)
-			return NULL;
-		t_ws->stream = sgpu_stream_create();
-		if (!t_ws->stream) {
-			free(t_ws);
-			t_ws = NULL;
-		}
-	}
+	if (!t_ws)
+		t_ws = ws_new();
 	return t_ws;
 }
 
@@ -1597,6 +1611,7 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 		     size_t n)
 {
 	int err;
+	tk_drain();
 	table_rdlock();
 	err = srtp ? sess_host(&srtp, 1) : 0;
 	if (!err)
@@ -2213,6 +2228,8 @@ struct mpg {
 	atomic_int bad;
 	uint8_t *need;          /* resident: st[k] is to be uploaded */
 	atomic_uint nup;        /* ... how many */
+	uint64_t pend, done;    /* async: this call's sequence number, the
+				   thread's last completed one */
 };
 
 static void mplan_gather_part(void *arg, size_t a, size_t b)
@@ -2238,6 +2255,15 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 		}
 		if (g->cm)
 			g->cm[k] = 2u * s->slot;        /* comp[0] = RTP */
+		if (g->pend) {
+			/* a pending single-stream call plans from host state
+			 * this call cannot see yet */
+			if (s->pend_p > g->done) {
+				atomic_store(&g->bad, 1);
+				return;
+			}
+			((struct srtp *)s)->pend_m = g->pend;
+		}
 		if (g->need) {
 			/* resident states: upload only what the host changed
 			 * since the device last held it */
@@ -2269,7 +2295,7 @@ static int mplan_gather(struct srtp **sessv, size_t nsess,
 			struct sgpu_sstate *st, uint32_t *cm)
 {
 	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, NULL,
-			0};
+			0, 0, 0};
 	do {
 		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
 	} while (!g.epoch);
@@ -2286,10 +2312,11 @@ static int mplan_gather(struct srtp **sessv, size_t nsess,
  */
 static int mplan_gather_res(struct srtp **sessv, size_t nsess,
 			    struct sgpu_sstate *st, uint32_t *cm,
-			    uint8_t *need, uint32_t *nup)
+			    uint8_t *need, uint32_t *nup, uint64_t pend,
+			    uint64_t done)
 {
 	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, need,
-			0};
+			0, pend, done};
 	size_t k;
 	do {
 		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
@@ -2341,7 +2368,7 @@ static void mplan_apply_part(void *arg, size_t a, size_t b)
 static void mplan_apply(struct srtp **sessv, size_t nsess,
 			const struct sgpu_sstate *o, int prot)
 {
-	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0, NULL, 0};
+	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0, NULL, 0, 0, 0};
 	par_for(nsess, mplan_par(), mplan_apply_part, &g);
 }
 
@@ -3011,33 +3038,46 @@ static int run_batch(int op, struct srtp **sessv, size_t nsess,
 static int run_batch(int op, struct srtp **sessv, size_t nsess,
 		     struct srtp_batch *b);
 
-/* single-stream RTP batch planned and processed on the device; -1: not
- * plannable (nothing modified), else 0 / errno */
-static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
+/* one device-planned batch between its launches and its completion
+ * (the synchronous calls and the asynchronous tickets share it) */
+struct dcall {
+	int op;
+	struct srtp **sessv;
+	size_t nsess;
+	struct srtp_batch_dev d;
+	struct ws *w;
+	const uint32_t *pred;   /* gate word of the pending call before */
+	uint32_t *gate;         /* this call's gate word (chained) or NULL */
+	struct sgpu_plan_in in; /* single stream: the plan input */
+	size_t foff;            /* ... fold area in w->pl */
+	uint32_t nup;           /* many sessions: states uploaded */
+	uint64_t pend, done;    /* async: sequence numbers (mpg) */
+	double t[3];
+};
+
+/* single-stream RTP batch planned and processed on the device: the
+ * launches (no host synchronisation) */
+static int dev_planned_issue(struct dcall *k)
 {
-	const int prot = op == OP_RTP_ENC;
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
 	const struct comp *c0 = &s->rtp;
 	const size_t n = d->n;
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
 	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 			      (T > 4 ? T : 4u)) : 0u;
-	const unsigned ns0 = s->nstreams;
-	struct srtp_stream old;
-	struct sgpu_plan_in in;
 	struct sgpu_plan_out *po, *po_d;
 	struct sgpu_hdr *hd_d;
 	uint64_t *desc_d;
-	uint32_t *scr, *es_d, *save_d, *nfail_d, *flist_d, nfail = 0;
+	uint32_t *scr, *es_d, *save_d, *nfail_d, *flist_d;
 	uint32_t cm = c0->dev;
 	uint8_t *vd_d;
-	void *stream;
-	struct ws *w = ws_get();
+	void *stream = d->stream;       /* NULL: the default (null) stream */
 	size_t foff;
 	int err;
 
-	if (!w)
-		return ENOMEM;
-	stream = d->stream;     /* NULL: the default (null) stream */
 	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
 	if (!err)
 		err = pool_reserve(w, &w->dsc, n * 12);
@@ -3047,6 +3087,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = pool_reserve(w, &w->cm, 4);
 	/* pl: plan out | plan scratch | fold out | fold scratch */
 	foff = (sizeof(struct sgpu_plan_out) + (n / 256 + 8) * 4 + 63) & ~63ul;
+	k->foff = foff;
 	if (!err)
 		err = pool_reserve(w, &w->pl, foff + 64 + (n / 256 + 4) * 20);
 	if (!err)
@@ -3064,19 +3105,21 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	scr = (uint32_t *)(w->pl.d + sizeof(*po));
 	es_d = (uint32_t *)w->es.d;
 
-	plan_in(&in, s, (uint32_t)n, prot, T, need);
+	plan_in(&k->in, s, (uint32_t)n, prot, T, need);
 	{
 		/* one launch: parse + end copy + zeroed counters + comp map */
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
 			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm};
-		in.zeroed = 1;
+		k->in.zeroed = 1;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
 					  &pro, stream);
 	}
+	if (!err && k->pred)
+		err = sgpu_gate_pred(k->pred, &po_d->fail, stream);
 	if (!err)
-		err = sgpu_plan_rtp(&in, hd_d, d->pos, es_d, d->cap,
+		err = sgpu_plan_rtp(&k->in, hd_d, d->pos, es_d, d->cap,
 				    d->arena_size, desc_d, scr, po_d, stream);
 	if (!err) {
 		struct sgpu_compact C = {
@@ -3090,18 +3133,47 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
 					(uint32_t)n,
 					prot ? (int32_t)T : -(int32_t)T, stream);
+	if (!err && k->gate)
+		err = sgpu_gate_set(&po_d->fail, nfail_d, k->gate, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
 	/* the miss count lands in pinned memory next to the plan (a
 	 * pageable destination would stage the copy through the runtime) */
 	if (!err)
 		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
-	if (!err)
-		err = sgpu_stream_sync(stream);
-	if (err)
-		return err;
+	return err;
+}
+
+/* ... after its launches completed: 0 / errno, -1 not plannable or a
+ * forged packet the host must fold (nothing modified), -2 gated by the
+ * chained call before (nothing modified) */
+static int dev_planned_finish(struct dcall *k)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const unsigned ns0 = s->nstreams;
+	const size_t foff = k->foff;
+	struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
+	struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
+	struct sgpu_hdr *hd_d = (struct sgpu_hdr *)w->hd.d;
+	uint64_t *desc_d = (uint64_t *)w->dsc.d;
+	uint32_t *nfail_d = (uint32_t *)w->vs.d;
+	uint32_t *save_d = (uint32_t *)(w->vs.d + 64);
+	uint8_t *vd_d = w->vs.d + 64 + n * 4;
+	uint32_t *es_d = (uint32_t *)w->es.d;
+	void *stream = d->stream;
+	struct srtp_stream old;
+	uint32_t nfail;
+	int err = 0;
+
 	nfail = *(const uint32_t *)(po + 1);
 	if (po->fail) {
+		if (po->fail & SPF_PRED)
+			return -2;
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
@@ -3120,8 +3192,8 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		struct sgpu_fold_out *fo = (struct sgpu_fold_out *)(w->pl.h + foff);
 		struct sgpu_fold_out *fo_d =
 			(struct sgpu_fold_out *)(w->pl.d + foff);
-		err = sgpu_fold_rtp(&in, hd_d, desc_d, vd_d, es_d, d->pos, d->end,
-				    d->err, c0->mode == SGPU_MODE_GCM,
+		err = sgpu_fold_rtp(&k->in, hd_d, desc_d, vd_d, es_d, d->pos,
+				    d->end, d->err, c0->mode == SGPU_MODE_GCM,
 				    (uint32_t *)(w->pl.d + foff + 64), fo_d,
 				    stream);
 		if (!err)
@@ -3143,7 +3215,7 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	}
 	count(&g_cnt_folds, 1);
 	/* undo on the device, fold on the host engine */
-	if (!err) {
+	{
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
@@ -3159,6 +3231,27 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		return err;
 	plan_unapply(s, ns0, &old);
 	return -1;
+}
+
+/* synchronous: -1 not plannable (nothing modified), else 0 / errno */
+static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
+{
+	struct dcall k;
+	int err;
+	memset(&k, 0, sizeof(k));
+	k.op = op;
+	k.sessv = &s;
+	k.nsess = 1;
+	k.d = *d;
+	k.w = ws_get();
+	if (!k.w)
+		return ENOMEM;
+	err = dev_planned_issue(&k);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	if (err)
+		return err;
+	return dev_planned_finish(&k);
 }
 
 /*
@@ -3307,14 +3400,18 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 /*
  * Many sessions with at most one RTP stream each, every array in HBM: the
  * multi-session device planner (plan_multi.hip) plus the compact kernels
- * in length order; host work is O(sessions) (gather the stream states,
- * apply the returned ones).  -1: not plannable (nothing modified), or a
- * forged packet (undone; the caller folds through the staged engine).
+ * in length order, against the session states resident in HBM
+ * (sgpu_sst_*); host work is one O(sessions) pass (slot map, residency).
+ * The launches; -1: not plannable (after a synchronisation; nothing
+ * modified).
  */
-static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
-			struct srtp_batch_dev *d)
+static int dev_mplanned_issue(struct dcall *k)
 {
-	const int prot = op == OP_RTP_ENC;
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp **sessv = k->sessv;
+	const size_t nsess = k->nsess;
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
 	const struct comp *c0 = &sessv[0]->rtp;
 	const size_t n = d->n;
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
@@ -3324,18 +3421,13 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	struct sgpu_mplan_in in;
 	struct sgpu_hdr *hd_d;
 	uint64_t *desc_d;
-	uint32_t *es_d, *save_d, *nfail_d, *cm_h, *order_d, nfail = 0, bits = 1;
-	uint32_t nup = 0;
+	uint32_t *es_d, *save_d, *nfail_d, *cm_h, *order_d, bits = 1;
 	uint8_t *vd_d, *need_h, *need_d;
 	size_t scr;
 	void *stream = d->stream;
-	struct ws *w = ws_get();
 	const int times = g_env.times;
-	double t[4];
 	int err;
 
-	if (!w)
-		return ENOMEM;
 	while (bits < 32 && ((size_t)1 << bits) < nsess)
 		bits++;
 	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
@@ -3399,26 +3491,29 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 				   d->arena_size, d->sess, sin_d, sout_d,
 				   desc_d, w->mscr.d, scr, po_d, order_d,
 				   stream);
+	if (!err && k->pred)
+		err = sgpu_gate_pred(k->pred, &po_d->fail, stream);
 	if (err)
 		return err;
 	/* one pass over the sessions: suite check, slot map, and the states
 	 * the device does not hold yet (none once sessions are resident) */
-	t[0] = times ? now_ms() : 0;
-	if (mplan_gather_res(sessv, nsess, up_h, cm_h, need_h, &nup)) {
+	k->t[0] = times ? now_ms() : 0;
+	if (mplan_gather_res(sessv, nsess, up_h, cm_h, need_h, &k->nup,
+			     k->pend, k->done)) {
 		/* the queued sort only wrote scratch */
 		err = sgpu_stream_sync(stream);
 		return err ? err : -1;
 	}
-	t[1] = times ? now_ms() : 0;
+	k->t[1] = times ? now_ms() : 0;
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
-	if (!err && nup)
+	if (!err && k->nup)
 		err = sgpu_memcpy_h2d(up_d, up_h,
 				      nsess * (sizeof(struct sgpu_sstate) + 1),
 				      stream);
 	if (!err)
 		err = sgpu_sst_load((const uint32_t *)w->cm.d,
-				    nup ? need_d : NULL, up_d, (uint32_t)nsess,
-				    sin_d, stream);
+				    k->nup ? need_d : NULL, up_d,
+				    (uint32_t)nsess, sin_d, stream);
 	if (!err)
 		err = sgpu_mplan_rtp_phase(2, &in, hd_d, d->pos, es_d, d->cap,
 					   d->arena_size, d->sess, sin_d,
@@ -3442,33 +3537,56 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
 				      (uint32_t)nsess, &po_d->fail, nfail_d,
 				      stream);
+	if (!err && k->gate)
+		err = sgpu_gate_set(&po_d->fail, nfail_d, k->gate, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
 	if (!err)   /* pinned, next to the plan (see dev_planned) */
 		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
-	t[2] = times ? now_ms() : 0;
-	if (!err)
-		err = sgpu_stream_sync(stream);
-	if (err)
-		return err;
-	nfail = *(const uint32_t *)(po + 1);
+	k->t[2] = times ? now_ms() : 0;
+	return err;
+}
+
+/* ... after its launches completed: 0 / errno, -1 not plannable or a
+ * forged packet (undone; the host folds), -2 gated by the chained call
+ * before (nothing modified) */
+static int dev_mplanned_finish(struct dcall *k)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp **sessv = k->sessv;
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const struct comp *c0 = &sessv[0]->rtp;
+	const size_t n = d->n;
+	struct sgpu_plan_out *po = (struct sgpu_plan_out *)w->pl.h;
+	struct sgpu_plan_out *po_d = (struct sgpu_plan_out *)w->pl.d;
+	struct sgpu_hdr *hd_d = (struct sgpu_hdr *)w->hd.d;
+	uint64_t *desc_d = (uint64_t *)w->dsc.d;
+	uint32_t *nfail_d = (uint32_t *)w->vs.d;
+	uint32_t *save_d = (uint32_t *)(w->vs.d + 64);
+	uint8_t *vd_d = w->vs.d + 64 + n * 4;
+	uint32_t *es_d = (uint32_t *)w->es.d;
+	void *stream = d->stream;
+	uint32_t nfail = *(const uint32_t *)(po + 1);
+	int err;
+
+	if (g_env.times)
+		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu up=%u: gather "
+			"%.3f submit %.3f wait %.3f ms\n", n, k->nsess, k->nup,
+			k->t[1] - k->t[0], k->t[2] - k->t[1],
+			now_ms() - k->t[2]);
 	if (po->fail) {
+		if (po->fail & SPF_PRED)
+			return -2;
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
-	if (nfail) {
-		count(&g_cnt_misses, nfail);
-		count(&g_cnt_folds, 1);
-	}
-	t[3] = times ? now_ms() : 0;
-	if (times)
-		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu up=%u: gather "
-			"%.3f submit %.3f wait %.3f ms\n", n, nsess, nup,
-			t[1] - t[0], t[2] - t[1], t[3] - t[2]);
 	if (!nfail)
 		return 0;
+	count(&g_cnt_misses, nfail);
+	count(&g_cnt_folds, 1);
 	/* a forged packet: undo on the device, fold on the host engine */
-	if (!err) {
+	{
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
@@ -3483,6 +3601,255 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	if (err)
 		return err;
 	return -1;      /* resident states untouched: the host folds */
+}
+
+/* synchronous: -1 not plannable (nothing modified), else 0 / errno */
+static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
+			struct srtp_batch_dev *d)
+{
+	struct dcall k;
+	int err;
+	memset(&k, 0, sizeof(k));
+	k.op = op;
+	k.sessv = sessv;
+	k.nsess = nsess;
+	k.d = *d;
+	k.w = ws_get();
+	if (!k.w)
+		return ENOMEM;
+	err = dev_mplanned_issue(&k);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	if (err)
+		return err;
+	return dev_mplanned_finish(&k);
+}
+
+/* ---- asynchronous device batches (re_srtp_batch.h) -------------------- */
+
+#define TK_MAX   4              /* pending calls per thread */
+#define TK_GATES 64             /* per-thread gate words (a ring > TK_MAX) */
+
+enum { TK_PLANNED = 1, TK_MPLANNED = 2, TK_DONE = 3 };
+
+struct srtp_batch_ticket {
+	struct srtp_batch_ticket *next;
+	pthread_t owner;
+	uint64_t seq;
+	int kind;               /* TK_* */
+	int result;             /* TK_DONE: the call's result */
+	struct dcall k;
+	void *ev;               /* recorded after the launches */
+};
+
+static __thread struct srtp_batch_ticket *t_tk_head, *t_tk_tail;
+static __thread uint64_t t_tk_seq, t_tk_done;
+static __thread int t_tk_n;
+static __thread void *t_tk_stream;
+static __thread uint32_t *t_gates;
+static __thread struct ws *t_aws[TK_MAX + 1];
+static __thread int t_naws;
+
+static int run_dev(int op, struct srtp **sessv, size_t nsess,
+		   struct srtp_batch_dev *d);
+static int dev_staged(int op, struct srtp **sessv, size_t nsess,
+		      struct srtp_batch_dev *d);
+
+/* complete the thread's oldest pending call (its result stays in the
+ * ticket until srtp_batch_wait) */
+static void tk_finish_one(void)
+{
+	struct srtp_batch_ticket *t = t_tk_head;
+	struct dcall *k = &t->k;
+	int r;
+
+	r = sgpu_event_sync(t->ev);
+	if (!r)
+		r = t->kind == TK_PLANNED ? dev_planned_finish(k)
+					  : dev_mplanned_finish(k);
+	t_tk_head = t->next;
+	if (!t_tk_head)
+		t_tk_tail = NULL;
+	t_tk_n--;
+	t_tk_done = t->seq;
+	t_aws[t_naws++] = k->w;
+	sgpu_event_destroy(t->ev);
+	t->ev = NULL;
+	if (r == -2) {
+		/* gated behind an earlier call that the host completed:
+		 * nothing was modified, run it now */
+		r = run_dev(k->op, k->sessv, k->nsess, &k->d);
+	}
+	else if (r == -1) {
+		r = sess_host(k->sessv, k->nsess);
+		if (!r)
+			r = dev_staged(k->op, k->sessv, k->nsess, &k->d);
+	}
+	t->result = r;
+	t->kind = TK_DONE;
+	table_unlock();         /* held since the call was issued */
+}
+
+/* complete every pending call of this thread (before any other entry
+ * point: those see the sessions as the calls in order leave them) */
+static void tk_drain(void)
+{
+	while (t_tk_head)
+		tk_finish_one();
+}
+
+static void tk_drain_upto(uint64_t seq)
+{
+	while (t_tk_head && t_tk_done < seq)
+		tk_finish_one();
+}
+
+static int batch_async(int op, struct srtp **sessv, size_t nsess,
+		       struct srtp_batch_dev *d,
+		       struct srtp_batch_ticket **tp)
+{
+	struct srtp_batch_ticket *t;
+	struct dcall *k;
+	size_t i;
+	int kind = 0, err;
+
+	if (!tp || !sessv || !nsess || !d || !d->arena || !d->pos ||
+	    !d->end || !d->cap || !d->err)
+		return EINVAL;
+	for (i = 0; i < nsess; i++)
+		if (!sessv[i])
+			return EINVAL;
+	if (d->n > UINT32_MAX / 4 || d->arena_size > UINT32_MAX)
+		return EINVAL;
+	t = calloc(1, sizeof(*t));
+	if (!t)
+		return ENOMEM;
+	t->owner = pthread_self();
+	*tp = t;
+	env_init();
+	/* the chain's gate words are ordered by the stream */
+	if (t_tk_n && t_tk_stream != d->stream)
+		tk_drain();
+	while (t_tk_n >= TK_MAX)
+		tk_finish_one();
+	if (!t_gates) {
+		t_gates = sgpu_malloc(TK_GATES * 4);
+		if (!t_gates || sgpu_memset(t_gates, 0, TK_GATES * 4, NULL) ||
+		    sgpu_stream_sync(NULL)) {
+			t->kind = TK_DONE;
+			t->result = ENOMEM;
+			return 0;
+		}
+	}
+	if (d->n && (op == OP_RTP_ENC || op == OP_RTP_DEC) &&
+	    !g_env.noplan && !g_env.general) {
+		if (nsess == 1 && !d->sess)
+			kind = TK_PLANNED;
+		else if (nsess > 1 && d->sess)
+			kind = TK_MPLANNED;
+	}
+	if (kind == TK_PLANNED) {
+		struct srtp *s = sessv[0];
+		uint64_t p = s->pend_p > s->pend_m ? s->pend_p : s->pend_m;
+		/* plans from the host copy of its state: the pending calls
+		 * on it complete first */
+		if (p > t_tk_done)
+			tk_drain_upto(p);
+		table_rdlock();
+		err = sess_host(&s, 1);
+		table_unlock();
+		if (err || s->nstreams > 1)
+			kind = 0;
+	}
+	if (!kind) {
+		tk_drain();
+		table_rdlock();
+		t->result = run_dev(op, sessv, nsess, d);
+		table_unlock();
+		t->kind = TK_DONE;
+		return 0;
+	}
+	k = &t->k;
+	k->op = op;
+	k->sessv = sessv;
+	k->nsess = nsess;
+	k->d = *d;
+	k->w = t_naws ? t_aws[--t_naws] : ws_new();
+	if (!k->w) {
+		t->kind = TK_DONE;
+		t->result = ENOMEM;
+		return 0;
+	}
+	t->seq = t_tk_seq + 1;
+	k->pred = t_tk_n ? &t_gates[t_tk_tail->seq % TK_GATES] : NULL;
+	k->gate = &t_gates[t->seq % TK_GATES];
+	k->pend = t->seq;
+	k->done = t_tk_done;
+	t->ev = sgpu_event_create();
+	table_rdlock();         /* until the call completes (tk_finish_one) */
+	err = t->ev ? 0 : ENOMEM;
+	if (!err)
+		err = kind == TK_PLANNED ? dev_planned_issue(k)
+					 : dev_mplanned_issue(k);
+	if (!err)
+		err = sgpu_event_record(t->ev, d->stream);
+	if (err) {
+		/* nothing queued that completes the call: run it here */
+		t_aws[t_naws++] = k->w;
+		if (t->ev)
+			sgpu_event_destroy(t->ev);
+		t->ev = NULL;
+		table_unlock();
+		if (err == -1) {
+			tk_drain();
+			table_rdlock();
+			err = sess_host(sessv, nsess);
+			if (!err)
+				err = run_dev(op, sessv, nsess, d);
+			table_unlock();
+		}
+		t->kind = TK_DONE;
+		t->result = err;
+		return 0;
+	}
+	t_tk_seq = t->seq;
+	t->kind = kind;
+	if (kind == TK_PLANNED)
+		sessv[0]->pend_p = t->seq;
+	if (t_tk_tail)
+		t_tk_tail->next = t;
+	else
+		t_tk_head = t;
+	t_tk_tail = t;
+	t_tk_n++;
+	t_tk_stream = d->stream;
+	return 0;
+}
+
+int srtp_encrypt_batch_dev_async(struct srtp **sessv, size_t nsess,
+				 struct srtp_batch_dev *b,
+				 struct srtp_batch_ticket **tp)
+{
+	return batch_async(OP_RTP_ENC, sessv, nsess, b, tp);
+}
+
+int srtp_decrypt_batch_dev_async(struct srtp **sessv, size_t nsess,
+				 struct srtp_batch_dev *b,
+				 struct srtp_batch_ticket **tp)
+{
+	return batch_async(OP_RTP_DEC, sessv, nsess, b, tp);
+}
+
+int srtp_batch_wait(struct srtp_batch_ticket *t)
+{
+	int r;
+	if (!t || !pthread_equal(t->owner, pthread_self()))
+		return EINVAL;
+	while (t->kind != TK_DONE)
+		tk_finish_one();
+	r = t->result;
+	free(t);
+	return r;
 }
 
 /* any other batch: stage the device arrays through the host engine */
@@ -3595,6 +3962,7 @@ static int locked(int kind, int op, struct srtp **sessv, size_t nsess,
 		  void *b)
 {
 	int err;
+	tk_drain();
 	table_rdlock();
 	if (kind == DEV) {
 		err = run_dev(op, sessv, nsess, b);
@@ -3666,6 +4034,7 @@ int srtp_stream_export(const struct srtp *srtp, uint32_t ssrc,
 	int err;
 	if (!srtp || !st)
 		return EINVAL;
+	tk_drain();
 	table_rdlock();
 	err = sess_host(&sp, 1);
 	table_unlock();
@@ -3696,6 +4065,7 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 	int err;
 	if (!srtp || !st)
 		return EINVAL;
+	tk_drain();
 	table_rdlock();
 	err = sess_host(&srtp, 1);
 	table_unlock();

@@ -225,7 +225,22 @@ enum {
 	SPF_SIZE    = 1u << 6,  /* payload of 1 MiB or more */
 	SPF_CAP     = 1u << 7,  /* protect: tag does not fit (ENOMEM) */
 	SPF_BAD     = 1u << 8,  /* invalid window (pos/end/cap/arena) */
+	SPF_PRED    = 1u << 9,  /* the chained call before did not complete
+				   on the device (async batches) */
 };
+
+/*
+ * Chained asynchronous batches: a call queued behind a pending one on the
+ * same stream is planned as failed (SPF_PRED, nothing modified) if the
+ * earlier call's gate word is set, i.e. if that call must be completed on
+ * the host; it is then re-run when waited for.
+ *   pred: *fail |= SPF_PRED if *pred (launch after fail is zeroed, before
+ *         the plan's guards are derived from it)
+ *   set:  *gate = *fail || (nfail && *nfail)  (after the call's launches)
+ */
+int   sgpu_gate_pred(const uint32_t *pred, uint32_t *fail, void *stream);
+int   sgpu_gate_set(const uint32_t *fail, const uint32_t *nfail,
+		    uint32_t *gate, void *stream);
 
 #define SGPU_PLAN_TAIL 65
 struct sgpu_plan_out {

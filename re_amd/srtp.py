@@ -103,7 +103,8 @@ EXPORTS = (
     "srtcp_decrypt_mbufs", "srtp_encrypt_batch", "srtp_decrypt_batch",
     "srtcp_encrypt_batch", "srtcp_decrypt_batch", "srtp_encrypt_batch_dev",
     "srtp_decrypt_batch_dev", "srtcp_encrypt_batch_dev",
-    "srtcp_decrypt_batch_dev", "srtp_stream_export",
+    "srtcp_decrypt_batch_dev", "srtp_encrypt_batch_dev_async",
+    "srtp_decrypt_batch_dev_async", "srtp_batch_wait", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
     "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune", "srtp_gpu_counter",
     "srtp_udp_alloc", "srtp_udp_recv", "srtp_udp_send", "srtp_udp_stats",
@@ -143,6 +144,11 @@ def load():
             ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatch)]
         getattr(L, f + "_batch_dev").argtypes = [
             ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatchDev)]
+    for f in ("srtp_encrypt", "srtp_decrypt"):
+        getattr(L, f + "_batch_dev_async").argtypes = [
+            ctypes.POINTER(vp), sz, ctypes.POINTER(SrtpBatchDev),
+            ctypes.POINTER(vp)]
+    L.srtp_batch_wait.argtypes = [vp]
     L.srtp_suite_name.restype = ctypes.c_char_p
     L.srtp_suite_name.argtypes = [ctypes.c_int]
     L.srtp_gpu_error.restype = ctypes.c_char_p
@@ -435,6 +441,32 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
     sv = session_array(sessions)
     return getattr(lib(), opname + "_batch_dev")(sv, len(sv),
                                                  ctypes.byref(b))
+
+
+def device_batch_dev_async(opname, sessions, arena_ptr, arena_size,
+                           pos_ptr, end_ptr, cap_ptr, err_ptr, n,
+                           sess_ptr=None, stream=None):
+    """srtp_*_batch_dev_async: returns (rc, ticket, keepalive); pass the
+    ticket to batch_wait() (the session array must outlive it: keep the
+    returned keepalive until then)."""
+    b = SrtpBatchDev()
+    b.arena = arena_ptr
+    b.arena_size = arena_size
+    b.pos, b.end, b.cap, b.err = pos_ptr, end_ptr, cap_ptr, err_ptr
+    b.sess = sess_ptr
+    b.n = n
+    b.stream = stream
+    sv = session_array(sessions)
+    t = ctypes.c_void_p()
+    rc = getattr(lib(), opname + "_batch_dev_async")(sv, len(sv),
+                                                     ctypes.byref(b),
+                                                     ctypes.byref(t))
+    return rc, t, sv
+
+
+def batch_wait(ticket):
+    """srtp_batch_wait: the asynchronous call's result"""
+    return lib().srtp_batch_wait(ticket)
 
 
 def counter(name):

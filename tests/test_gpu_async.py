@@ -1,0 +1,195 @@
+"""GPU tests of the asynchronous device batches (srtp_*_batch_dev_async +
+srtp_batch_wait, include/re_srtp_batch.h).
+
+An asynchronous call must give exactly the results of the synchronous
+srtp_*_batch_dev calls made in issue order -- which the other GPU tests pin
+to the oracle and the reference goldens -- also when a call in the chain
+has to be completed on the host (a rejected device plan, a forged packet),
+which gates every call queued behind it.
+"""
+import numpy as np
+import pytest
+
+import re_amd.srtp as P
+from tests.test_gpu_fastpath import (keys_for, multi_session_traffic,
+                                     next_batch, seq_batch, states, to_arena)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+class Dev:
+    """one batch's device arrays"""
+
+    def __init__(self, torch, arena, pos, end, cap, sess):
+        t = lambda a: torch.from_numpy(
+            np.ascontiguousarray(a, dtype=np.int64)).cuda().to(torch.int32)
+        self.arena = torch.from_numpy(arena.copy()).cuda()
+        self.nbytes = arena.nbytes
+        self.pos, self.end, self.cap = t(pos), t(end), t(cap)
+        self.err = torch.full((len(pos),), -1, dtype=torch.int32,
+                              device="cuda")
+        self.sess = t(sess) if sess is not None else None
+        self.n = len(pos)
+
+    def args(self):
+        return (self.arena.data_ptr(), self.nbytes, self.pos.data_ptr(),
+                self.end.data_ptr(), self.cap.data_ptr(), self.err.data_ptr(),
+                self.n, self.sess.data_ptr() if self.sess is not None
+                else None)
+
+    def out(self):
+        u = lambda x: x.cpu().numpy().view(np.uint32)
+        return (self.arena.cpu().numpy(), u(self.pos), u(self.end),
+                self.err.cpu().numpy())
+
+
+def run_chain(torch, calls, mode):
+    """calls: [(opname, sessions, Dev)] on one device arena each; mode
+    "sync" or "async" (all issued, then all waited); returns outputs"""
+    torch.cuda.synchronize()
+    if mode == "sync":
+        for op, ss, d in calls:
+            assert P.device_batch_dev(op, ss, *d.args()) == 0
+    else:
+        pend = []
+        for op, ss, d in calls:
+            rc, t, keep = P.device_batch_dev_async(op, ss, *d.args())
+            assert rc == 0
+            pend.append((t, keep))
+        for t, _ in pend:
+            assert P.batch_wait(t) == 0
+    torch.cuda.synchronize()
+    return [d.out() for _, _, d in calls]
+
+
+def same(a, b):
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert (u == v).all()
+
+
+def roundtrip_calls(torch, tx, rx, pkts, sess=None):
+    """protect then unprotect of one arena, chained"""
+    arena, pos, end, cap, s = to_arena(pkts)
+    d = Dev(torch, arena, pos, end, cap, s if sess else None)
+    return [("srtp_encrypt", tx, d), ("srtp_decrypt", rx, d)]
+
+
+@pytest.mark.parametrize("suite", [1, 4])
+def test_async_single_stream_chain(suite, torch_cuda):
+    """protect (tx) then unprotect (rx) of one arena, then a second batch
+    on the same contexts: async == sync, states included"""
+    torch = torch_cuda
+    rng = np.random.default_rng(31 + suite)
+    key = keys_for(suite, 1)[0]
+    b1 = seq_batch(rng, range(65400, 65400 + 2000))
+    b2 = seq_batch(rng, range(65400 + 2000, 65400 + 3000))
+    res = {}
+    for mode in ("sync", "async"):
+        tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
+        calls = roundtrip_calls(torch, [tx], [rx], b1) + \
+            roundtrip_calls(torch, [tx], [rx], b2)
+        res[mode] = (run_chain(torch, calls, mode),
+                     states([tx], [0x5151]), states([rx], [0x5151]))
+        tx.close()
+        rx.close()
+    same(res["sync"][0], res["async"][0])
+    assert res["sync"][1:] == res["async"][1:]
+    out = res["async"][0]
+    assert not out[1][3].any() and not out[3][3].any()
+
+
+@pytest.mark.parametrize("suite", [1])
+def test_async_gated_by_host_completion(suite, torch_cuda):
+    """the first call's plan is rejected (reordered packets: completed on
+    the host when waited for); the unprotect queued behind it reads that
+    arena, so it is gated and re-run: still == sync"""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    key = keys_for(suite, 1)[0]
+    seqs = list(range(100, 1100))
+    seqs[500], seqs[501] = seqs[501], seqs[500]
+    pk = seq_batch(rng, seqs)
+    res = {}
+    for mode in ("sync", "async"):
+        tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
+        r0 = P.counter("rejects")
+        calls = roundtrip_calls(torch, [tx], [rx], pk)
+        res[mode] = (run_chain(torch, calls, mode),
+                     states([tx], [0x5151]), states([rx], [0x5151]))
+        assert P.counter("rejects") > r0
+        tx.close()
+        rx.close()
+    same(res["sync"][0], res["async"][0])
+    assert res["sync"][1:] == res["async"][1:]
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_async_multi_session_chain(suite, torch_cuda):
+    """two protect/unprotect rounds over 40 resident sessions queued back
+    to back (round 2 planned against round 1's device-resident states); a
+    forged packet in round 1's unprotect makes the host fold it and gates
+    round 2's unprotect"""
+    torch = torch_cuda
+    rng = np.random.default_rng(5 + suite)
+    nsess = 40
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    r1 = multi_session_traffic(rng, 2000, nsess, s0=65300)
+    last = {s: int.from_bytes(p[2:4], "big") for s, p in r1}
+    r2 = next_batch(rng, last, 2000, nsess)
+    res = {}
+    for mode in ("sync", "async"):
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        calls = []
+        for rb in (r1, r2):
+            arena, pos, end, cap, s = to_arena(rb)
+            d = Dev(torch, arena, pos, end, cap, s)
+            calls.append(("srtp_encrypt", tx, d))
+        outs = run_chain(torch, calls, mode)
+        dec = []
+        for bi, (rb, o) in enumerate(zip((r1, r2), outs)):
+            prot = [(s, o[0][o[1][i]:o[2][i]].tobytes())
+                    for i, (s, _) in enumerate(rb)]
+            if bi == 0:
+                q = bytearray(prot[333][1])
+                q[-4] ^= 0x20
+                prot[333] = (prot[333][0], bytes(q))
+            arena, pos, end, cap, s = to_arena(prot)
+            dec.append(("srtp_decrypt", rx, Dev(torch, arena, pos, end,
+                                                cap, s)))
+        douts = run_chain(torch, dec, mode)
+        res[mode] = (outs + douts, states(tx, ssrcs), states(rx, ssrcs))
+        for c in tx + rx:
+            c.close()
+    same(res["sync"][0], res["async"][0])
+    assert res["sync"][1:] == res["async"][1:]
+    assert int(res["async"][0][2][3][333]) == P.EAUTH
+
+
+def test_async_then_sync_calls_drain(torch_cuda):
+    """a synchronous call (and export) on the issuing thread completes the
+    pending tickets first; a ticket waited later still returns its result"""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    key = keys_for(1, 1)[0]
+    pk = seq_batch(rng, range(7, 1007))
+    tx = P.Srtp(1, key)
+    arena, pos, end, cap, _ = to_arena(pk)
+    d = Dev(torch, arena, pos, end, cap, None)
+    rc, t, keep = P.device_batch_dev_async("srtp_encrypt", [tx], *d.args())
+    assert rc == 0
+    e, st = tx.export(0x5151)          # drains the ticket
+    assert e == 0 and st.s_l == 1006
+    assert P.batch_wait(t) == 0
+    assert not d.out()[3].any()
+    tx.close()

@@ -161,6 +161,15 @@ def main():
                          "batch (a fraction if < 1) between protect and "
                          "unprotect, spread evenly (EAUTH expected for "
                          "exactly those)")
+    ap.add_argument("--ssrcs", type=int, default=1,
+                    help="one session, packets interleaved over this many "
+                         "SSRCs (packet i -> stream i mod K, per-stream seq "
+                         "from 65000): the per-stream device planner")
+    ap.add_argument("--fresh-streams", action="store_true",
+                    help="--ssrcs: the session's streams are created by the "
+                         "timed batch (default: announced before it, like "
+                         "SDP a=ssrc, by srtp_stream_import of a fresh "
+                         "stream state)")
     ap.add_argument("--sq-json", default=None,
                     help="SQ-counter summary to attach as int_frac/lds_frac "
                          "(scripts/pmc_sq_summary.py --json)")
@@ -213,12 +222,18 @@ def main():
         s0 = S.shard_seq0(rank, n, 65000)   # this shard's first seq
     lengths = cfg["length"] if cfg["length"] else W.mixed_lengths(n)
     sess = W.random_sessions(n, nsess) if nsess > 1 else None
+    K = max(1, args.ssrcs)
+    if K > 1:
+        assert nsess == 1 and cfg_id in (2, 3) and not args.rtcp, \
+            "--ssrcs: configs 2 and 3"
+        cfg["name"] += " x %d SSRCs" % K
     if args.rtcp:
         assert nsess == 1 and cfg["length"], "--rtcp: configs 2 and 3"
         arena_h, pos, end, cap = W.make_rtcp_arena(n, lengths)
     else:
-        arena_h, pos, end, cap = W.make_arena(n, lengths, s0=s0 & 0xffff,
-                                              sess=sess)
+        arena_h, pos, end, cap = W.make_arena(
+            n, lengths, s0=s0 & 0xffff,
+            sess=sess if K == 1 else np.arange(n, dtype=np.uint32) % K)
     OPS = ("srtcp_encrypt", "srtcp_decrypt") if args.rtcp else \
         ("srtp_encrypt", "srtp_decrypt")
     log("workload built (%d packets)" % n)
@@ -245,6 +260,12 @@ def main():
                 rank, n, 65000, W.SSRC_BASE, False, P.StreamState)) == 0
             assert rx[0].import_(S.shard_state(
                 rank, n, 65000, W.SSRC_BASE, True, P.StreamState)) == 0
+        if K > 1 and not args.fresh_streams:
+            for s in tx + rx:
+                for k in range(K):
+                    st = P.StreamState()
+                    st.ssrc = W.SSRC_BASE + k
+                    assert s.import_(st) == 0
         return tx, rx
 
     # per-call descriptor arrays (the API updates pos/end in place).
@@ -511,7 +532,9 @@ def main():
         "config": {"workload": "config%d: %s" % (cfg_id, cfg["name"]),
                    "packets_per_gpu": n, "pkt_len": cfg["length"] or
                    "200/1400", "suite": P.suite_name(suite),
-                   "sessions": nsess, "parallelism": "shard%d" % world,
+                   "sessions": nsess, "ssrcs_per_session": K,
+                   "streams_announced": K > 1 and not args.fresh_streams,
+                   "parallelism": "shard%d" % world,
                    "api": ("srtp_*_batch_dev_async" if use_async else
                            "srtp_*_batch_dev") if use_dev else
                    "srtp_*_batch"},
@@ -521,6 +544,8 @@ def main():
         "forged_per_batch": nforge,
         "folds": {"device": P.counter("devfolds"),
                   "host": P.counter("folds")},
+        "plans": {"rejected": P.counter("rejects"),
+                  "per_stream": P.counter("splans")},
         "verified_roundtrip": verified,
         "roofline": roof,
     }

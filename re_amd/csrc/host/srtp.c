@@ -104,6 +104,8 @@ static struct {
 	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
 	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
 				   device-planned single-key batches */
+	int splan;              /* srtp_gpu_tune splan: single-session RTP
+				   batches through the per-stream planner */
 	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
 				   device-planned batch fold on the host */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
@@ -142,6 +144,7 @@ static uint64_t g_cnt_misses;   /* MAC/tag speculation misses */
 static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
+static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
 
 static void count(uint64_t *c, uint64_t v)
 {
@@ -160,6 +163,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_rejects, __ATOMIC_RELAXED);
 	if (!strcmp(name, "devfolds"))
 		return __atomic_load_n(&g_cnt_devfolds, __ATOMIC_RELAXED);
+	if (!strcmp(name, "splans"))
+		return __atomic_load_n(&g_cnt_splans, __ATOMIC_RELAXED);
 	return 0;
 }
 
@@ -178,6 +183,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nolean = value > 0;
 	else if (!strcmp(name, "nodevfold"))
 		g_env.nodevfold = value > 0;
+	else if (!strcmp(name, "splan"))
+		g_env.splan = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -2144,12 +2151,12 @@ static size_t fast_chunk(void)
 /* replay state after the planned batch: the last <= 65 indices suffice
  * (every index is new and increasing, so older bits have shifted out) */
 static struct replay plan_replay(const struct replay *r0,
-				 const struct sgpu_plan_out *o, size_t n)
+				 const uint64_t *tail_ix, size_t n)
 {
 	struct replay r = *r0;
 	size_t k, m = n < SGPU_PLAN_TAIL ? n : SGPU_PLAN_TAIL;
 	if (n > SGPU_PLAN_TAIL) {
-		r.lix = o->tail_ix[0];
+		r.lix = tail_ix[0];
 		r.bitmap = 1;
 		k = 1;
 	}
@@ -2157,7 +2164,7 @@ static struct replay plan_replay(const struct replay *r0,
 		k = 0;
 	}
 	for (; k < m; k++)
-		(void)replay_check(&r, o->tail_ix[k]);
+		(void)replay_check(&r, tail_ix[k]);
 	return r;
 }
 
@@ -2198,7 +2205,7 @@ static void plan_apply(struct srtp *s, const struct sgpu_plan_out *po,
 	st->roc += po->wraps;
 	st->s_l = (uint16_t)po->s_l_last;
 	if (!prot)
-		st->replay_rtp = plan_replay(&st->replay_rtp, po, n);
+		st->replay_rtp = plan_replay(&st->replay_rtp, po->tail_ix, n);
 }
 
 static void plan_unapply(struct srtp *s, unsigned nstreams0,
@@ -3053,6 +3060,8 @@ struct dcall {
 	uint32_t nup;           /* many sessions: states uploaded */
 	uint64_t pend, done;    /* async: sequence numbers (mpg) */
 	double t[3];
+	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
+	struct sgpu_splan_in sin; /* several streams: the plan input */
 };
 
 /* single-stream RTP batch planned and processed on the device: the
@@ -3171,6 +3180,7 @@ static int dev_planned_finish(struct dcall *k)
 	int err = 0;
 
 	nfail = *(const uint32_t *)(po + 1);
+	k->pfail = po->fail;
 	if (po->fail) {
 		if (po->fail & SPF_PRED)
 			return -2;
@@ -3233,8 +3243,10 @@ static int dev_planned_finish(struct dcall *k)
 	return -1;
 }
 
-/* synchronous: -1 not plannable (nothing modified), else 0 / errno */
-static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
+/* synchronous: -1 not plannable (nothing modified; *pfail: why, 0 for a
+ * forged packet the host must fold), else 0 / errno */
+static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
+		       uint32_t *pfail)
 {
 	struct dcall k;
 	int err;
@@ -3251,7 +3263,212 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_stream_sync(d->stream);
 	if (err)
 		return err;
-	return dev_planned_finish(&k);
+	err = dev_planned_finish(&k);
+	*pfail = k.pfail;
+	return err;
+}
+
+/* ---- one session, several streams (plan_streams.hip) ------------------ */
+
+static void splan_in(struct sgpu_splan_in *in, const struct srtp *s,
+		     uint32_t n, int prot, uint32_t T, uint32_t need)
+{
+	unsigned k;
+	memset(in, 0, sizeof(*in));
+	in->n = n;
+	in->prot = (uint32_t)prot;
+	in->tag = T;
+	in->need = need;
+	in->maxlen = SGPU_CACHED_MAX(s->rtp.mode);
+	in->nst = s->nstreams;
+	for (k = 0; k < s->nstreams; k++) {
+		const struct srtp_stream *x = &s->streams[k];
+		in->st[k].ssrc = x->ssrc;
+		in->st[k].roc = x->roc;
+		in->st[k].s_l = x->s_l;
+		in->st[k].flags = SST_EXISTS | (x->s_l_set ? SST_SL_SET : 0);
+		in->st[k].lix = x->replay_rtp.lix;
+		in->st[k].bitmap = x->replay_rtp.bitmap;
+	}
+}
+
+/* stream states after an accepted plan: streams with packets in the batch
+ * advance, new SSRCs are appended in first-appearance order (stream_new,
+ * stream.c:45-67) */
+static void splan_apply(struct srtp *s, const struct sgpu_splan_out *po,
+			int prot)
+{
+	unsigned k;
+	for (k = 0; k < po->nst && k < SRTP_MAX_STREAMS; k++) {
+		struct srtp_stream *x = &s->streams[k];
+		if (!po->cnt[k])
+			continue;
+		if (k >= s->nstreams) {
+			memset(x, 0, sizeof(*x));
+			x->ssrc = po->ssrc[k];
+		}
+		x->s_l_set = 1;
+		x->roc += po->wraps[k];
+		x->s_l = (uint16_t)po->s_l_last[k];
+		if (!prot)
+			x->replay_rtp = plan_replay(&x->replay_rtp, po->tail_ix[k],
+						    po->cnt[k]);
+	}
+	if (po->nst > s->nstreams)
+		s->nstreams = po->nst;
+}
+
+/* the launches (no host synchronisation) */
+static int dev_splanned_issue(struct dcall *k)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
+	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
+			      (T > 4 ? T : 4u)) : 0u;
+	const size_t scr = sgpu_splan_scratch((uint32_t)n);
+	struct sgpu_splan_out *po, *po_d;
+	struct sgpu_hdr *hd_d;
+	uint64_t *desc_d;
+	uint32_t *es_d, *save_d, *nfail_d;
+	uint8_t *vd_d;
+	void *stream = d->stream;
+	int err;
+
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 12);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, sizeof(struct sgpu_splan_out) + 64);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = pool_reserve(w, &w->mscr, scr);
+	if (err)
+		return err;
+	hd_d = (struct sgpu_hdr *)w->hd.d;
+	desc_d = (uint64_t *)w->dsc.d;
+	nfail_d = (uint32_t *)w->vs.d;
+	save_d = (uint32_t *)(w->vs.d + 64);
+	vd_d = w->vs.d + 64 + n * 4;
+	po = (struct sgpu_splan_out *)w->pl.h;
+	po_d = (struct sgpu_splan_out *)w->pl.d;
+	es_d = (uint32_t *)w->es.d;
+
+	splan_in(&k->sin, s, (uint32_t)n, prot, T, need);
+	{
+		struct sgpu_prologue pro = {
+			es_d, nfail_d, (uint32_t *)po_d, 1,
+			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d,
+			c0->dev};
+		k->sin.zeroed = 1;
+		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
+					  d->end, hd_d, NULL, (uint32_t)n, 0,
+					  &pro, stream);
+	}
+	if (!err && k->pred)
+		err = sgpu_gate_pred(k->pred, &po_d->base.fail, stream);
+	if (!err)
+		err = sgpu_splan_rtp(&k->sin, hd_d, d->pos, es_d, d->cap,
+				     d->arena_size, desc_d, w->mscr.d, scr, po_d,
+				     stream);
+	if (!err) {
+		struct sgpu_compact C = {
+			d->pos, es_d, hd_d, desc_d, NULL,
+			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
+			save_d, nfail_d, 0, 1, NULL, 0, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  &po_d->base, prot, stream);
+	}
+	if (!err)
+		err = sgpu_plan_results(&po_d->base.fail, es_d, d->end, d->err,
+					(uint32_t)n,
+					prot ? (int32_t)T : -(int32_t)T, stream);
+	if (!err && k->gate)
+		err = sgpu_gate_set(&po_d->base.fail, nfail_d, k->gate, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)   /* pinned, next to the plan (see dev_planned_issue) */
+		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
+	return err;
+}
+
+/* ... after its launches completed: 0 / errno, -1 not plannable or a
+ * forged packet (undone on the device; the host folds), -2 gated by the
+ * chained call before (nothing modified) */
+static int dev_splanned_finish(struct dcall *k)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const struct sgpu_splan_out *po = (const struct sgpu_splan_out *)w->pl.h;
+	struct sgpu_splan_out *po_d = (struct sgpu_splan_out *)w->pl.d;
+	const uint32_t nfail = *(const uint32_t *)(po + 1);
+	int err;
+
+	k->pfail = po->base.fail;
+	if (po->base.fail) {
+		if (po->base.fail & SPF_PRED)
+			return -2;
+		count(&g_cnt_rejects, 1);
+		return -1;
+	}
+	count(&g_cnt_splans, 1);
+	if (!nfail) {
+		splan_apply(s, po, prot);
+		return 0;
+	}
+	count(&g_cnt_misses, nfail);
+	count(&g_cnt_folds, 1);
+	/* a forged packet: undo on the device, fold on the host engine */
+	{
+		struct sgpu_compact C = {
+			d->pos, (uint32_t *)w->es.d, (struct sgpu_hdr *)w->hd.d,
+			(uint64_t *)w->dsc.d, NULL, (const uint32_t *)w->cm.d,
+			NULL, 0, (uint32_t)n, w->vs.d + 64 + n * 4,
+			(uint32_t *)(w->vs.d + 64), (uint32_t *)w->vs.d, 1, 1,
+			NULL, 0, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0, &po_d->base,
+				  prot, d->stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, w->es.d, n * 4, d->stream);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	return err ? err : -1;
+}
+
+/* synchronous: -1 not plannable or folded on the host (nothing
+ * modified), else 0 / errno */
+static int dev_splanned(int op, struct srtp *s, struct srtp_batch_dev *d)
+{
+	struct dcall k;
+	int err;
+	memset(&k, 0, sizeof(k));
+	k.op = op;
+	k.sessv = &s;
+	k.nsess = 1;
+	k.d = *d;
+	k.w = ws_get();
+	if (!k.w)
+		return ENOMEM;
+	err = dev_splanned_issue(&k);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	if (err)
+		return err;
+	return dev_splanned_finish(&k);
 }
 
 /*
@@ -3371,7 +3588,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 			(s->streams[0].rtcp_index + (uint32_t)n) & 0x7fffffffu;
 	else if (c0->has_hmac)
 		s->streams[0].replay_rtcp =
-			plan_replay(&s->streams[0].replay_rtcp, po, n);
+			plan_replay(&s->streams[0].replay_rtcp, po->tail_ix, n);
 	if (!nfail)
 		return 0;
 	count(&g_cnt_misses, nfail);
@@ -3630,7 +3847,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 #define TK_MAX   4              /* pending calls per thread */
 #define TK_GATES 64             /* per-thread gate words (a ring > TK_MAX) */
 
-enum { TK_PLANNED = 1, TK_MPLANNED = 2, TK_DONE = 3 };
+enum { TK_PLANNED = 1, TK_MPLANNED = 2, TK_SPLANNED = 3, TK_DONE = 4 };
 
 struct srtp_batch_ticket {
 	struct srtp_batch_ticket *next;
@@ -3665,8 +3882,9 @@ static void tk_finish_one(void)
 
 	r = sgpu_event_sync(t->ev);
 	if (!r)
-		r = t->kind == TK_PLANNED ? dev_planned_finish(k)
-					  : dev_mplanned_finish(k);
+		r = t->kind == TK_PLANNED ? dev_planned_finish(k) :
+		    t->kind == TK_SPLANNED ? dev_splanned_finish(k)
+					   : dev_mplanned_finish(k);
 	t_tk_head = t->next;
 	if (!t_tk_head)
 		t_tk_tail = NULL;
@@ -3682,7 +3900,12 @@ static void tk_finish_one(void)
 	}
 	else if (r == -1) {
 		r = sess_host(k->sessv, k->nsess);
-		if (!r)
+		/* a second SSRC in a single-stream plan: the per-stream one */
+		if (!r && t->kind == TK_PLANNED && (k->pfail & SPF_SSRC))
+			r = dev_splanned(k->op, k->sessv[0], &k->d);
+		else if (!r)
+			r = -1;
+		if (r == -1)
 			r = dev_staged(k->op, k->sessv, k->nsess, &k->d);
 	}
 	t->result = r;
@@ -3758,8 +3981,10 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 		table_rdlock();
 		err = sess_host(&s, 1);
 		table_unlock();
-		if (err || s->nstreams > 1)
+		if (err)
 			kind = 0;
+		else if (s->nstreams > 1 || g_env.splan)
+			kind = TK_SPLANNED;
 	}
 	if (!kind) {
 		tk_drain();
@@ -3789,8 +4014,9 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 	table_rdlock();         /* until the call completes (tk_finish_one) */
 	err = t->ev ? 0 : ENOMEM;
 	if (!err)
-		err = kind == TK_PLANNED ? dev_planned_issue(k)
-					 : dev_mplanned_issue(k);
+		err = kind == TK_PLANNED ? dev_planned_issue(k) :
+		      kind == TK_SPLANNED ? dev_splanned_issue(k)
+					  : dev_mplanned_issue(k);
 	if (!err)
 		err = sgpu_event_record(t->ev, d->stream);
 	if (err) {
@@ -3814,7 +4040,7 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 	}
 	t_tk_seq = t->seq;
 	t->kind = kind;
-	if (kind == TK_PLANNED)
+	if (kind == TK_PLANNED || kind == TK_SPLANNED)
 		sessv[0]->pend_p = t->seq;
 	if (t_tk_tail)
 		t_tk_tail->next = t;
@@ -3939,9 +4165,16 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 			return err;
 	}
 	if ((op == OP_RTP_ENC || op == OP_RTP_DEC) && nsess == 1 &&
-	    !d->sess && sessv[0]->nstreams <= 1 &&
-	    !g_env.noplan && !g_env.general) {
-		int r = dev_planned(op, sessv[0], d);
+	    !d->sess && !g_env.noplan && !g_env.general) {
+		/* one stream: the single-stream planner (with the device verdict
+		 * fold); several SSRCs (or a plan rejected for a second one):
+		 * the per-stream planner */
+		uint32_t pf = SPF_SSRC;
+		int r = -1;
+		if (sessv[0]->nstreams <= 1 && !g_env.splan)
+			r = dev_planned(op, sessv[0], d, &pf);
+		if (r == -1 && (pf & SPF_SSRC))
+			r = dev_splanned(op, sessv[0], d);
 		if (r >= 0)
 			return r;
 	}

@@ -287,6 +287,49 @@ struct sgpu_sstate {            /* 32 bytes */
 	uint64_t bitmap;
 };
 
+/*
+ * Device planning of a single-session RTP batch over up to SGPU_SP_MAX
+ * streams (SRTP_MAX_STREAMS SSRCs of one struct srtp, plan_streams.hip):
+ * the speculation of sgpu_plan_rtp per stream, new SSRCs appended in
+ * first-appearance order.  in->st[k] (k < nst): the session's streams in
+ * table order (SST_EXISTS, SST_SL_SET, RTP replay).  Per stream k of
+ * out->ssrc[0..nst): wraps, packets (cnt), final s_l (if cnt) and the
+ * indices of its last min(cnt, 65) packets; out->base.fail / skip[] as in
+ * sgpu_plan_out (nst > SGPU_SP_MAX: SPF_SSRC).
+ */
+#define SGPU_SP_MAX 8
+struct sgpu_splan_in {
+	uint32_t n;
+	uint32_t prot;
+	uint32_t tag;
+	uint32_t need;
+	uint32_t maxlen;
+	uint32_t zeroed;        /* out already zeroed */
+	uint32_t nst;           /* streams before the batch */
+	uint32_t pad;
+	struct sgpu_sstate st[SGPU_SP_MAX];
+};
+struct sgpu_splan_out {
+	struct sgpu_plan_out base;      /* fail, hl0, skip[] */
+	uint32_t nst;                   /* streams after the batch */
+	uint32_t pad;
+	uint32_t ssrc[SGPU_SP_MAX];
+	uint32_t wraps[SGPU_SP_MAX];
+	uint32_t cnt[SGPU_SP_MAX];
+	uint32_t s_l_last[SGPU_SP_MAX];
+	int32_t last[SGPU_SP_MAX];      /* last packet index of the stream */
+	uint32_t pad2[2];
+	uint64_t tail_ix[SGPU_SP_MAX][SGPU_PLAN_TAIL];
+};
+size_t sgpu_splan_scratch(uint32_t n);
+int   sgpu_splan_rtp(const struct sgpu_splan_in *in,
+		     const struct sgpu_hdr *hdr, const uint32_t *pos,
+		     const uint32_t *end, const uint32_t *cap,
+		     uint64_t arena_size, uint64_t *desc, void *scratch,
+		     size_t scratch_bytes, struct sgpu_splan_out *out,
+		     void *stream);
+
+
 struct sgpu_mplan_in {
 	uint32_t n;
 	uint32_t nsess;

@@ -1,12 +1,23 @@
 #!/bin/bash
-# Round-end measurement set: parity tests, smoke, and the bench lines
-# committed under profiles/ (configs 2/3/4, host-array API, end-to-end).
+# Round-end measurement set: the bench lines committed under profiles/
+# (configs 2/3/4, SRTCP, host-array API, end-to-end, socket to socket,
+# adversarial receive, several SSRCs).  Every GPU step under its own
+# time limit; the first failure ends the script.
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit $?
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || exit $?
-timeout -k 10 300 python bench.py --config 3 > gpurun_out/b_c3.json 2> gpurun_out/b_c3.err || exit $?
-timeout -k 10 300 python bench.py --config 4 > gpurun_out/b_c4.json 2> gpurun_out/b_c4.err || exit $?
-timeout -k 10 300 python bench.py --host-arrays --no-cpu-baseline > gpurun_out/b_c2_host.json 2> gpurun_out/b_c2_host.err || exit $?
-timeout -k 10 300 python bench.py --e2e --no-cpu-baseline > gpurun_out/b_c2_e2e.json 2> gpurun_out/b_c2_e2e.err || exit $?
+O=gpurun_out/round
+mkdir -p $O
+b() {   # name, bench args...
+  local n=$1; shift
+  timeout -k 10 300 python bench.py "$@" > $O/$n.json 2> $O/$n.err || exit $?
+}
+b c2
+b c3 --config 3
+b c4 --config 4
+b c2_rtcp --rtcp --no-cpu-baseline
+b c3_rtcp --config 3 --rtcp --no-cpu-baseline
+b c2_host --host-arrays --no-cpu-baseline
+b c2_sync --sync --no-cpu-baseline
+b c2_e2e --e2e --no-cpu-baseline
+b c2_udp --udp
+b c2_forge1 --forge 1 --no-cpu-baseline
+b c2_ssrc2 --ssrcs 2 --no-cpu-baseline

@@ -4,6 +4,8 @@
 // SRTP packet), without / with the packet memory traffic:
 //   aes   : keystream only           sha   : SHA-1 only
 //   both  : keystream + SHA-1         mem   : both + 64-B load/store/chunk
+//   wave-per-packet: one packet per wavefront (k_wave), the alternative
+//                    layout north_star names, for comparison
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -Ire_amd/csrc -Iinclude \
 //         scripts/ubench_ctr.hip -o /tmp/ubc && /tmp/ubc
 #include "hip/kern_common.h"
@@ -143,6 +145,85 @@ __global__ void __launch_bounds__(BLK) k_ub(const uint32_t *T0g,
 	out[t] = acc ^ h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
 }
 
+/*
+ * The north_star's literal layout: one packet per wavefront.  Lane l
+ * computes the keystream of 64-byte chunk l (lanes 0..18 of a 1200-B
+ * packet; the rest idle) and moves that chunk (coalesced across the wave);
+ * then the HMAC's SHA-1 chain runs chunk by chunk with the 16 message
+ * words broadcast from the owning lane by wavefront shuffles -- every lane
+ * computes the same 80 dependent rounds.  SHA1_ONLY: no keystream.
+ */
+template <bool SHA1_ONLY>
+__global__ void __launch_bounds__(BLK) k_wave(const uint32_t *T0g,
+					     const uint32_t *rkg,
+					     uint8_t *arena, uint32_t *out)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	tt4_fill(smem, T0g);
+	__syncthreads();
+	const uint32_t L = threadIdx.x & 63u;
+	const uint32_t p = (blockIdx.x * BLK + threadIdx.x) >> 6;  /* packet */
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	uint32_t rk[44];
+#pragma unroll
+	for (int k = 0; k < 44; k++)
+		rk[k] = __builtin_amdgcn_readfirstlane(rkg[k]);
+	uint8_t *pkt = arena + (size_t)p * 1216;
+	uint32_t d[16];
+	if (L < NCH) {
+#pragma unroll
+		for (int g = 0; g < 4; g++) {
+			const uint4 v = *(const uint4 *)(pkt + 64 * L + 16 * g);
+			d[4 * g] = v.x; d[4 * g + 1] = v.y;
+			d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+		}
+		if (!SHA1_ONLY) {
+			uint32_t iv[4] = {p * 0x9e3779b9u, p ^ 0x12345678u, p * 7u, 0};
+			CtrKs<10, true, true> C;
+			C.init(smem, lo, rk, iv);
+			uint32_t carry[4] = {0, 0, 0, 0}, ks[16];
+			chunk_ks<10, 3>(smem, lo, rk, C, 4 * L, carry, ks);
+#pragma unroll
+			for (int q = 0; q < 16; q++)
+				d[q] ^= ks[q];
+		}
+#pragma unroll
+		for (int g = 0; g < 4; g++)
+			*(uint4 *)(pkt + 64 * L + 16 * g) =
+				make_uint4(d[4 * g], d[4 * g + 1], d[4 * g + 2],
+					   d[4 * g + 3]);
+	}
+	uint32_t h[5] = {p, 1, 2, 3, 4};
+	for (int k = 0; k < NCH; k++) {
+		uint32_t w[16];
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			w[q] = bswap32((uint32_t)__shfl((int)d[q], k));
+		sha1_compress(h, w);
+	}
+	if (L == 0)
+		out[p] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+}
+
+template <bool SHA1_ONLY>
+static float run_wave(const uint32_t *T0, const uint32_t *rk, uint8_t *arena,
+		      uint32_t *out, int n)
+{
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	const int nb = n / (BLK / 64);
+	k_wave<SHA1_ONLY><<<nb, BLK>>>(T0, rk, arena, out);
+	hipEventRecord(a);
+	for (int i = 0; i < 2; i++)
+		k_wave<SHA1_ONLY><<<nb, BLK>>>(T0, rk, arena, out);
+	hipEventRecord(b);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	return ms / 2;
+}
+
 static uint32_t sbox(int x)
 {
 	/* AES S-box by inversion + affine map (FIPS-197 5.1.1) */
@@ -210,5 +291,9 @@ int main()
 	printf("s16 addr %.3f ms\n", run<B | M_S16>(T0d, rkd, arena, out, n));
 	printf("quad+xpose %.3f ms\n", run<B | M_QUAD | M_XPQ>(T0d, rkd, arena, out, n));
 	printf("s16+xpose %.3f ms\n", run<B | M_S16 | M_XP16>(T0d, rkd, arena, out, n));
+	printf("wave-per-packet sha %.3f ms\n", run_wave<true>(T0d, rkd, arena,
+								   out, n));
+	printf("wave-per-packet aes+sha+mem %.3f ms\n",
+	       run_wave<false>(T0d, rkd, arena, out, n));
 	return 0;
 }

@@ -583,14 +583,19 @@ __device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
 	uint8_t *pkt = arena + j.off;
 	const uint64_t pasz = asz - j.off;
 	const uint32_t A = j.a_len;
-	const uint32_t c_off = j.c_off, c_len = j.c_len;
+	/* SRTCP: E || index closes the AAD (srtcp.c:82-102, 239-262); an
+	 * unencrypted SRTCP packet has no cipher region */
+	const bool trail = (j.flags & SJ_TRAILER) != 0;
+	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
+	const uint32_t aad_total = A + (trail ? 4u : 0u);
+	const uint32_t c_off = j.c_off, c_len = do_cipher ? j.c_len : 0u;
 	const uint32_t c_end = c_off + c_len;
 	const uint32_t t = c_off >> 4;
 	const uint32_t nfull = c_len / 16u;
 	uint32_t X[4] = {0, 0, 0, 0};
-	for (uint32_t p = 0; p < A; p += 16) {
+	for (uint32_t p = 0; p < aad_total; p += 16) {
 		uint32_t w[4];
-		aad_block(pkt, pasz, p, A, false, 0u, w);
+		aad_block(pkt, pasz, p, A, trail, j.trailer, w);
 		X[0] ^= w[0]; X[1] ^= w[1]; X[2] ^= w[2]; X[3] ^= w[3];
 		ghash8_mul(X, smem, hi16);
 	}
@@ -765,7 +770,8 @@ __device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
 
 	/* length block: bitlen(AAD) || bitlen(C) */
 	{
-		const uint64_t al = (uint64_t)A * 8u, cl = (uint64_t)c_len * 8u;
+		const uint64_t al = (uint64_t)aad_total * 8u;
+		const uint64_t cl = (uint64_t)c_len * 8u;
 		X[0] ^= (uint32_t)(al >> 32); X[1] ^= (uint32_t)al;
 		X[2] ^= (uint32_t)(cl >> 32); X[3] ^= (uint32_t)cl;
 		ghash8_mul(X, smem, hi16);
@@ -776,11 +782,13 @@ __device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
 	const uint32_t tg[4] = {X[0] ^ bswap32(e0[0]), X[1] ^ bswap32(e0[1]),
 				X[2] ^ bswap32(e0[2]), X[3] ^ bswap32(e0[3])};
 	uint8_t *tp = pkt + j.tag_off;
-	uint8_t vd = SV_CIPHERED;
+	uint8_t vd = do_cipher ? SV_CIPHERED : 0;
 	if (PROT) {
 #pragma unroll
 		for (int q = 0; q < 4; q++)
 			st_be32(tp + 4 * q, tg[q]);
+		if (j.flags & SJ_STORE_TRAIL)
+			st_be32(pkt + j.t_off, j.trailer);
 	}
 	else {
 		uint32_t diff = 0;

@@ -151,6 +151,9 @@ def main():
                          "asynchronous srtp_*_batch_dev_async + "
                          "srtp_batch_wait pair (protect and unprotect "
                          "queued back to back on the stream)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="asynchronous pairs: wait for each step before "
+                         "issuing the next (default: two steps in flight)")
     ap.add_argument("--host-arrays", action="store_true",
                     help="srtp_*_batch with host pos/end/err arrays instead "
                          "of the device-resident srtp_*_batch_dev")
@@ -274,6 +277,7 @@ def main():
     use_dev = not args.host_arrays
     # asynchronous pair (srtp_*_batch_dev_async) for the RTP device path
     use_async = use_dev and not args.sync and not args.e2e and not args.rtcp
+    pipelined = use_async and not args.no_pipeline and not args.forge
     sess_d = None
     if use_dev:
         i32 = lambda a: torch.from_numpy(
@@ -284,7 +288,7 @@ def main():
         p_d, e_d = torch.empty_like(pos_d), torch.empty_like(end_d)
         # per-step result arrays: the API fills them inside the timed
         # region; the bench tallies them after it (verification, not path)
-        errbuf = torch.zeros((2, max(1, args.steps), n), dtype=torch.int32,
+        errbuf = torch.zeros((2, max(1, args.steps, args.warmup), n), dtype=torch.int32,
                              device=dev)
     else:
         p, e = np.empty_like(pos), np.empty_like(end)
@@ -338,7 +342,7 @@ def main():
         forge_idx = torch.from_numpy(pos[forge_pk].astype(np.int64) +
                                      12 + 20).to(dev)
 
-    def step(tx, rx, k=0):
+    def step(tx, rx, k=0, inflight=None):
         if use_dev:
             err_ed, err_dd = errbuf[0, k], errbuf[1, k]
         if args.e2e:
@@ -367,6 +371,9 @@ def main():
                 else:
                     rc = P.device_batch_dev(*a)
                 assert rc == 0, (rc, P.lib().srtp_gpu_error())
+            if inflight is not None:
+                inflight.extend(pend)   # the caller waits, a step later
+                return 0
             for t, _ in pend:
                 rc = P.batch_wait(t)
                 assert rc == 0, (rc, P.lib().srtp_gpu_error())
@@ -381,13 +388,37 @@ def main():
         assert rc == 0, (rc, P.lib().srtp_gpu_error())
         return np.count_nonzero(err_e) + np.count_nonzero(err_d)
 
+    def run_steps(sets, k0=0):
+        """one step per session set; asynchronous pairs run two steps in
+        flight: step k's calls are issued (their host planning overlaps
+        step k-1 on the GPU, which shares the stream), then step k-1's are
+        waited for"""
+        errs = 0
+        inflight = [] if pipelined else None
+        for k, (tx, rx) in enumerate(sets):
+            mark = len(inflight) if inflight is not None else 0
+            errs += step(tx, rx, k0 + k, inflight)
+            if inflight is not None:
+                done, inflight[:] = inflight[:mark], inflight[mark:]
+                for t, _ in done:
+                    rc = P.batch_wait(t)
+                    assert rc == 0, (rc, P.lib().srtp_gpu_error())
+        for t, _ in inflight or []:
+            rc = P.batch_wait(t)
+            assert rc == 0, (rc, P.lib().srtp_gpu_error())
+        return errs
+
     log("arena resident, warmup")
-    # ---- warmup (untimed) ----
-    for _ in range(args.warmup):
-        tx, rx = make_sessions()
-        step(tx, rx)
-        for s in tx + rx:
-            s.close()
+    # ---- warmup (untimed; as many steps in flight as the timed loop, so
+    # the library's per-call workspaces exist before timing) ----
+    if args.warmup:
+        warm = [make_sessions() for _ in range(args.warmup)]
+        run_steps([(P.session_array(tx), P.session_array(rx))
+                   for tx, rx in warm])
+        torch.cuda.synchronize()
+        for tx, rx in warm:
+            for s in tx + rx:
+                s.close()
     torch.cuda.synchronize()
     # the C session pointer arrays are built once per set (not timed);
     # the Srtp handles stay alive until the end (they own the sessions)
@@ -403,9 +434,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    errors = 0
-    for k in range(args.steps):
-        errors += step(*sess_sets[k], k)
+    errors = run_steps(sess_sets)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -534,6 +563,7 @@ def main():
                    "200/1400", "suite": P.suite_name(suite),
                    "sessions": nsess, "ssrcs_per_session": K,
                    "streams_announced": K > 1 and not args.fresh_streams,
+                   "steps_in_flight": 2 if pipelined else 1,
                    "parallelism": "shard%d" % world,
                    "api": ("srtp_*_batch_dev_async" if use_async else
                            "srtp_*_batch_dev") if use_dev else

@@ -24,7 +24,7 @@ kfn_t sgpu_pick_ctr10_fast(int prot, int refix)
 	return prot ? k_ctr_fast_any<10, true> : k_ctr_fast_any<10, false>;
 }
 
-unsigned sgpu_ctr_fast_block(void)
+unsigned sgpu_ctr_fast_block(int prot)
 {
-	return CTRF_BLOCK;
+	return CTRF_BLK(prot);
 }

@@ -25,6 +25,10 @@
 #ifndef CTRF_BLOCK
 #define CTRF_BLOCK 1024
 #endif
+#ifndef CTRF_BLOCK_U        /* unprotect block (its register budget) */
+#define CTRF_BLOCK_U CTRF_BLOCK
+#endif
+#define CTRF_BLK(PROT) ((PROT) ? CTRF_BLOCK : CTRF_BLOCK_U)
 #ifndef CTRF_COAL_P         /* quad-coalesced steady chunks, protect */
 #define CTRF_COAL_P 1
 #endif
@@ -506,8 +510,8 @@ __device__ __forceinline__ int fast_class(const KArgs &a)
 
 template <int NR, bool PROT>
 __global__ void
-__attribute__((amdgpu_flat_work_group_size(1, CTRF_BLOCK)))
-__attribute__((amdgpu_waves_per_eu(CTRF_BLOCK / 256, 8)))
+__attribute__((amdgpu_flat_work_group_size(1, CTRF_BLK(PROT))))
+__attribute__((amdgpu_waves_per_eu(CTRF_BLK(PROT) / 256, 8)))
 k_ctr_fast_any(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];

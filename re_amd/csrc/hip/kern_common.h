@@ -698,5 +698,5 @@ kfn_t sgpu_pick_gcm(bool compact, bool uni, int nr, int prot);
 /* refix: 0 the kernel, 1 full-grid restore, 2 list restore (c.flist) */
 kfn_t sgpu_pick_ctr10_fast(int prot, int refix);
 kfn_t sgpu_pick_ctr14_fast(int prot, int refix);
-unsigned sgpu_ctr_fast_block(void);
+unsigned sgpu_ctr_fast_block(int prot);
 unsigned sgpu_gcm_block(bool uni);

@@ -292,10 +292,23 @@ __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 		out[i] = h;
 		return;
 	}
-	const uint32_t cc = b[0] & 0x0fu, x = (b[0] >> 4) & 1u;
-	h.seq = (uint16_t)(b[2] << 8 | b[3]);
-	h.ssrc = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 |
-		 (uint32_t)b[10] << 8 | b[11];
+	uint32_t b0;
+	if (!(p & 3u)) {
+		/* the batch APIs' 4-byte aligned windows: two dword loads
+		 * (words 0 and 2 of the header) instead of seven byte loads */
+		const uint32_t w0 = *(const uint32_t *)b;
+		const uint32_t w2 = *(const uint32_t *)(b + 8);
+		b0 = w0 & 0xffu;
+		h.seq = (uint16_t)((w0 >> 8 & 0xff00u) | (w0 >> 24));
+		h.ssrc = __builtin_bswap32(w2);
+	}
+	else {
+		b0 = b[0];
+		h.seq = (uint16_t)(b[2] << 8 | b[3]);
+		h.ssrc = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 |
+			 (uint32_t)b[10] << 8 | b[11];
+	}
+	const uint32_t cc = b0 & 0x0fu, x = (b0 >> 4) & 1u;
 	uint32_t hl = 12;
 	if (left - hl < 4 * cc) {
 		h.err_pos = (uint16_t)hl;
@@ -1030,7 +1043,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		kfn_t ff = nr == 10 ? sgpu_pick_ctr10_fast(prot, 0)
 				    : sgpu_pick_ctr14_fast(prot, 0);
 		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
-			       (hipStream_t)stream, sgpu_ctr_fast_block());
+			       (hipStream_t)stream, sgpu_ctr_fast_block(prot));
 		if (!e && !prot && c->flist) {
 			/* one workgroup per listed forged packet (grid-
 			 * strided past 1024); all exit at once if none */
@@ -1045,7 +1058,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 			e = launch(nr == 10 ? sgpu_pick_ctr10_fast(0, 1)
 					    : sgpu_pick_ctr14_fast(0, 1),
 				   a, c->n, -1, (hipStream_t)stream,
-				   sgpu_ctr_fast_block());
+				   sgpu_ctr_fast_block(1));
 		return e;
 	}
 	kfn_t f = mode == SGPU_MODE_GCM ?

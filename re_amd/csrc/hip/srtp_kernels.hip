@@ -26,6 +26,7 @@
  * No MFMA: this is byte/word integer work (VALU + LDS).
  */
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
@@ -759,6 +760,26 @@ __global__ void k_sst_zero(const uint32_t *slot, uint32_t n,
 		sst[slot[i]] = sgpu_sstate{};
 }
 
+/* the 32-byte state as two 16-byte words (table and arrays are 32-byte
+ * strided from 256-byte aligned bases): plain vector loads and stores --
+ * a struct copy here was promoted through LDS (32 KiB per block) */
+static_assert(sizeof(struct sgpu_sstate) == 32 &&
+	      offsetof(struct sgpu_sstate, flags) == 12,
+	      "sst_ld/sst_st move the state as two 16-byte words");
+
+__device__ __forceinline__ void sst_ld(const struct sgpu_sstate *p, uint4 &a,
+				       uint4 &b)
+{
+	a = ((const uint4 *)p)[0];
+	b = ((const uint4 *)p)[1];
+}
+
+__device__ __forceinline__ void sst_st(struct sgpu_sstate *p, uint4 a, uint4 b)
+{
+	((uint4 *)p)[0] = a;
+	((uint4 *)p)[1] = b;
+}
+
 __global__ void k_sst_load(const uint32_t *cm, const uint8_t *need,
 			   const struct sgpu_sstate *up, uint32_t nsess,
 			   struct sgpu_sstate *sst, struct sgpu_sstate *st_in)
@@ -767,15 +788,15 @@ __global__ void k_sst_load(const uint32_t *cm, const uint8_t *need,
 	if (k >= nsess)
 		return;
 	const uint32_t slot = cm[k] >> 1;
-	struct sgpu_sstate S;
+	uint4 a, b;
 	if (need && need[k]) {
-		S = up[k];
-		sst[slot] = S;
+		sst_ld(up + k, a, b);
+		sst_st(sst + slot, a, b);
 	}
 	else {
-		S = sst[slot];
+		sst_ld(sst + slot, a, b);
 	}
-	st_in[k] = S;
+	sst_st(st_in + k, a, b);
 }
 
 __global__ void k_sst_commit(const uint32_t *cm,
@@ -786,11 +807,12 @@ __global__ void k_sst_commit(const uint32_t *cm,
 	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
 	if (k >= nsess || *fail || *nfail)
 		return;
-	struct sgpu_sstate o = st_out[k];
-	if (!(o.flags & SST_TOUCHED))
+	uint4 a, b;
+	sst_ld(st_out + k, a, b);
+	if (!(a.w & SST_TOUCHED))       /* flags: the fourth word */
 		return;
-	o.flags &= ~(uint32_t)SST_TOUCHED;
-	sst[cm[k] >> 1] = o;
+	a.w &= ~(uint32_t)SST_TOUCHED;
+	sst_st(sst + (cm[k] >> 1), a, b);
 }
 
 __global__ void k_sst_read(const uint32_t *slot, uint32_t n,

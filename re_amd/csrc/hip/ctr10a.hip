@@ -24,7 +24,18 @@ kfn_t sgpu_pick_ctr10_fast(int prot, int refix)
 	return prot ? k_ctr_fast_any<10, true> : k_ctr_fast_any<10, false>;
 }
 
+/* ... and their multi-session (per-lane key) form */
+kfn_t sgpu_pick_ctr10_fast_mk(int prot)
+{
+	return prot ? k_ctr_fast_mk<10, true> : k_ctr_fast_mk<10, false>;
+}
+
 unsigned sgpu_ctr_fast_block(int prot)
 {
 	return CTRF_BLK(prot);
+}
+
+unsigned sgpu_ctr_fast_mk_block(void)
+{
+	return CTRF_MK_BLOCK;
 }

@@ -23,3 +23,9 @@ kfn_t sgpu_pick_ctr14_fast(int prot, int refix)
 		return k_ctr_fast_refix<14>;
 	return prot ? k_ctr_fast_any<14, true> : k_ctr_fast_any<14, false>;
 }
+
+/* ... and their multi-session (per-lane key) form */
+kfn_t sgpu_pick_ctr14_fast_mk(int prot)
+{
+	return prot ? k_ctr_fast_mk<14, true> : k_ctr_fast_mk<14, false>;
+}

@@ -43,14 +43,20 @@
 #define CTR_UNI_UNP_BLOCK 768
 #endif
 
+#ifndef CTR_MULTI_BLOCK     /* per-lane keys (multi-session batches) */
+#define CTR_MULTI_BLOCK 512u
+#endif
+
 __host__ __device__ constexpr unsigned ctr_block(bool prot, bool uni)
 {
-	return uni ? (prot ? CTR_UNI_PROT_BLOCK : CTR_UNI_UNP_BLOCK) : 512u;
+	return uni ? (prot ? CTR_UNI_PROT_BLOCK : CTR_UNI_UNP_BLOCK)
+		   : CTR_MULTI_BLOCK;
 }
 
 __host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
 {
-	return uni ? (int)(ctr_block(prot, uni) / 256u) : 1;
+	return uni || CTR_MULTI_BLOCK > 512u ?
+		(int)(ctr_block(prot, uni) / 256u) : 1;
 }
 
 /*

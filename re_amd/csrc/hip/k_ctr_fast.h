@@ -93,7 +93,7 @@ __device__ __forceinline__ bool fast_pkt(const struct sgpu_compact &c,
 {
 	if (t >= c.n)
 		return false;
-	f.p = c.base + t;
+	f.p = c.idx ? c.idx[c.base + t] : c.base + t;
 	const uint64_t d = c.desc[f.p];
 	const uint32_t fl = (uint32_t)(d >> 48);
 	if (!(fl & SD_RUN))
@@ -129,6 +129,25 @@ fast_keys(const KArgs &a, uint32_t rk[4 * (NR + 1)])
 #pragma unroll
 	for (int k = 0; k < 4 * (NR + 1); k++)
 		rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
+	return cp;
+}
+
+/* round keys of packet f's own context in VGPRs (multi-session batches:
+ * one context per lane, c.compmap[c.sess[p]]), same layout as fast_keys */
+template <int NR>
+__device__ __forceinline__ const struct sgpu_comp *
+lane_keys(const KArgs &a, const FastPkt &f, uint32_t rk[4 * (NR + 1)])
+{
+	const struct sgpu_comp *cp = a.comps + a.c.compmap[a.c.sess[f.p]];
+#pragma unroll
+	for (int k = 0; k < NR + 1; k++) {
+		const uint4 v = *(const uint4 *)&cp->rk[4 * k];
+		rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
+		rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
+	}
+#pragma unroll
+	for (int k = 4; k < 4 * NR; k++)
+		rk[k] = rot16(rk[k]);
 	return cp;
 }
 
@@ -174,7 +193,7 @@ __device__ __forceinline__ void tail_xor_store(const uint8_t *smem,
 	}
 }
 
-template <int NR, int SHIFT, bool PROT>
+template <int NR, int SHIFT, bool PROT, bool MK = false>
 __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 {
 	tt4_fill(smem, a.t0);
@@ -183,7 +202,10 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 	if (!fast_pkt(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
 		return;
 	uint32_t rk[4 * (NR + 1)];
-	const struct sgpu_comp *cp = fast_keys<NR>(a, rk);
+	/* MK: every lane its own session context (keys in VGPRs); all of
+	 * them one suite, so the tag length stays uniform */
+	const struct sgpu_comp *cp = MK ? lane_keys<NR>(a, f, rk)
+					: fast_keys<NR>(a, rk);
 	const uint32_t lo = (threadIdx.x & 31u) * 4u;
 	const uint32_t lane = threadIdx.x & 63u;
 	uint8_t *const arena = a.arena;
@@ -520,6 +542,32 @@ k_ctr_fast_any(const KArgs a)
 	case 1: ctr_fast_body<NR, 1, PROT>(a, smem); break;
 	case 2: ctr_fast_body<NR, 2, PROT>(a, smem); break;
 	case 3: ctr_fast_body<NR, 3, PROT>(a, smem); break;
+	default: break;                 /* rejected plan */
+	}
+}
+
+/*
+ * The lean kernel for multi-session batches (the multi-session device
+ * planner's shape: every packet planned, one suite, per-lane keys, packets
+ * taken in the planner's launch order c.idx).  A forged packet is left
+ * decrypted with SV_CIPHERED: the caller undoes the whole batch (general
+ * kernel, c.undo) before the host fold, so no restore pass runs here.
+ */
+#ifndef CTRF_MK_BLOCK
+#define CTRF_MK_BLOCK 768
+#endif
+template <int NR, bool PROT>
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, CTRF_MK_BLOCK)))
+__attribute__((amdgpu_waves_per_eu(CTRF_MK_BLOCK / 256, 8)))
+k_ctr_fast_mk(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	switch (fast_class(a)) {
+	case 0: ctr_fast_body<NR, 0, PROT, true>(a, smem); break;
+	case 1: ctr_fast_body<NR, 1, PROT, true>(a, smem); break;
+	case 2: ctr_fast_body<NR, 2, PROT, true>(a, smem); break;
+	case 3: ctr_fast_body<NR, 3, PROT, true>(a, smem); break;
 	default: break;                 /* rejected plan */
 	}
 }

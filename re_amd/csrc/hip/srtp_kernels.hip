@@ -1083,6 +1083,25 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				   sgpu_ctr_fast_block(1));
 		return e;
 	}
+	if (mode == SGPU_MODE_CTR && shift < 0 && c->uniform == 3 &&
+	    !c->undo && c->sess) {
+		/* multi-session device plan: the lean kernel with per-lane
+		 * keys, in the planner's launch order */
+		KArgs a;
+		memset(&a, 0, sizeof(a));
+		a.arena = arena;
+		a.asz = arena_size;
+		a.comps = (const struct sgpu_comp *)g_table;
+		a.t0 = g_T0_dev;
+		a.verdict = c->verdict;
+		a.save = c->save;
+		a.c = *c;
+		a.c.uniform = 0;
+		return launch(nr == 10 ? sgpu_pick_ctr10_fast_mk(prot)
+				       : sgpu_pick_ctr14_fast_mk(prot),
+			      a, c->n, prof_slot(mode, nr, 3, prot),
+			      (hipStream_t)stream, sgpu_ctr_fast_mk_block());
+	}
 	kfn_t f = mode == SGPU_MODE_GCM ?
 			  sgpu_pick_gcm(true, c->uniform != 0, nr, prot)
 		  : nr == 10 ? sgpu_pick_ctr10(true, c->uniform != 0, shift, prot)

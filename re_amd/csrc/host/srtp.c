@@ -104,6 +104,8 @@ static struct {
 	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
 	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
 				   device-planned single-key batches */
+	int nomk;               /* srtp_gpu_tune nomk: multi-session plans on
+				   the general per-lane-key kernel */
 	int splan;              /* srtp_gpu_tune splan: single-session RTP
 				   batches through the per-stream planner */
 	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
@@ -185,6 +187,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nodevfold = value > 0;
 	else if (!strcmp(name, "splan"))
 		g_env.splan = value > 0;
+	else if (!strcmp(name, "nomk"))
+		g_env.nomk = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -2423,9 +2427,13 @@ static int run_classes(uint8_t *arena, uint64_t asz, struct sgpu_compact C,
 	}
 	if (!C.undo && !g_env.perclass) {
 		C.guard = po_d->skip;
-		/* one key and the planner's packet shape: lean kernels */
+		/* one key and the planner's packet shape: lean kernels;
+		 * per-lane keys (multi-session plan): their per-lane form */
 		if (C.uniform == 1 && !g_env.nolean)
 			C.uniform = 2;
+		else if (!C.uniform && C.sess && !g_env.nolean &&
+			 !g_env.nomk)
+			C.uniform = 3;
 		return sgpu_run_compact(arena, asz, &C, c0->mode, (int)c0->nr,
 					-1, prot, stream);
 	}

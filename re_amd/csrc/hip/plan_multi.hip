@@ -140,19 +140,23 @@ k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
 		if (first ? ((S.flags & SST_EXISTS) && h.ssrc != S.ssrc)
 			  : h.ssrc != pssrc)
 			f |= SPF_SSRC;
-		if (!in.prot && h.hdr_len != 0xffffffffu &&
-		    end[i] - pos[i] - h.hdr_len < in.tag)
-			f |= SPF_PARSE;
 		if (!in.prot && (int)seq - (int)sb > 32768)
 			f |= SPF_TIMEOUT;
-		if (end[i] - pos[i] >= in.maxlen)
-			f |= SPF_SIZE;
-		if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
-		    (cap && (end[i] > cap[i] || cap[i] > asz)))
-			f |= SPF_BAD;
-		if (in.prot && cap &&
-		    (uint64_t)end[i] + in.need > (uint64_t)cap[i])
-			f |= SPF_CAP;
+		/* the window checks: made by the parse prologue (coalesced,
+		 * in.wchk, folded in by k_mp_scan) or here (gathers) */
+		if (!in.wchk) {
+			if (!in.prot && h.hdr_len != 0xffffffffu &&
+			    end[i] - pos[i] - h.hdr_len < in.tag)
+				f |= SPF_PARSE;
+			if (end[i] - pos[i] >= in.maxlen)
+				f |= SPF_SIZE;
+			if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
+			    (cap && (end[i] > cap[i] || cap[i] > asz)))
+				f |= SPF_BAD;
+			if (in.prot && cap &&
+			    (uint64_t)end[i] + in.need > (uint64_t)cap[i])
+				f |= SPF_CAP;
+		}
 		wrap = mp_wrap(seq, sb);
 		if (!last && !wrap && seq < sb)
 			f |= SPF_ORDER;
@@ -168,14 +172,20 @@ k_mp_count(const struct sgpu_mplan_in in, mp_ctx c, const uint32_t *pos,
 
 /* exclusive scan of the per-block wrap counts (one workgroup) */
 __global__ void __launch_bounds__(1024)
-k_mp_scan(uint32_t *bcnt, uint32_t nb)
+k_mp_scan(uint32_t *bcnt, uint32_t nb, const uint32_t *wchk,
+	  struct sgpu_plan_out *out)
 {
 	__shared__ uint32_t part[1024];
 	const uint32_t per = (nb + 1023u) / 1024u;
 	const uint32_t a = threadIdx.x * per;
-	uint32_t sum = 0;
-	for (uint32_t k = a; k < a + per && k < nb; k++)
+	uint32_t sum = 0, f = 0;
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
 		sum += bcnt[k];
+		if (wchk)
+			f |= wchk[k];
+	}
+	if (f)
+		atomicOr(&out->fail, f);
 	part[threadIdx.x] = sum;
 	__syncthreads();
 	for (uint32_t d = 1; d < 1024; d <<= 1) {
@@ -546,7 +556,8 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 	mp_ctx c = {kout, vout, hdr, st_in, n, sseq, sssrc};
 	hipLaunchKernelGGL(k_mp_count, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,
 			   pos, end, cap, arena_size, bcnt, out);
-	hipLaunchKernelGGL(k_mp_scan, dim3(1), dim3(1024), 0, st, bcnt, nb);
+	hipLaunchKernelGGL(k_mp_scan, dim3(1), dim3(1024), 0, st, bcnt, nb,
+			   in->wchk, out);
 	hipLaunchKernelGGL(k_mp_mark, dim3(nb), dim3(MP_BLOCK), 0, st, c,
 			   (const uint32_t *)bcnt, pex, segf, segl);
 	hipLaunchKernelGGL(k_mp_desc, dim3(nb), dim3(MP_BLOCK), 0, st, *in, c,

@@ -240,6 +240,101 @@ __global__ void k_setup(const struct sgpu_keyreq *__restrict__ req,
 /* rtp_hdr_decode (src/rtp/rtp.c:88-137), including the position at
  * which each EBADMSG is raised.  get_rtcp_ssrc (srtcp.c:19-28).        */
 
+/* one RTP header (rtp_hdr_decode, rtp.c:88-137) from a window of `left`
+ * bytes at b (p: its arena offset, for the aligned fast load) */
+__device__ __forceinline__ struct sgpu_hdr parse_rtp_hdr(const uint8_t *b,
+							 uint32_t p,
+							 uint32_t left)
+{
+	struct sgpu_hdr h;
+	h.ssrc = 0; h.seq = 0; h.err_pos = 0; h.hdr_len = 0xffffffffu;
+	if (left < 12)
+		return h;
+	uint32_t b0;
+	if (!(p & 3u)) {
+		const uint32_t w0 = *(const uint32_t *)b;
+		const uint32_t w2 = *(const uint32_t *)(b + 8);
+		b0 = w0 & 0xffu;
+		h.seq = (uint16_t)((w0 >> 8 & 0xff00u) | (w0 >> 24));
+		h.ssrc = __builtin_bswap32(w2);
+	}
+	else {
+		b0 = b[0];
+		h.seq = (uint16_t)(b[2] << 8 | b[3]);
+		h.ssrc = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 |
+			 (uint32_t)b[10] << 8 | b[11];
+	}
+	const uint32_t cc = b0 & 0x0fu, x = (b0 >> 4) & 1u;
+	uint32_t hl = 12;
+	if (left - hl < 4 * cc) {
+		h.err_pos = (uint16_t)hl;
+		return h;
+	}
+	hl += 4 * cc;
+	if (x) {
+		if (left - hl < 4) {
+			h.err_pos = (uint16_t)hl;
+			return h;
+		}
+		const uint32_t xl = (uint32_t)b[hl + 2] << 8 | b[hl + 3];
+		hl += 4;
+		if (left - hl < 4 * xl) {
+			h.err_pos = (uint16_t)hl;
+			return h;
+		}
+		hl += 4 * xl;
+	}
+	h.hdr_len = hl;
+	return h;
+}
+
+/*
+ * k_parse for an RTP batch of a device planner, with the planner's
+ * per-packet window checks (k_plan_count / k_mp_count) made here, where
+ * pos / end / cap are read coalesced: the OR of a 256-packet block goes
+ * to wchk[block] (plain stores, read by the planner's scan -- no zeroed
+ * word needed).  Block size 256 (= the planners' blocks).
+ */
+__device__ __forceinline__ void k_parse_rtp_checked(
+	const uint8_t *__restrict__ arena, uint64_t asz,
+	const uint32_t *__restrict__ pos, const uint32_t *__restrict__ end,
+	struct sgpu_hdr *__restrict__ out, uint32_t n,
+	const struct sgpu_prologue &pro)
+{
+	__shared__ uint32_t bf;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (threadIdx.x == 0)
+		bf = 0;
+	__syncthreads();
+	if (i < n) {
+		const uint32_t p = pos[i], e = end[i];
+		if (pro.end_copy)
+			pro.end_copy[i] = e;
+		const uint32_t left = (e > p && e <= asz) ? e - p : 0;
+		const struct sgpu_hdr h = parse_rtp_hdr(arena + p, p, left);
+		out[i] = h;
+		uint32_t f = 0;
+		if (h.hdr_len == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (!pro.prot && e - p - h.hdr_len < pro.tag)
+			f |= SPF_PARSE;
+		if (e - p >= pro.maxlen)
+			f |= SPF_SIZE;
+		const uint32_t c = pro.cap ? pro.cap[i] : 0u;
+		if ((p & 3u) || p > e || e > asz ||
+		    (pro.cap && (e > c || c > asz)))
+			f |= SPF_BAD;
+		if (pro.prot && pro.cap &&
+		    (uint64_t)e + pro.need > (uint64_t)c)
+			f |= SPF_CAP;
+		if (f)
+			atomicOr(&bf, f);
+	}
+	__syncthreads();
+	if (threadIdx.x == 0)
+		pro.wchk[blockIdx.x] = bf;
+}
+
 __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 			const uint32_t *__restrict__ pos,
 			const uint32_t *__restrict__ end,
@@ -256,6 +351,10 @@ __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 			pro.z1[k] = 0;
 		if (pro.cm_out && threadIdx.x == 0)
 			*pro.cm_out = pro.cm;
+	}
+	if (pro.wchk) {
+		k_parse_rtp_checked(arena, asz, pos, end, out, n, pro);
+		return;
 	}
 	if (i >= n)
 		return;

@@ -3127,7 +3127,8 @@ static int dev_planned_issue(struct dcall *k)
 		/* one launch: parse + end copy + zeroed counters + comp map */
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
-			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm};
+			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm, NULL, NULL,
+			0, 0, 0, 0};
 		k->in.zeroed = 1;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
@@ -3376,7 +3377,7 @@ static int dev_splanned_issue(struct dcall *k)
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
 			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d,
-			c0->dev};
+			c0->dev, NULL, NULL, 0, 0, 0, 0};
 		k->sin.zeroed = 1;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
@@ -3549,7 +3550,8 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		 * plan + comp map, one launch */
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
-			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm};
+			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm, NULL, NULL,
+			0, 0, 0, 0};
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, prot ? NULL : eix_d,
 					  (uint32_t)n, 1, &pro, stream);
@@ -3671,8 +3673,9 @@ static int dev_mplanned_issue(struct dcall *k)
 	if (!err)
 		err = pool_reserve(w, &w->ms,
 				   nsess * (3 * sizeof(struct sgpu_sstate) + 1));
-	if (!err)   /* scratch, then the launch order (n words) */
-		err = pool_reserve(w, &w->mscr, scr + n * 4);
+	if (!err)   /* scratch, the launch order (n words), then the parse
+		     * prologue's window-check words (one per 256 packets) */
+		err = pool_reserve(w, &w->mscr, scr + n * 4 + (n / 256 + 1) * 4);
 	if (err)
 		return err;
 	hd_d = (struct sgpu_hdr *)w->hd.d;
@@ -3693,16 +3696,22 @@ static int dev_mplanned_issue(struct dcall *k)
 	need_h = (uint8_t *)(up_h + nsess);
 	order_d = (uint32_t *)(w->mscr.d + scr);
 	/* parse + end copy (the kernels keep reading the input windows) +
-	 * zeroed miss counter, one launch; it runs while the host gathers */
+	 * zeroed miss counter + the planner's window checks, one launch */
+	memset(&in, 0, sizeof(in));
+	in.wchk = (const uint32_t *)(w->mscr.d + scr + n * 4);
 	{
-		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0};
+		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0,
+					    (uint32_t *)in.wchk, d->cap,
+					    (uint32_t)prot, T,
+					    prot ? (gcm ? 16u : (T > 4 ? T : 4u))
+						 : 0u,
+					    SGPU_CACHED_MAX(c0->mode)};
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
 					  &pro, stream);
 		if (err)
 			return err;
 	}
-	memset(&in, 0, sizeof(in));
 	in.n = (uint32_t)n;
 	in.nsess = (uint32_t)nsess;
 	in.prot = (uint32_t)prot;

@@ -338,6 +338,11 @@ struct sgpu_mplan_in {
 	uint32_t need;
 	uint32_t key_bits;      /* bits of the session index */
 	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
+	uint32_t pad;
+	const uint32_t *wchk;   /* or NULL: the window checks (SPF_PARSE,
+				   SIZE, BAD, CAP) were made by the parse
+				   prologue, one word per 256-packet block
+				   (sgpu_prologue.wchk) */
 };
 
 /* the same in two launch groups: phase 1 sorts the packets by session
@@ -483,6 +488,12 @@ struct sgpu_prologue {
 	uint32_t nz0, nz1;
 	uint32_t *cm_out;
 	uint32_t cm;
+	/* wchk != NULL: per 256-packet block, the OR of each packet's
+	 * window checks of the RTP planners (k_plan_count / k_mp_count:
+	 * SPF_PARSE, SPF_SIZE, SPF_BAD, SPF_CAP), with these parameters */
+	uint32_t *wchk;
+	const uint32_t *cap;
+	uint32_t prot, tag, need, maxlen;
 };
 int   sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
 			  const uint32_t *pos, const uint32_t *end,

@@ -531,7 +531,7 @@ def main():
                 "lds_frac": round(sq["lds_frac"], 4) if sq and
                 "lds_frac" in sq else None,
                 "int_src": os.path.basename(sj) if sq else None,
-                "kernel": (("k_ctr_fast_any" if nsess == 1 else "k_ctr_hmac")
+                "kernel": (("k_ctr_fast_any" if nsess == 1 else "k_ctr_fast_mk")
                            if (dom["slot"] & 8) == 0 else
                            ("k_gcmu" if nsess == 1 else "k_gcm")),
                 "dir": dom["dir"],

@@ -29,7 +29,7 @@ import json
 import sys
 from collections import defaultdict
 
-CRYPTO = ("k_ctr_fast_any", "k_ctr_hmac", "k_gcm")
+CRYPTO = ("k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_hmac", "k_gcm")
 VALU_RATE = 54.56e12 / 65536   # wave-instructions/s per SIMD (v_xor, 4 w/S)
 SIMDS = 1024
 

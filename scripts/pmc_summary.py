@@ -11,9 +11,10 @@ import csv
 import json
 import sys
 
-# the crypto kernels: k_ctr_fast_any (lean, device-planned single key),
+# the crypto kernels: k_ctr_fast_any / k_ctr_fast_mk (lean: device-planned
+# single key / per-lane keys),
 # k_ctr_hmac / k_ctr_hmac_any (general compact), k_gcmu / k_gcm
-CRYPTO = ("k_ctr_fast_any", "k_ctr_hmac", "k_gcm")
+CRYPTO = ("k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_hmac", "k_gcm")
 
 
 def per_kernel(path, counter):

@@ -142,3 +142,17 @@ def test_host_pool_covers_every_range_once(tmp_path):
         cb = FN(part)
         L.par_for(n, min_per, cb, None)
         assert (seen == 1).all(), (n, min_per)
+
+
+def test_tune_knobs_and_counters():
+    """srtp_gpu_tune accepts every A/B knob the library documents and
+    rejects unknown ones; srtp_gpu_counter names every diagnostic counter
+    (no GPU needed: neither touches the device)"""
+    L = P.load()
+    for k in ("noplan", "general", "perclass", "nolean", "nodevfold",
+              "splan", "nomk", "trace", "times"):
+        assert L.srtp_gpu_tune(k.encode(), 1) == 0, k
+        assert L.srtp_gpu_tune(k.encode(), 0) == 0, k
+    assert L.srtp_gpu_tune(b"no-such-knob", 1) != 0
+    for c in ("misses", "folds", "rejects", "devfolds", "splans"):
+        assert P.counter(c) >= 0, c

@@ -244,3 +244,79 @@ def test_streams_async_chain(suite, torch_cuda):
         for u, v in zip(x, y):
             assert (u == v).all()
     assert outs["sync"][1] == outs["async"][1]
+
+
+@pytest.mark.parametrize("suite", [1, 4])
+def test_streams_edge_shapes(suite, torch_cuda):
+    """per-stream planner edge shapes, each vs the general engine: batches
+    of 1, 255, 257 and 1025 packets; an 8th stream joining 7 existing
+    ones; a 9th SSRC in a later batch (ENOSR); a stream whose s_l is not
+    set yet (created by SRTCP first); a ROC wrap exactly at the batch
+    boundary; a replay of the previous batch's last packet"""
+    torch = torch_cuda
+    rng = np.random.default_rng(1234 + suite)
+    key = keys_for(suite, 1)[0]
+
+    def run_both(batches, ssrcs, pre=None, rx_mutate=None):
+        res = []
+        for mode in ("plan", "general"):
+            knobs = {"plan": {}, "general": {"general": 1}}[mode]
+            tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
+            if pre:
+                pre(tx, rx)
+            outs = []
+            with P.tune(**knobs):
+                for bi, pk in enumerate(batches):
+                    a, p, e, c = arena_of(pk)
+                    r = run_dev(torch, "srtp_encrypt", [tx], a, p, e, c,
+                                None)
+                    outs.append(r)
+                    rp = protected(r, p)
+                    if rx_mutate:
+                        rp = rx_mutate(bi, rp)
+                    a2, p2, e2, c2 = arena_of(rp)
+                    outs.append(run_dev(torch, "srtp_decrypt", [rx], a2, p2,
+                                        e2, c2, None))
+            res.append((outs, (states([tx], ssrcs), states([rx], ssrcs))))
+            tx.close()
+            rx.close()
+        same(res[0], res[1], "edge")
+        return res[0]
+
+    # sizes around the planner's block (1024) and the LDS scan width
+    for n in (1, 255, 257, 1025):
+        which = rng.integers(0, 3, n)
+        pk, _ = interleaved(rng, which, {k: 65530 + k for k in range(3)})
+        run_both([pk], [SSRC0 + k for k in range(3)])
+
+    # 7 streams, then an 8th joins; then a 9th SSRC (ENOSR) in batch 3
+    b1, nxt = interleaved(rng, rng.integers(0, 7, 700),
+                          {k: 100 * k for k in range(9)})
+    b2, nxt = interleaved(rng, rng.integers(0, 8, 700), nxt)
+    b3, _ = interleaved(rng, rng.integers(0, 9, 700), nxt)
+    out, _ = run_both([b1, b2, b3], [SSRC0 + k for k in range(9)])
+    assert errno.ENOSR in {int(x) for x in out[4][3]}
+
+    # a stream created by SRTCP (s_l not set), then RTP on it and another
+    def rtcp_first(tx, rx):
+        for ctx in (tx, rx):
+            st = P.StreamState()
+            st.ssrc = SSRC0 + 1
+            assert ctx.import_(st) == 0     # exists, s_l_set = 0
+    pk, _ = interleaved(rng, rng.integers(0, 2, 600), {0: 5, 1: 65000})
+    run_both([pk], [SSRC0, SSRC0 + 1], pre=rtcp_first)
+
+    # a ROC wrap exactly at the batch boundary, and a replayed last packet
+    b1, nxt = interleaved(rng, np.array([0, 1] * 268),
+                          {0: 65536 - 268, 1: 65536 - 268})
+    b2, _ = interleaved(rng, np.array([0, 1] * 300), nxt)
+
+    saved = []
+
+    def replay_last(bi, rp):
+        if bi == 0:
+            saved[:] = [rp[-1]]         # the batch's last packet ...
+            return rp
+        return saved + rp               # ... received again first
+    out, _ = run_both([b1, b2], [SSRC0, SSRC0 + 1], rx_mutate=replay_last)
+    assert errno.EALREADY in {int(x) for x in out[3][3]}

@@ -482,6 +482,8 @@ k_plan_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
 	bool wrap = false;
 	uint32_t f = 0;
+	if (i == 0 && in.pred && *in.pred)     /* sgpu_gate_pred */
+		atomicOr(&out->fail, (uint32_t)SPF_PRED);
 	if (i < in.n) {
 		const struct sgpu_hdr h = hdr[i];
 		const uint32_t hl0 = hdr[0].hdr_len;
@@ -1725,6 +1727,40 @@ k_plan_results(const uint32_t *__restrict__ guard,
 		return;
 	end[i] = end0[i] + (uint32_t)delta;
 	err[i] = 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_plan_finish(const uint32_t *__restrict__ guard,
+	      const uint32_t *__restrict__ end0, uint32_t *__restrict__ end,
+	      int32_t *__restrict__ err, uint32_t n, int32_t delta,
+	      const uint32_t *nfail, uint32_t *gate, uint32_t *nfail_out)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t g = *guard;
+	if (i == 0) {
+		const uint32_t nf = nfail ? *nfail : 0u;
+		if (gate)
+			*gate = g || nf;
+		if (nfail_out)
+			*nfail_out = nf;
+	}
+	if (i >= n || g)
+		return;
+	end[i] = end0[i] + (uint32_t)delta;
+	err[i] = 0;
+}
+
+extern "C" int sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
+				uint32_t *end, int32_t *err, uint32_t n,
+				int32_t delta, const uint32_t *nfail,
+				uint32_t *gate, uint32_t *nfail_out,
+				void *stream)
+{
+	const uint32_t nb = n ? (n + 255) / 256 : 1;
+	hipLaunchKernelGGL(k_plan_finish, dim3(nb), dim3(256), 0,
+			   (hipStream_t)stream, guard, end0, end, err, n, delta,
+			   nfail, gate, nfail_out);
+	return herr(hipGetLastError(), "finish launch");
 }
 
 extern "C" int sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,

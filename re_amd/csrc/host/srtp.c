@@ -3134,8 +3134,7 @@ static int dev_planned_issue(struct dcall *k)
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
 					  &pro, stream);
 	}
-	if (!err && k->pred)
-		err = sgpu_gate_pred(k->pred, &po_d->fail, stream);
+	k->in.pred = k->pred;   /* the gate check rides in k_plan_count */
 	if (!err)
 		err = sgpu_plan_rtp(&k->in, hd_d, d->pos, es_d, d->cap,
 				    d->arena_size, desc_d, scr, po_d, stream);
@@ -3147,18 +3146,15 @@ static int dev_planned_issue(struct dcall *k)
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
+	/* results, gate word and the miss count next to the plan: one
+	 * launch, one copy into pinned memory */
 	if (!err)
-		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
-					(uint32_t)n,
-					prot ? (int32_t)T : -(int32_t)T, stream);
-	if (!err && k->gate)
-		err = sgpu_gate_set(&po_d->fail, nfail_d, k->gate, stream);
+		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
+				       (uint32_t)n,
+				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
+				       k->gate, &po_d->nfail, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
-	/* the miss count lands in pinned memory next to the plan (a
-	 * pageable destination would stage the copy through the runtime) */
-	if (!err)
-		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	return err;
 }
 
@@ -3188,7 +3184,7 @@ static int dev_planned_finish(struct dcall *k)
 	uint32_t nfail;
 	int err = 0;
 
-	nfail = *(const uint32_t *)(po + 1);
+	nfail = po->nfail;
 	k->pfail = po->fail;
 	if (po->fail) {
 		if (po->fail & SPF_PRED)
@@ -3398,15 +3394,12 @@ static int dev_splanned_issue(struct dcall *k)
 				  &po_d->base, prot, stream);
 	}
 	if (!err)
-		err = sgpu_plan_results(&po_d->base.fail, es_d, d->end, d->err,
-					(uint32_t)n,
-					prot ? (int32_t)T : -(int32_t)T, stream);
-	if (!err && k->gate)
-		err = sgpu_gate_set(&po_d->base.fail, nfail_d, k->gate, stream);
+		err = sgpu_plan_finish(&po_d->base.fail, es_d, d->end, d->err,
+				       (uint32_t)n,
+				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
+				       k->gate, &po_d->base.nfail, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
-	if (!err)   /* pinned, next to the plan (see dev_planned_issue) */
-		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	return err;
 }
 
@@ -3423,7 +3416,7 @@ static int dev_splanned_finish(struct dcall *k)
 	const size_t n = d->n;
 	const struct sgpu_splan_out *po = (const struct sgpu_splan_out *)w->pl.h;
 	struct sgpu_splan_out *po_d = (struct sgpu_splan_out *)w->pl.d;
-	const uint32_t nfail = *(const uint32_t *)(po + 1);
+	const uint32_t nfail = po->base.nfail;
 	int err;
 
 	k->pfail = po->base.fail;
@@ -3569,19 +3562,17 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
 	}
 	if (!err)
-		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
-					(uint32_t)n,
-					prot ? (int32_t)grow : -(int32_t)grow,
-					stream);
+		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
+				       (uint32_t)n,
+				       prot ? (int32_t)grow : -(int32_t)grow,
+				       nfail_d, NULL, &po_d->nfail, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
-	if (!err)   /* pinned, next to the plan (see dev_planned) */
-		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
-	nfail = *(const uint32_t *)(po + 1);
+	nfail = po->nfail;
 	if (po->fail) {
 		count(&g_cnt_rejects, 1);
 		return -1;
@@ -3762,21 +3753,18 @@ static int dev_mplanned_issue(struct dcall *k)
 				  po_d, prot, stream);
 	}
 	if (!err)
-		err = sgpu_plan_results(&po_d->fail, es_d, d->end, d->err,
-					(uint32_t)n,
-					prot ? (int32_t)T : -(int32_t)T, stream);
+		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
+				       (uint32_t)n,
+				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
+				       k->gate, &po_d->nfail, stream);
 	/* the new states replace the resident ones if the plan held and every
 	 * tag verified (a forged packet: the host folds from the old ones) */
 	if (!err)
 		err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
 				      (uint32_t)nsess, &po_d->fail, nfail_d,
 				      stream);
-	if (!err && k->gate)
-		err = sgpu_gate_set(&po_d->fail, nfail_d, k->gate, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
-	if (!err)   /* pinned, next to the plan (see dev_planned) */
-		err = sgpu_memcpy_d2h(po + 1, nfail_d, 4, stream);
 	k->t[2] = times ? now_ms() : 0;
 	return err;
 }
@@ -3801,7 +3789,7 @@ static int dev_mplanned_finish(struct dcall *k)
 	uint8_t *vd_d = w->vs.d + 64 + n * 4;
 	uint32_t *es_d = (uint32_t *)w->es.d;
 	void *stream = d->stream;
-	uint32_t nfail = *(const uint32_t *)(po + 1);
+	uint32_t nfail = po->nfail;
 	int err;
 
 	if (g_env.times)

@@ -205,6 +205,9 @@ struct sgpu_plan_in {
 	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
 	uint32_t zeroed;        /* out already zeroed (sgpu_parse_prologue) */
 	uint32_t pad;
+	const uint32_t *pred;   /* async chain: the gate word of the call
+				   before, or NULL (sgpu_gate_pred, folded
+				   into the plan's first kernel) */
 };
 
 /* compact (counter-cached) kernels take packets shorter than this:
@@ -249,7 +252,8 @@ struct sgpu_plan_out {
 	uint32_t ssrc0;
 	uint32_t hl0;           /* header length of packet 0 */
 	uint32_t s_l_last;      /* s_l after the last packet */
-	uint32_t pad;
+	uint32_t nfail;         /* the crypto launch's speculation misses
+				   (copied here by sgpu_plan_finish) */
 	uint32_t skip[4];       /* guard of the shift-class-s crypto launch:
 				   fail || class(hl0) != s */
 	uint64_t tail_ix[SGPU_PLAN_TAIL]; /* ix of the last min(n,65) packets */
@@ -455,6 +459,13 @@ int   sgpu_fold_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
 
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */
+/* sgpu_plan_results, and in the same launch: *gate = *guard || *nfail
+ * (sgpu_gate_set; gate may be NULL) and *nfail_out = *nfail (next to the
+ * plan, so one copy brings both back; nfail_out may be NULL) */
+int   sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
+		       uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
+		       const uint32_t *nfail, uint32_t *gate,
+		       uint32_t *nfail_out, void *stream);
 int   sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
 			uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
 			void *stream);

@@ -225,6 +225,20 @@ def main():
         s0 = S.shard_seq0(rank, n, 65000)   # this shard's first seq
     lengths = cfg["length"] if cfg["length"] else W.mixed_lengths(n)
     sess = W.random_sessions(n, nsess) if nsess > 1 else None
+    gidx = gsess = None
+    key_ids = None
+    if nsess > 1 and world > 1:
+        # a multi-session load shards by session id -- one
+        # workload of world x n packets over world x nsess sessions, each
+        # rank the packets of the sessions it owns (re_amd/shard.py), so
+        # every stream's state stays on its rank (weak scaling: ~n each)
+        g_sess = W.random_sessions(n * world, nsess * world)
+        gidx, sess = S.shard_sessions(g_sess, world, rank)
+        gsess = g_sess[gidx]
+        lengths = W.mixed_lengths(n * world)[gidx]
+        n = len(gidx)
+        key_ids = np.arange(nsess, dtype=np.uint64) * world + rank
+        cfg["name"] += ", sessions hashed over %d ranks" % world
     K = max(1, args.ssrcs)
     if K > 1:
         assert nsess == 1 and cfg_id in (2, 3) and not args.rtcp, \
@@ -236,14 +250,15 @@ def main():
     else:
         arena_h, pos, end, cap = W.make_arena(
             n, lengths, s0=s0 & 0xffff,
-            sess=sess if K == 1 else np.arange(n, dtype=np.uint32) % K)
+            sess=(gsess if gsess is not None else sess) if K == 1 else
+            np.arange(n, dtype=np.uint32) % K, idx=gidx)
     OPS = ("srtcp_encrypt", "srtcp_decrypt") if args.rtcp else \
         ("srtp_encrypt", "srtp_decrypt")
     log("workload built (%d packets)" % n)
     arena = torch.from_numpy(arena_h).to(dev)
     plain = arena.clone() if not args.no_verify else None
     klen = P.key_len(suite) + P.salt_len(suite)
-    keys = W.make_keys(nsess, klen)
+    keys = W.make_keys(nsess, klen, ids=key_ids)
     # one explicit stream for the whole run (torch copies and the library
     # calls), so ordering is explicit rather than via the null stream
     torch.cuda.synchronize()

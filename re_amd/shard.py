@@ -48,6 +48,29 @@ def shard_state(rank, per_rank, s0, ssrc, receiver, state_cls=None):
     return o
 
 
+def session_rank(sess, world):
+    """rank owning each session of a multi-session workload (SURVEY 8(e):
+    shard by session id): the id modulo the world size.  Every packet of a
+    session -- so every stream's ROC, s_l and replay state -- stays on one
+    rank, with no hand-off; the generated ids are uniform, so ranks get
+    equal shares."""
+    import numpy as np
+    if world < 1:
+        raise ValueError("session_rank: world >= 1")
+    return (np.asarray(sess, dtype=np.uint64) %
+            np.uint64(world)).astype(np.int64)
+
+
+def shard_sessions(sess, world, rank):
+    """rank's shard of a multi-session workload: (global indices of its
+    packets in arrival order, their dense local session ids
+    global // world).  Local id k is global session k * world + rank."""
+    import numpy as np
+    sess = np.asarray(sess)
+    mine = np.flatnonzero(session_rank(sess, world) == rank)
+    return mine, (sess[mine] // world).astype(np.uint32)
+
+
 def shard_seq0(rank, per_rank, s0):
     """first sequence number of rank's shard"""
     return (s0 + rank * per_rank) & 0xffff

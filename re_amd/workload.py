@@ -68,25 +68,31 @@ def xs_bytes(seed, idx, nbytes):
     return out.view(np.uint8)[:, :nbytes]
 
 
-def make_keys(nsess, klen, seed=SEED_KEYS):
-    return np.ascontiguousarray(xs_bytes(seed, np.arange(nsess), klen))
+def make_keys(nsess, klen, seed=SEED_KEYS, ids=None):
+    """keys of sessions 0..nsess-1, or of the global session ids `ids`"""
+    ids = np.arange(nsess) if ids is None else np.asarray(ids)
+    return np.ascontiguousarray(xs_bytes(seed, ids, klen))
 
 
 def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
-               payload=True, first=0, room=16):
+               payload=True, first=0, room=16, idx=None):
     """Returns (arena uint8[n*slot], pos, end, cap) numpy arrays.
 
     lengths: int or uint32 array (RTP packet length incl. 12-B header).
     sess: optional per-packet session index (SSRC = SSRC_BASE + sess).
     first: global index of packet 0 (a shard of a longer stream: payload
     generators and ts continue the stream).
+    idx: or the global index of every packet (a session-hashed shard of a
+    longer workload, re_amd/shard.py shard_sessions).
     """
     lengths = np.broadcast_to(np.asarray(lengths, dtype=np.uint32),
                               (npkts,)).copy()
     maxlen = int(lengths.max())
     slot = slot_size(maxlen, room)
     arena = np.zeros((npkts, slot), dtype=np.uint8)
-    gidx = np.arange(first, first + npkts, dtype=np.uint64)
+    gidx = np.arange(first, first + npkts, dtype=np.uint64) if idx is None \
+        else np.asarray(idx, dtype=np.uint64)
+    assert len(gidx) == npkts
     if payload and maxlen > 12:
         # in chunks: the uint64 word matrix of 1M packets is ~1.2 GB
         step = 1 << 16

@@ -123,3 +123,39 @@ def test_gloo_world2_shards_and_reduction(per_rank, s0):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_session_hash_shards():
+    """multi-session loads shard by session id: disjoint
+    packet sets covering the workload, every session on one rank, dense
+    local ids, arrival order kept, balanced ranks; a shard's packets are
+    byte-identical to the same packets of the whole workload"""
+    import numpy as np
+    from re_amd import shard as S
+    from re_amd import workload as W
+    world, per, nsess = 4, 3000, 64
+    n = per * world
+    g_sess = W.random_sessions(n, nsess * world)
+    lengths = W.mixed_lengths(n)
+    full, fpos, fend, _ = W.make_arena(n, lengths, s0=65000, sess=g_sess)
+    seen = np.zeros(n, dtype=np.int64)
+    owner = {}
+    for r in range(world):
+        gidx, loc = S.shard_sessions(g_sess, world, r)
+        assert (np.diff(gidx) > 0).all()                  # arrival order
+        assert abs(len(gidx) - per) < per * 0.1            # balanced
+        assert loc.max() < nsess                           # dense ids
+        assert (loc * world + r == g_sess[gidx]).all()
+        for s in np.unique(g_sess[gidx]):
+            assert owner.setdefault(int(s), r) == r        # one rank
+        seen[gidx] += 1
+        a, pos, end, _ = W.make_arena(len(gidx), lengths[gidx], s0=65000,
+                                      sess=g_sess[gidx], idx=gidx)
+        for j in range(0, len(gidx), 97):
+            i = gidx[j]
+            assert a[pos[j]:end[j]].tobytes() == \
+                full[fpos[i]:fend[i]].tobytes(), (r, j)
+        keys = W.make_keys(nsess, 30, ids=np.arange(nsess) * world + r)
+        allk = W.make_keys(nsess * world, 30)
+        assert (keys == allk[np.arange(nsess) * world + r]).all()
+    assert (seen == 1).all()

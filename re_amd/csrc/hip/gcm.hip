@@ -299,8 +299,12 @@ k_gcm(const KArgs a)
 				   packets against 768 threads (3 waves/SIMD,
 				   no spills) -- the LDS latency wants waves */
 #endif
-#ifndef GCMU_COAL
-#define GCMU_COAL 1
+#ifndef GCMU_COAL           /* quad-coalesced 64-byte chunks: off since the
+			       1024-thread blocks -- the quad offsets and
+			       transposes cost registers (protect spilled),
+			       and per-lane chunks measured faster (protect
+			       1.64 -> 1.57 ms, unprotect 1.64 -> 1.62) */
+#define GCMU_COAL 0
 #endif
 #ifndef GCMU_ALIGNED        /* packet-aligned 64-byte chunks (gcma_packet) */
 #define GCMU_ALIGNED 1

@@ -35,6 +35,9 @@
 #ifndef CTRF_COAL_U         /* ... unprotect */
 #define CTRF_COAL_U 1
 #endif
+#ifndef CTRF_COAL_MK        /* ... per-lane-key (multi-session) kernel */
+#define CTRF_COAL_MK 1
+#endif
 #ifndef CTRF_SHAFIRST_U     /* unprotect steady chunk: MAC, then decrypt */
 #define CTRF_SHAFIRST_U 1
 #endif
@@ -268,7 +271,8 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 	for (; k < kf0; k++)
 		general(k);
 
-	constexpr bool COAL = PROT ? CTRF_COAL_P : CTRF_COAL_U;
+	constexpr bool COAL = MK ? CTRF_COAL_MK :
+			      PROT ? CTRF_COAL_P : CTRF_COAL_U;
 	uint32_t K0 = kf1, K1 = kf1;
 	uint32_t qo[4];                         /* 32-bit quad offsets */
 	if constexpr (COAL) {

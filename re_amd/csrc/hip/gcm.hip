@@ -306,6 +306,10 @@ k_gcm(const KArgs a)
 			       1.64 -> 1.57 ms, unprotect 1.64 -> 1.62) */
 #define GCMU_COAL 0
 #endif
+#ifndef GCMU_B8             /* counters < 256 (packets < SGPU_CACHED_MAX_GCM
+			       = 4032 B): 5 fewer T-table lookups per block */
+#define GCMU_B8 1
+#endif
 #ifndef GCMU_ALIGNED        /* packet-aligned 64-byte chunks (gcma_packet) */
 #define GCMU_ALIGNED 1
 #endif
@@ -400,7 +404,7 @@ __device__ __forceinline__ void ghash8_mul(uint32_t x[4], const uint8_t *smem,
 template <int NR, bool PROT>
 __device__ __forceinline__ uint8_t gcmu_packet(const uint8_t *smem, uint32_t lo,
 					       uint32_t hi16, const uint32_t *rk,
-					       const CtrKs<NR, true> &C,
+					       const CtrKs<NR, true, false, GCMU_B8> &C,
 					       uint8_t *arena, uint64_t asz,
 					       const struct sgpu_job &j,
 					       uint32_t lane)
@@ -549,7 +553,7 @@ __device__ __forceinline__ uint8_t gcmu_packet(const uint8_t *smem, uint32_t lo,
 template <int NR, bool PROT>
 __device__ __forceinline__ void gcm_block16(const uint8_t *smem, uint32_t lo,
 					   uint32_t hi16, const uint32_t *rk,
-					   const CtrKs<NR, true> &C, uint8_t *pkt,
+					   const CtrKs<NR, true, false, GCMU_B8> &C, uint8_t *pkt,
 					   uint64_t pasz, uint32_t c_off,
 					   uint32_t b, uint32_t X[4])
 {
@@ -582,7 +586,7 @@ __device__ __forceinline__ void gcm_block16(const uint8_t *smem, uint32_t lo,
 template <int NR, bool PROT, int S>
 __device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
 					       uint32_t hi16, const uint32_t *rk,
-					       const CtrKs<NR, true> &C,
+					       const CtrKs<NR, true, false, GCMU_B8> &C,
 					       uint8_t *arena, uint64_t asz,
 					       const struct sgpu_job &j,
 					       uint32_t lane)
@@ -875,7 +879,7 @@ k_gcmu(const KArgs a)
 		iv[2] = ks.z ^ bswap32(be2);
 		iv[3] = 0;
 	}
-	CtrKs<NR, true> C;
+	CtrKs<NR, true, false, GCMU_B8> C;
 	C.init(smem, lo, rk, iv);
 
 	if (j.flags & SJ_UNDO) {

@@ -102,7 +102,10 @@ __device__ __forceinline__ void ctr_block(const uint8_t *smem, uint32_t lo,
 #define CTR_B15 1
 #endif
 
-template <int NR, bool CACHED, bool T4 = false>
+/* B8 (two-table image only): every block index < 256 -- only the low
+ * counter byte varies, so round 1 has one varying lookup and round 2 four
+ * (the single-key GCM kernel; SGPU_CACHED_MAX_GCM bounds its packets) */
+template <int NR, bool CACHED, bool T4 = false, bool B8 = false>
 struct CtrKs {
 	uint32_t t0, t1, t2, t3c;       /* IV ^ rk[0..3] (t3c: bytes 14,15 = rk) */
 	uint32_t A0, P0, A1, P1;        /* round 1: s0 = A0^rot16(P0^T1[t3.b3]) */
@@ -172,6 +175,17 @@ struct CtrKs {
 		     lds_u32(smem, TT_ADDR(S3, 1, lo) + 128);
 		C3a = lds_u32(smem, TT_ADDR(S3, 0, lo));
 		C3b = lds_u32(smem, TT_ADDR(S2, 3, lo) + 128) ^ k2[3];
+		if (B8) {
+			/* t3 byte 2 is constant too: s1 and its four round-2
+			 * lookups fold into the constants */
+			const uint32_t s1 = A1 ^ rot16(P1 ^ lds_u32(smem,
+						TT_ADDR(t3c, 2, lo)));
+			R0 ^= lds_u32(smem, TT_ADDR(s1, 1, lo) + 128);
+			C1a ^= lds_u32(smem, TT_ADDR(s1, 0, lo));
+			C2 ^= rot16(lds_u32(smem, TT_ADDR(s1, 3, lo) + 128) ^
+				    k2[2]);
+			C3a ^= rot16(lds_u32(smem, TT_ADDR(s1, 2, lo)) ^ C3b);
+		}
 	}
 
 	/* keystream block b.  CACHED: exact for 0 <= b < 65536, and with
@@ -210,6 +224,22 @@ struct CtrKs {
 			uint32_t r2 = xor3(T.t2(s0), T.t3(s1), C2);
 			uint32_t r3 = xor3(T.t1(s0), T.t2(s1), C3a);
 			aes4_rounds<NR, 3>(T, rk, r0, r1, r2, r3);
+			ks[0] = r0; ks[1] = r1; ks[2] = r2; ks[3] = r3;
+			return;
+		}
+		if (B8) {
+			/* b < 256: bswap32(b) = b << 24, one varying byte */
+			const uint32_t t3b = t3c ^ ((uint32_t)b << 24);
+			const uint32_t s0 = A0 ^ rot16(P0 ^ lds_u32(smem,
+						TT_ADDR(t3b, 3, lo) + 128));
+			uint32_t r0 = lds_u32(smem, TT_ADDR(s0, 0, lo)) ^ R0;
+			uint32_t r1 = C1a ^ rot16(C1b ^ lds_u32(smem,
+						TT_ADDR(s0, 3, lo) + 128));
+			uint32_t r2 = C2 ^ rot16(lds_u32(smem,
+						TT_ADDR(s0, 2, lo)));
+			uint32_t r3 = C3a ^ lds_u32(smem,
+						   TT_ADDR(s0, 1, lo) + 128);
+			aes_rounds<NR, 3>(smem, lo, rk, r0, r1, r2, r3);
 			ks[0] = r0; ks[1] = r1; ks[2] = r2; ks[3] = r3;
 			return;
 		}

@@ -652,6 +652,8 @@ k_plan_rtcp(const struct sgpu_rplan_in in, const struct sgpu_hdr *hdr,
 	if ((pos[i] & 3u) || pos[i] > end[i] || end[i] > asz ||
 	    (cap && (end[i] > cap[i] || cap[i] > asz)))
 		f |= SPF_BAD;
+	if (L >= in.maxlen)
+		f |= SPF_SIZE;
 	uint32_t ix, E;
 	if (in.prot) {
 		if (cap && (uint64_t)end[i] + in.need > (uint64_t)cap[i])

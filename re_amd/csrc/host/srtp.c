@@ -3538,6 +3538,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 	in.hmac = (uint32_t)c0->has_hmac;
 	in.encrypted = (uint32_t)(gcm ? c0->encrypted : c0->has_aes);
 	in.need = grow;
+	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	{
 		/* parse (+ E || index words) + end copy + zeroed counters and
 		 * plan + comp map, one launch */

@@ -212,9 +212,9 @@ struct sgpu_plan_in {
 
 /* compact (counter-cached) kernels take packets shorter than this:
  * AES-CM caches rounds 1-2 for block indices < 256 (kern_common.h CtrKs,
- * CTR_B15), GCM for counters < 65536 */
+ * CTR_B15), the single-key GCM kernel for counters < 256 (GCMU_B8) */
 #define SGPU_CACHED_MAX_CTR (4096u - 64u)
-#define SGPU_CACHED_MAX_GCM ((1u << 20) - 64u)
+#define SGPU_CACHED_MAX_GCM (4096u - 64u)
 #define SGPU_CACHED_MAX(mode) \
 	((mode) == SGPU_MODE_GCM ? SGPU_CACHED_MAX_GCM : SGPU_CACHED_MAX_CTR)
 
@@ -417,6 +417,9 @@ struct sgpu_rplan_in {
 	uint32_t encrypted;     /* E for protect (has_aes / encrypted) */
 	uint32_t need;          /* protect: bytes appended */
 	uint64_t lix, bitmap;   /* replay_rtcp */
+	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE
+				   (the counter-cached kernels' bound) */
+	uint32_t pad;
 };
 
 int   sgpu_plan_rtcp(const struct sgpu_rplan_in *in,

@@ -15,6 +15,7 @@ import re_amd.srtp as P
 from re_amd import workload as W
 from tests import oracle_lib as O
 from tests.test_gpu_fastpath import keys_for, to_arena
+from tests.test_gpu_fastpath import run_dev as run_dev_arrays
 
 pytestmark = pytest.mark.gpu
 
@@ -132,3 +133,47 @@ def test_srtcp_fallbacks_vs_oracle(torch_cuda, suite):
     assert run_dev(torch, "srtcp_encrypt", tx, pk) == \
         oracle_run(ob, o2, "srtcp_encrypt", pk)
     assert run_dev(torch, "srtcp_encrypt", tx, pk)[10][0] == errno.EBADMSG
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_srtcp_large_packets(suite, torch_cuda):
+    """SRTCP packets either side of the counter-cached kernels' size bound
+    (SGPU_CACHED_MAX, 4032 B): the device planner sends the large ones to
+    the plain kernels; every packet matches the oracle both ways"""
+    torch = torch_cuda
+    rng = np.random.default_rng(4040 + suite)
+    key = keys_for(suite, 1)[0]
+    lens = [4000, 4028, 4032, 4100, 6000, 200]
+    pkts = []
+    for i in range(24):
+        L = lens[i % len(lens)]
+        b = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        b[0], b[1] = 0x80, 200
+        b[2], b[3] = ((L // 4 - 1) >> 8) & 0xff, (L // 4 - 1) & 0xff
+        b[4:8] = (0x5150).to_bytes(4, "big")
+        pkts.append((0, bytes(b)))
+    arena, pos, end, cap, _ = to_arena(pkts)
+    tx, rx = P.Srtp(suite, key), P.Srtp(suite, key)
+    a = run_dev_arrays(torch, "srtcp_encrypt", [tx], arena, pos, end, cap,
+                       None)
+    be = O.OracleBackend()
+    octx = be.alloc(suite, key, 0)[0]
+    orx = be.alloc(suite, key, 0)[0]
+    prot = []
+    for i, (_, p) in enumerate(pkts):
+        e, po, en, _, buf = be.call(octx, "srtcp_encrypt", len(p) + 64, 0,
+                                    len(p), p, len(p) + 20)
+        assert (int(a[3][i]), int(a[2][i] - pos[i])) == (e, en), i
+        assert a[0][pos[i]:a[2][i]].tobytes() == buf[:en], (i, len(p))
+        prot.append((0, bytes(buf[:en])))
+    a2, p2, e2, c2, _ = to_arena(prot)
+    d = run_dev_arrays(torch, "srtcp_decrypt", [rx], a2, p2, e2, c2, None)
+    for i, (_, p) in enumerate(prot):
+        e, po, en, _, buf = be.call(orx, "srtcp_decrypt", len(p) + 64, 0,
+                                    len(p), p, len(p))
+        assert (int(d[3][i]), int(d[2][i] - p2[i])) == (e, en), i
+        assert d[0][p2[i]:p2[i] + en].tobytes() == buf[:en], i
+    be.free(octx)
+    be.free(orx)
+    tx.close()
+    rx.close()

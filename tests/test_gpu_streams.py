@@ -320,3 +320,42 @@ def test_streams_edge_shapes(suite, torch_cuda):
         return saved + rp               # ... received again first
     out, _ = run_both([b1, b2], [SSRC0, SSRC0 + 1], rx_mutate=replay_last)
     assert errno.EALREADY in {int(x) for x in out[3][3]}
+
+
+def test_streams_full_size(torch_cuda):
+    """BASELINE size through the per-stream planner: 1M x 1200-B packets of
+    one session over two SSRCs (bench.py --ssrcs 2: packet i on stream
+    i mod 2, each stream's seq from 65000 -- eight ROC wraps), protect and
+    unprotect, against the general engine: the whole arena, every end and
+    errno, both streams' final states"""
+    import hashlib
+    from re_amd import workload as W
+    torch = torch_cuda
+    n = 1 << 20
+    arena, pos, end, cap = W.make_arena(
+        n, 1200, s0=65000, sess=np.arange(n, dtype=np.uint32) % 2)
+    key = keys_for(1, 1)[0]
+    ssrcs = [W.SSRC_BASE, W.SSRC_BASE + 1]
+    res = {}
+    for mode in ("plan", "general"):
+        knobs = {"plan": {}, "general": {"general": 1}}[mode]
+        tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+        s0 = P.counter("splans")
+        with P.tune(**knobs):
+            a, p, e, err = run_dev(torch, "srtp_encrypt", [tx], arena, pos,
+                                   end, cap, None)
+            assert not err.any()
+            d, p2, e2, err2 = run_dev(torch, "srtp_decrypt", [rx], a, pos,
+                                      e, cap, None)
+            assert not err2.any()
+        if mode == "plan":
+            assert P.counter("splans") - s0 == 2
+        res[mode] = (hashlib.sha256(a.tobytes()).hexdigest(),
+                     hashlib.sha256(e.tobytes()).hexdigest(),
+                     hashlib.sha256(d.tobytes()).hexdigest(),
+                     hashlib.sha256(e2.tobytes()).hexdigest(),
+                     states([tx], ssrcs), states([rx], ssrcs))
+        tx.close()
+        rx.close()
+    assert res["plan"] == res["general"]
+    assert (d.reshape(n, -1)[:, :1200] == arena.reshape(n, -1)[:, :1200]).all()

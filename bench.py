@@ -116,6 +116,94 @@ def cpu_baseline(cfg, rtcp=False):
             "sample": "%d pairs through the portable C restatement" % n}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(nranks):
+    """`bench.py --gpus N` with no launcher: start the N ranks ourselves,
+    one child process per GPU, each with RANK/LOCAL_RANK/WORLD_SIZE/
+    MASTER_ADDR/MASTER_PORT set exactly as torch.distributed.run would.
+    The parent never touches the GPU (no torch import here): every child
+    initialises HIP itself.  Children inherit stdout, so rank 0's JSON line
+    is this command's output.  If any rank fails the others are stopped and
+    the parent exits non-zero."""
+    env0 = dict(os.environ)
+    env0.setdefault("MASTER_ADDR", "127.0.0.1")
+    env0.setdefault("MASTER_PORT", str(_free_port()))
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(nranks):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                   GROUP_RANK="0", ROLE_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                print("bench.py: rank %d exited with %d; stopping the "
+                      "others" % (procs.index(p), r), file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+                stop_at = time.monotonic() + 30
+        if live:
+            if rc and time.monotonic() > stop_at:
+                for q in live:
+                    q.kill()
+            time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """--dry-run (CPU, testing the launcher): the rank plumbing of the
+    sharded run without a GPU -- gloo rendezvous, this rank's shard of the
+    config-5 stream (first seq and imported state, re_amd/shard.py) and
+    the counter / max-time reduction.  Prints a line that says so; it
+    measures nothing."""
+    import torch
+    import torch.distributed as dist
+    from re_amd import shard as S
+    from re_amd import workload as W
+    if world > 1:
+        dist.init_process_group("gloo")
+    n = args.packets or 4096
+    s0 = S.shard_seq0(rank, n, 65000)
+    arena, pos, end, cap = W.make_arena(n, 1200, s0=s0)
+    st = S.shard_state(rank, n, 65000, W.SSRC_BASE, True)
+    seq = int.from_bytes(arena[pos[0] + 2:pos[0] + 4].tobytes(), "big")
+    assert seq == s0, (seq, s0)
+    counters = torch.tensor([n, float((end - pos).sum()), 0.0],
+                            dtype=torch.float64)
+    tmax = torch.tensor([0.001 * (rank + 1)], dtype=torch.float64)
+    S.reduce_results(dist if world > 1 else None, counters, tmax)
+    seen = dist.get_world_size() if world > 1 else 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s",
+                          "n_gpus": world, "dist_world": seen,
+                          "dist_backend": "gloo" if world > 1 else None,
+                          "dry_run": True,
+                          "packets_total": int(counters[0].item()),
+                          "bytes_total": int(counters[1].item()),
+                          "tmax": float(tmax.item()),
+                          "rank0_state": st}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,7 +266,23 @@ def main():
                          "(scripts/pmc_sq_summary.py --json)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary to attach (profiles/*.json)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="testing only (CPU): rank plumbing, no GPU work")
     args = ap.parse_args()
+
+    # ranks: under torch.distributed.run WORLD_SIZE is set and must equal
+    # --gpus; without a launcher, --gpus N > 1 starts the N ranks itself
+    # (before anything here touches the GPU)
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return spawn_ranks(args.gpus)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" %
+              (os.environ["WORLD_SIZE"], args.gpus), file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, int(os.environ.get("WORLD_SIZE", "1")),
+                       int(os.environ.get("RANK", "0")))
 
     import torch
     import torch.distributed as dist
@@ -565,6 +669,8 @@ def main():
         "unit": "GiB/s",
         "mpkt_s": round(tot_pkts / T / 1e6, 4),
         "n_gpus": world,
+        "dist_world": dist.get_world_size() if world > 1 else 1,
+        "dist_backend": dist.get_backend() if world > 1 else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(T / args.steps * 1e3, 3),
@@ -686,4 +792,4 @@ def ctypes_stream(stream):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

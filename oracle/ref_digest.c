@@ -10,8 +10,16 @@
  * receiver contexts, and prints SHA-256 digests of the arena, the end
  * array, the per-packet errnos and the final stream states after each
  * direction.  tests/golden/fullsize_digests.json is this program's output
- * for configs 1-4 (scripts/make_fullsize_digests.sh); the -m gpu tests
- * compare the HIP path's full-size outputs with it.
+ * for configs 1-4 and for the shapes beyond them (scripts/
+ * make_fullsize_digests.sh); the -m gpu tests compare the HIP path's
+ * full-size outputs with it:
+ *
+ *   5  the config-5 stream: 2M x 1200 B, one SSRC (two 1M shards of it)
+ *   6  config 2 over 2 SSRCs of one session (packet i -> SSRC i mod 2,
+ *      per-SSRC seq from 65000)
+ *   7  SRTCP, config-2 arena shape (1M x 1200-B RTCP packets, CM128/HMAC80,
+ *      srtcp_encrypt/srtcp_decrypt, src/srtp/srtcp.c:31-287)
+ *   8  SRTCP, config-3 shape (AEAD_AES_256_GCM)
  *
  *   ref_digest <config> [npkts]
  */
@@ -67,14 +75,21 @@ struct cfg {
 	size_t nsess;
 	unsigned s0;
 	int test_key;
+	unsigned nssrc;         /* SSRCs of session 0: packet i -> i mod nssrc */
+	int rtcp;               /* SRTCP (workload.make_rtcp_arena) */
 };
 
-static const struct cfg CFG[5] = {
-	{0, 0, 0, 0, 0, 0},
-	{1, 1024, 160, 1, 1, 1},
-	{1, 1u << 20, 1200, 1, 65000, 0},
-	{5, 1u << 20, 1200, 1, 65000, 0},
-	{1, 1u << 20, 0, 1u << 16, 65000, 0},
+#define NCFG 9
+static const struct cfg CFG[NCFG] = {
+	{0, 0, 0, 0, 0, 0, 1, 0},
+	{1, 1024, 160, 1, 1, 1, 1, 0},
+	{1, 1u << 20, 1200, 1, 65000, 0, 1, 0},
+	{5, 1u << 20, 1200, 1, 65000, 0, 1, 0},
+	{1, 1u << 20, 0, 1u << 16, 65000, 0, 1, 0},
+	{1, 2u << 20, 1200, 1, 65000, 0, 1, 0},
+	{1, 1u << 20, 1200, 1, 65000, 0, 2, 0},
+	{1, 1u << 20, 1200, 1, 65000, 0, 1, 1},
+	{5, 1u << 20, 1200, 1, 65000, 0, 1, 1},
 };
 
 static void hex(const uint8_t *p, size_t n)
@@ -93,23 +108,32 @@ static void sha(const void *p, size_t n)
 	hex(md, 32);
 }
 
-/* per session: roc u32, s_l u32, replay_rtp lix u64, bitmap u64 (LE) */
-static void states(struct srtp **ctx, size_t nsess, uint32_t ssrc0,
-		   uint8_t *buf)
+/* per stream row k (session k, or stream k of session 0 when nssrc > 1):
+ * roc u32, s_l u32, replay_rtp lix u64, bitmap u64 (LE).  SRTCP rows:
+ * rtcp_index u32, 0, replay_rtcp lix, bitmap */
+static void states(struct srtp **ctx, size_t nrows, int by_stream, int rtcp,
+		   uint32_t ssrc0, uint8_t *buf)
 {
 	size_t k;
-	for (k = 0; k < nsess; k++) {
+	for (k = 0; k < nrows; k++) {
 		struct srtp_stream *st = NULL;
+		struct srtp *c = ctx[by_stream ? 0 : k];
 		uint8_t *o = buf + 24 * k;
 		struct le *le;
 		memset(o, 0, 24);
-		for (le = ctx[k]->streaml.head; le; le = le->next) {
+		for (le = c->streaml.head; le; le = le->next) {
 			struct srtp_stream *x = le->data;
 			if (x->ssrc == ssrc0 + (uint32_t)k)
 				st = x;
 		}
 		if (!st)
 			continue;
+		if (rtcp) {
+			memcpy(o, &st->rtcp_index, 4);
+			memcpy(o + 8, &st->replay_rtcp.lix, 8);
+			memcpy(o + 16, &st->replay_rtcp.bitmap, 8);
+			continue;
+		}
 		memcpy(o, &st->roc, 4);
 		{
 			uint32_t sl = st->s_l;
@@ -122,7 +146,8 @@ static void states(struct srtp **ctx, size_t nsess, uint32_t ssrc0,
 
 static void emit(const char *name, const uint8_t *arena, size_t n,
 		 size_t slot, const uint32_t *end, const int32_t *err,
-		 struct srtp **ctx, size_t nsess, uint8_t *stbuf)
+		 struct srtp **ctx, size_t nrows, int by_stream, int rtcp,
+		 uint8_t *stbuf)
 {
 	size_t b, nerr = 0, i;
 	for (i = 0; i < n; i++)
@@ -142,9 +167,9 @@ static void emit(const char *name, const uint8_t *arena, size_t n,
 	printf(",\"err\":");
 	sha(err, n * 4);
 	printf(",\"nerr\":%zu,\"states\":", nerr);
-	states(ctx, nsess, SSRC_BASE, stbuf);
-	sha(stbuf, 24 * nsess);
-	if (nsess == 1) {
+	states(ctx, nrows, by_stream, rtcp, SSRC_BASE, stbuf);
+	sha(stbuf, 24 * nrows);
+	if (nrows == 1) {
 		printf(",\"state0\":");
 		hex(stbuf, 24);
 	}
@@ -159,21 +184,23 @@ int main(int argc, char **argv)
 {
 	int c = argc > 1 ? atoi(argv[1]) : 0;
 	struct cfg cf;
-	size_t n, slot, maxlen, i, klen;
+	size_t n, slot, maxlen, i, klen, nrows;
 	uint8_t *arena, *keys, *stbuf;
 	uint32_t *pos, *end, *len, *sess, *cnt;
 	int32_t *err;
 	struct srtp **tx, **rx;
 
-	if (c < 1 || c > 4) {
-		fprintf(stderr, "usage: %s <config 1-4> [npkts]\n", argv[0]);
+	if (c < 1 || c >= NCFG) {
+		fprintf(stderr, "usage: %s <config 1-%d> [npkts]\n", argv[0],
+			NCFG - 1);
 		return 2;
 	}
 	cf = CFG[c];
 	n = argc > 2 ? (size_t)atol(argv[2]) : cf.n;
 	klen = keylen[cf.suite] + saltlen[cf.suite];
 	maxlen = cf.length ? cf.length : 1400;
-	slot = (maxlen + 16 + 15) & ~(size_t)15;
+	slot = (maxlen + (cf.rtcp ? 20 : 16) + 15) & ~(size_t)15;
+	nrows = cf.nssrc > 1 ? cf.nssrc : cf.nsess;
 
 	arena = calloc(n, slot);
 	pos = calloc(n, 4);
@@ -181,9 +208,9 @@ int main(int argc, char **argv)
 	len = calloc(n, 4);
 	sess = calloc(n, 4);
 	err = calloc(n, 4);
-	cnt = calloc(cf.nsess, 4);
+	cnt = calloc(cf.nsess > cf.nssrc ? cf.nsess : cf.nssrc, 4);
 	keys = calloc(cf.nsess, klen);
-	stbuf = calloc(cf.nsess, 24);
+	stbuf = calloc(nrows, 24);
 	tx = calloc(cf.nsess, sizeof(*tx));
 	rx = calloc(cf.nsess, sizeof(*rx));
 	if (!arena || !pos || !end || !len || !sess || !err || !cnt || !keys ||
@@ -224,8 +251,13 @@ int main(int argc, char **argv)
 			uint64_t s = xs_init(SEED_PAYLOAD + 2, i);
 			sess[i] = (uint32_t)((xs(&s) >> 32) % cf.nsess);
 		}
-		seq = (uint16_t)(cf.s0 + cnt[sess[i]]++);
-		ssrc = SSRC_BASE + sess[i];
+		{
+			/* stream of the packet: its session, or i mod nssrc */
+			uint32_t k = cf.nssrc > 1 ? (uint32_t)(i % cf.nssrc)
+						  : sess[i];
+			seq = (uint16_t)(cf.s0 + cnt[k]++);
+			ssrc = SSRC_BASE + k;
+		}
 		p[0] = 0x80;
 		p[1] = 0;
 		p[2] = (uint8_t)(seq >> 8);
@@ -235,12 +267,27 @@ int main(int argc, char **argv)
 		p[8] = (uint8_t)(ssrc >> 24); p[9] = (uint8_t)(ssrc >> 16);
 		p[10] = (uint8_t)(ssrc >> 8); p[11] = (uint8_t)ssrc;
 		xs_fill(p + 12, len[i] - 12, SEED_PAYLOAD, i);
+		if (cf.rtcp) {
+			/* workload.make_rtcp_arena: an SR-typed header, length
+			 * field len/4 - 1, SSRC_BASE (bytes 8-11 keep the RTP
+			 * SSRC) */
+			uint16_t w = (uint16_t)(len[i] / 4 - 1);
+			p[0] = 0x80;
+			p[1] = 200;
+			p[2] = (uint8_t)(w >> 8);
+			p[3] = (uint8_t)w;
+			p[4] = (uint8_t)(SSRC_BASE >> 24);
+			p[5] = (uint8_t)(SSRC_BASE >> 16);
+			p[6] = (uint8_t)(SSRC_BASE >> 8);
+			p[7] = (uint8_t)SSRC_BASE;
+		}
 		pos[i] = (uint32_t)(i * slot);
 		end[i] = pos[i] + len[i];
 	}
 
 	printf("{\"config\":%d,\"suite\":%d,\"n\":%zu,\"slot\":%zu,"
-	       "\"nsess\":%zu,\"plain\":", c, cf.suite, n, slot, cf.nsess);
+	       "\"nsess\":%zu,\"nssrc\":%u,\"rtcp\":%d,\"plain\":", c, cf.suite,
+	       n, slot, cf.nsess, cf.nssrc, cf.rtcp);
 	sha(arena, n * slot);
 
 	/* protect every packet in array order, in place (the slot has room
@@ -251,10 +298,12 @@ int main(int argc, char **argv)
 		mb.size = pos[i] + slot;
 		mb.pos = pos[i];
 		mb.end = end[i];
-		err[i] = srtp_encrypt(tx[sess[i]], &mb);
+		err[i] = cf.rtcp ? srtcp_encrypt(tx[sess[i]], &mb)
+				 : srtp_encrypt(tx[sess[i]], &mb);
 		end[i] = (uint32_t)mb.end;
 	}
-	emit("protect", arena, n, slot, end, err, tx, cf.nsess, stbuf);
+	emit("protect", arena, n, slot, end, err, tx, nrows, cf.nssrc > 1,
+	     cf.rtcp, stbuf);
 
 	for (i = 0; i < n; i++) {
 		struct mbuf mb;
@@ -262,10 +311,12 @@ int main(int argc, char **argv)
 		mb.size = pos[i] + slot;
 		mb.pos = pos[i];
 		mb.end = end[i];
-		err[i] = srtp_decrypt(rx[sess[i]], &mb);
+		err[i] = cf.rtcp ? srtcp_decrypt(rx[sess[i]], &mb)
+				 : srtp_decrypt(rx[sess[i]], &mb);
 		end[i] = (uint32_t)mb.end;
 	}
-	emit("unprotect", arena, n, slot, end, err, rx, cf.nsess, stbuf);
+	emit("unprotect", arena, n, slot, end, err, rx, nrows, cf.nssrc > 1,
+	     cf.rtcp, stbuf);
 	printf("}\n");
 
 	for (i = 0; i < cf.nsess; i++) {

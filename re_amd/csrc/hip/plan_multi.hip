@@ -78,9 +78,13 @@ __device__ __forceinline__ bool mp_first(const mp_ctx &c, uint32_t k)
  * every later table access (st, segf, segl) stays in bounds */
 template <typename K>
 __global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, K *kin,
-			  uint32_t n, uint32_t nsess, struct sgpu_plan_out *out)
+			  uint32_t n, uint32_t nsess, struct sgpu_plan_out *out,
+			  uint32_t *segl)
 {
 	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	/* segment ends start as "none" (k_mp_mark fills the touched ones) */
+	for (uint32_t k = i; k < nsess; k += gridDim.x * MP_BLOCK)
+		segl[k] = 0xffffffffu;
 	if (i < n) {
 		const uint32_t s = sess[i];
 		if (s >= nsess)
@@ -523,16 +527,15 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 		return EINVAL;
 	if (phase == 2)
 		goto plan;
-	if (hipMemsetAsync(out, 0, sizeof(*out), st) != hipSuccess ||
-	    hipMemsetAsync(segl, 0xff, (size_t)in->nsess * 4, st) !=
-	    hipSuccess)
+	if (!in->out_zeroed &&
+	    hipMemsetAsync(out, 0, sizeof(*out), st) != hipSuccess)
 		return EIO;
 	/* pex is free until k_mp_mark (the clamped keys), sseq until
 	 * k_mp_count (sorted 16-bit keys) */
 	if (in->nsess <= 65536 && in->key_bits <= 16) {
 		uint16_t *k16 = (uint16_t *)pex, *o16 = (uint16_t *)sseq;
 		hipLaunchKernelGGL(k_mp_iota<uint16_t>, dim3(nb), dim3(MP_BLOCK),
-				   0, st, vin, sess, k16, n, in->nsess, out);
+				   0, st, vin, sess, k16, n, in->nsess, out, segl);
 		if (hipcub::DeviceRadixSort::SortPairs(p, tb, k16, o16, vin,
 						       vout, (int)n, 0,
 						       (int)in->key_bits,
@@ -543,7 +546,7 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 	}
 	else {
 		hipLaunchKernelGGL(k_mp_iota<uint32_t>, dim3(nb), dim3(MP_BLOCK),
-				   0, st, vin, sess, pex, n, in->nsess, out);
+				   0, st, vin, sess, pex, n, in->nsess, out, segl);
 		if (hipcub::DeviceRadixSort::SortPairs(p, tb, pex, kout, vin,
 						       vout, (int)n, 0,
 						       (int)in->key_bits,

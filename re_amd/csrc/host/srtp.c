@@ -3692,7 +3692,9 @@ static int dev_mplanned_issue(struct dcall *k)
 	memset(&in, 0, sizeof(in));
 	in.wchk = (const uint32_t *)(w->mscr.d + scr + n * 4);
 	{
-		struct sgpu_prologue pro = {es_d, nfail_d, NULL, 1, 0, NULL, 0,
+		/* zeroes the plan out too (k_mp_iota ORs into it) */
+		struct sgpu_prologue pro = {es_d, nfail_d, (uint32_t *)po_d, 1,
+					    (uint32_t)(sizeof(*po) / 4), NULL, 0,
 					    (uint32_t *)in.wchk, d->cap,
 					    (uint32_t)prot, T,
 					    prot ? (gcm ? 16u : (T > 4 ? T : 4u))
@@ -3711,6 +3713,7 @@ static int dev_mplanned_issue(struct dcall *k)
 	in.need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
 	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	in.key_bits = bits;
+	in.out_zeroed = 1;
 	/* the sort by session needs no session state: it runs while the
 	 * host walks the sessions */
 	err = sgpu_mplan_rtp_phase(1, &in, hd_d, d->pos, es_d, d->cap,

@@ -342,7 +342,7 @@ struct sgpu_mplan_in {
 	uint32_t need;
 	uint32_t key_bits;      /* bits of the session index */
 	uint32_t maxlen;        /* packets of maxlen bytes or more: SPF_SIZE */
-	uint32_t pad;
+	uint32_t out_zeroed;    /* out already zeroed (sgpu_parse_prologue) */
 	const uint32_t *wchk;   /* or NULL: the window checks (SPF_PARSE,
 				   SIZE, BAD, CAP) were made by the parse
 				   prologue, one word per 256-packet block

@@ -163,12 +163,20 @@ def random_sessions(npkts, nsess, seed=SEED_PAYLOAD + 2):
     return ((v >> np.uint64(32)) % np.uint64(nsess)).astype(np.uint32)
 
 
-# BASELINE.json configs as workloads (oracle/ref_digest.c mirrors this)
+# BASELINE.json configs as workloads (oracle/ref_digest.c mirrors this),
+# plus the full-size shapes beyond them that the reference digests pin:
+#   5  the config-5 stream, 2M packets (two 1M shards of it)
+#   6  config 2 over 2 SSRCs of one session (packet i -> SSRC i mod 2)
+#   7  SRTCP in the config-2 shape, 8  SRTCP in the config-3 shape
 CONFIGS = {
     1: dict(suite=1, n=1024, length=160, nsess=1, s0=1, key=CONFIG1_KEY),
     2: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000),
     3: dict(suite=5, n=1 << 20, length=1200, nsess=1, s0=65000),
     4: dict(suite=1, n=1 << 20, length=None, nsess=1 << 16, s0=65000),
+    5: dict(suite=1, n=2 << 20, length=1200, nsess=1, s0=65000),
+    6: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, nssrc=2),
+    7: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, rtcp=True),
+    8: dict(suite=5, n=1 << 20, length=1200, nsess=1, s0=65000, rtcp=True),
 }
 
 KEY_LEN = {0: 30, 1: 30, 2: 46, 3: 46, 4: 28, 5: 44}
@@ -180,7 +188,15 @@ def build_config(cfg_id, n=None):
     n = n or c["n"]
     lengths = c["length"] if c["length"] else mixed_lengths(n)
     sess = random_sessions(n, c["nsess"]) if c["nsess"] > 1 else None
-    arena, pos, end, cap = make_arena(n, lengths, s0=c["s0"], sess=sess)
+    if c.get("rtcp"):
+        arena, pos, end, cap = make_rtcp_arena(n, lengths)
+    elif c.get("nssrc", 1) > 1:
+        # one session, packet i on stream i mod nssrc (SSRC_BASE + k)
+        arena, pos, end, cap = make_arena(
+            n, lengths, s0=c["s0"],
+            sess=np.arange(n, dtype=np.uint32) % c["nssrc"])
+    else:
+        arena, pos, end, cap = make_arena(n, lengths, s0=c["s0"], sess=sess)
     klen = KEY_LEN[c["suite"]]
     if c.get("key"):
         keys = np.frombuffer(c["key"], dtype=np.uint8).reshape(1, klen)

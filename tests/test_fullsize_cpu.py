@@ -23,7 +23,7 @@ def digests():
     return F.load()
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_workload_matches_reference_generator(digests, cfg):
     ref = digests[cfg]
     arena, pos, end, cap, sess, keys = W.build_config(cfg)

@@ -8,6 +8,8 @@ reference src/srtp compiled from its sources, oracle/ref_digest.c):
   config 3  AEAD_AES_256_GCM,        1M x 1200-B packets, one stream
   config 4  AES_CM_128_HMAC_SHA1_80, 1M packets of 200/1400 B over 64K
             sessions
+  shape 7/8 SRTCP (srtcp_*_batch_dev) over 1M x 1200-B RTCP packets,
+            AES_CM_128_HMAC_SHA1_80 / AEAD_AES_256_GCM
 
 For each config: protect every packet, then unprotect the whole protected
 arena with fresh receivers; after each direction the SHA-256 of the whole
@@ -62,12 +64,18 @@ def run_dev(torch, opname, sessions, arena_d, pos_d, end_d, cap_d, sess_d,
     return err
 
 
-def session_states(ctxs):
+def session_states(ctxs, rtcp=False):
     rows = []
     for k, c in enumerate(ctxs):
         e, st = c.export(W.SSRC_BASE + k)
-        rows.append((st.roc, st.s_l, st.replay_rtp_lix, st.replay_rtp_bitmap)
-                    if e == 0 else (0, 0, 0, 0))
+        if e:
+            rows.append((0, 0, 0, 0))
+        elif rtcp:     # ref_digest.c SRTCP rows: index, replay_rtcp
+            rows.append((st.rtcp_index, 0, st.replay_rtcp_lix,
+                         st.replay_rtcp_bitmap))
+        else:
+            rows.append((st.roc, st.s_l, st.replay_rtp_lix,
+                         st.replay_rtp_bitmap))
     return F.state_bytes(rows)
 
 
@@ -87,12 +95,14 @@ def check_config(torch, ref, cfg):
         tx, rx = [P.Srtp(suite, keys[0].tobytes())], \
                  [P.Srtp(suite, keys[0].tobytes())]
     bad = {}
-    for direction, op, ctxs in (("protect", "srtp_encrypt", tx),
-                                ("unprotect", "srtp_decrypt", rx)):
+    rtcp = bool(ref.get("rtcp"))
+    pfx = "srtcp" if rtcp else "srtp"
+    for direction, op, ctxs in (("protect", pfx + "_encrypt", tx),
+                                ("unprotect", pfx + "_decrypt", rx)):
         err = run_dev(torch, op, ctxs, dev, pos_d, end_d, cap_d, sess_d, n)
         m = F.compare(ref[direction], dev.cpu().numpy(), n, slot,
                       end_d.cpu().numpy().view(np.uint32),
-                      err.cpu().numpy(), session_states(ctxs))
+                      err.cpu().numpy(), session_states(ctxs, rtcp))
         if m:
             bad[direction] = m
     for c in tx + rx:
@@ -100,8 +110,10 @@ def check_config(torch, ref, cfg):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 7, 8])
 def test_fullsize_vs_reference(torch_cuda, digests, cfg):
+    """configs 1-4, and SRTCP arenas of the config-2 / config-3 shape
+    (7, 8: 1M x 1200-B RTCP packets through srtcp_*_batch_dev)"""
     check_config(torch_cuda, digests[cfg], cfg)
 
 

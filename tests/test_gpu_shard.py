@@ -5,7 +5,11 @@ and separately as two 1M-packet shards -- shard 0 by fresh contexts, shard
 1 by fresh contexts that srtp_stream_import() the state re_amd/shard.py
 computes for the boundary (what bench.py --gpus N hands each rank).  The
 shards must produce byte-identical arenas, identical per-packet errnos and
-ends, and the same final exported stream states as the unsharded run.
+ends, and the same final exported stream states as the unsharded run --
+and both must equal the reference itself: whole-arena, end, errno and
+final-state digests of the reference src/srtp over the same 2M-packet
+stream after each direction (tests/golden/fullsize_digests.json shape 5,
+oracle/ref_digest.c).
 """
 import numpy as np
 import pytest
@@ -59,40 +63,63 @@ def state(ctx):
 
 
 def test_two_shards_equal_one_stream(torch_cuda):
+    from tests import fullsize_util as F
     torch = torch_cuda
+    ref = F.load()[5]
     n = 2 * PER
-    arena, pos, end, cap = W.make_arena(n, 1200, s0=S0)
-    key = W.make_keys(1, 30)[0].tobytes()
+    arena, pos, end, cap, _, keys = W.build_config(5)
+    assert ref["n"] == n and F.sha(arena) == ref["plain"]
+    slot = ref["slot"]
+    key = keys[0].tobytes()
     one = torch.from_numpy(arena).cuda()
+    del arena
     two = one.clone()
     end1, end2 = end.copy(), end.copy()
+
+    def st_bytes(ctx):
+        return F.state_bytes([state(ctx)[:2] + state(ctx)[3:]])
 
     # unsharded: one context pair, one call per direction
     tx, rx = P.Srtp(1, key), P.Srtp(1, key)
     e1p = run(torch, "srtp_encrypt", tx, one, pos, end1, cap, 0, n)
+    bad = F.compare(ref["protect"], one.cpu().numpy(), n, slot, end1, e1p,
+                    st_bytes(tx))
+    assert not bad, ("unsharded protect", bad)
     e1u = run(torch, "srtp_decrypt", rx, one, pos, end1, cap, 0, n)
+    bad = F.compare(ref["unprotect"], one.cpu().numpy(), n, slot, end1, e1u,
+                    st_bytes(rx))
+    assert not bad, ("unsharded unprotect", bad)
 
-    # sharded: rank r's contexts start from the closed-form boundary state
-    errs, finals = [], []
+    # sharded: rank r's contexts start from the closed-form boundary state;
+    # all shards protect, then all shards unprotect
+    ctxs = []
     for r in range(2):
-        a, b = r * PER, (r + 1) * PER
-        assert (int(arena[pos[a] + 2]) << 8 | int(arena[pos[a] + 3])) == \
+        a = r * PER
+        assert (int(one[pos[a] + 2]) << 8 | int(one[pos[a] + 3])) == \
             S.shard_seq0(r, PER, S0)
         stx, srx = P.Srtp(1, key), P.Srtp(1, key)
         if r:
             for c, recv in ((stx, False), (srx, True)):
                 assert c.import_(S.shard_state(r, PER, S0, W.SSRC_BASE,
                                                recv, P.StreamState)) == 0
-        ep = run(torch, "srtp_encrypt", stx, two, pos, end2, cap, a, b)
-        eu = run(torch, "srtp_decrypt", srx, two, pos, end2, cap, a, b)
-        errs.append((ep, eu))
-        finals.append((state(stx), state(srx)))
+        ctxs.append((stx, srx))
+    errs = {}
+    for d, (op, k) in enumerate((("srtp_encrypt", 0), ("srtp_decrypt", 1))):
+        errs[op] = np.concatenate([
+            run(torch, op, ctxs[r][k], two, pos, end2, cap, r * PER,
+                (r + 1) * PER) for r in range(2)])
+        direction = ("protect", "unprotect")[d]
+        bad = F.compare(ref[direction], two.cpu().numpy(), n, slot, end2,
+                        errs[op], st_bytes(ctxs[1][k]))
+        assert not bad, ("sharded " + direction, bad)
+    finals = [(state(stx), state(srx)) for stx, srx in ctxs]
+    for stx, srx in ctxs:
         stx.close()
         srx.close()
 
     assert not e1p.any() and not e1u.any()
-    assert np.array_equal(np.concatenate([e[0] for e in errs]), e1p)
-    assert np.array_equal(np.concatenate([e[1] for e in errs]), e1u)
+    assert np.array_equal(errs["srtp_encrypt"], e1p)
+    assert np.array_equal(errs["srtp_decrypt"], e1u)
     assert np.array_equal(end1, end2)
     assert torch.equal(one, two)
     # the last shard ends where the single stream ends
@@ -104,3 +131,30 @@ def test_two_shards_equal_one_stream(torch_cuda):
                              last["replay_rtp_bitmap"])
     tx.close()
     rx.close()
+
+
+def test_bench_spawns_two_gpu_ranks():
+    """`bench.py --gpus 2` without a launcher runs two real ranks (here both
+    on cuda:0 with gloo counters, --same-device): config 5 shards, the
+    round trip verifies on each rank and rank 0 reports n_gpus 2"""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                        "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--same-device", "--packets", "8192",
+                        "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True,
+                       env=env, timeout=180, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines()
+             if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["dist_world"] == 2
+    assert ln["verified_roundtrip"] is True and ln["errors"] == 0
+    assert ln["config"]["workload"].startswith("config5")

@@ -159,3 +159,41 @@ def test_session_hash_shards():
         allk = W.make_keys(nsess * world, 30)
         assert (keys == allk[np.arange(nsess) * world + r]).all()
     assert (seen == 1).all()
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                        "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] +
+                       args, capture_output=True, text=True, env=env,
+                       timeout=timeout, cwd=root)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, [json.loads(ln) for ln in lines], r.stderr
+
+
+def test_bench_spawns_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (the
+    driver's SCALE run calls it that way): the ranks rendezvous, reduce
+    over gloo and rank 0 alone prints one line with n_gpus 2"""
+    rc, lines, err = _bench(["--gpus", "2", "--same-device", "--packets",
+                             "4096", "--dry-run"])
+    assert rc == 0, err
+    assert len(lines) == 1, (lines, err)
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["dist_world"] == 2, ln
+    assert ln["packets_total"] == 2 * 4096
+    assert ln["bytes_total"] == 2 * 4096 * 1200
+    assert ln["tmax"] == 0.002                      # max over the ranks
+    assert ln["rank0_state"]["roc"] == 0
+
+
+def test_bench_world_size_mismatch_fails():
+    rc, lines, err = _bench(["--gpus", "4", "--dry-run"],
+                            {"WORLD_SIZE": "2", "RANK": "0"})
+    assert rc != 0 and not lines and "WORLD_SIZE=2" in err

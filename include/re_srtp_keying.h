@@ -7,8 +7,15 @@
  *   client key | server key | client salt | server salt
  * into the client and server master key||salt that srtp_alloc() takes.
  * These functions do the same for many connections at once: the exporter
- * (RFC 5705 with the (D)TLS 1.2 PRF, RFC 5246 5: P_SHA256) runs on the
- * GPU, and the contexts are set up by the batched srtp_alloc_many().
+ * (RFC 5705 with the (D)TLS 1.2 PRF, RFC 5246 5) runs on the GPU, and the
+ * contexts are set up by the batched srtp_alloc_many().
+ *
+ * The (D)TLS 1.2 PRF hash is the negotiated cipher suite's: P_SHA256 for
+ * most suites, P_SHA384 for the *_SHA384 ones (RFC 5246 5, RFC 5289 3;
+ * OpenSSL's default cipher list, which libre uses unless tls_set_ciphers
+ * is called, tls.c:1185-1209, ranks ECDHE-*-AES256-GCM-SHA384 first).
+ * Each connection names its own in srtp_dtls_secret.prf (what
+ * SSL_CIPHER_get_handshake_digest() of the session's cipher gives).
  */
 #ifndef RE_SRTP_KEYING_H
 #define RE_SRTP_KEYING_H
@@ -19,12 +26,20 @@
 extern "C" {
 #endif
 
+/** PRF hash of a (D)TLS 1.2 connection */
+enum srtp_dtls_prf {
+	SRTP_DTLS_PRF_SHA256 = 0,   /**< default (zero-initialised) */
+	SRTP_DTLS_PRF_SHA384 = 1,   /**< the *_SHA384 cipher suites */
+};
+
 /** the DTLS 1.2 secrets of one connection (SSL_SESSION master key and the
- *  handshake randoms) */
+ *  handshake randoms) and its PRF hash (enum srtp_dtls_prf; another value
+ *  makes the call fail with EINVAL) */
 struct srtp_dtls_secret {
 	uint8_t master[48];
 	uint8_t client_random[32];
 	uint8_t server_random[32];
+	uint32_t prf;
 };
 
 /** key + salt bytes of a suite (the key_bytes srtp_alloc takes); 0 for a

@@ -5,9 +5,11 @@
  * for SSL_export_keying_material(ssl, keymat, 2 * (key + salt),
  * "EXTRACTOR-dtls_srtp", no context) and splits keymat as
  *   client key | server key | client salt | server salt.
- * For (D)TLS 1.2 OpenSSL's exporter is the TLS 1.2 PRF (RFC 5246 5,
- * P_SHA256) over the master secret with seed = label || client_random ||
- * server_random (RFC 5705 4; ssl/t1_enc.c tls1_export_keying_material).
+ * For (D)TLS 1.2 OpenSSL's exporter is the TLS 1.2 PRF (RFC 5246 5) over
+ * the master secret with seed = label || client_random || server_random
+ * (RFC 5705 4; ssl/t1_enc.c tls1_export_keying_material), P_<hash> with
+ * the negotiated suite's handshake digest: SHA-256, or SHA-384 for the
+ * *_SHA384 suites (cases with "prf":1).
  * This program evaluates that PRF with OpenSSL's own implementation
  * (EVP_PKEY_TLS1_PRF, the image's libcrypto) on deterministic inputs and
  * prints the inputs, the keying material and the split keys as JSON
@@ -39,12 +41,13 @@ static void hex(const char *k, const uint8_t *p, size_t n, int comma)
 	printf("\"%s", comma ? "," : "");
 }
 
-static int prf(const uint8_t *secret, size_t slen, const uint8_t *seed,
-	       size_t seedlen, uint8_t *out, size_t outlen)
+static int prf(const EVP_MD *md, const uint8_t *secret, size_t slen,
+	       const uint8_t *seed, size_t seedlen, uint8_t *out,
+	       size_t outlen)
 {
 	EVP_PKEY_CTX *pc = EVP_PKEY_CTX_new_id(EVP_PKEY_TLS1_PRF, NULL);
 	int ok = pc && EVP_PKEY_derive_init(pc) > 0 &&
-		 EVP_PKEY_CTX_set_tls1_prf_md(pc, EVP_sha256()) > 0 &&
+		 EVP_PKEY_CTX_set_tls1_prf_md(pc, md) > 0 &&
 		 EVP_PKEY_CTX_set1_tls1_prf_secret(pc, secret, (int)slen) > 0 &&
 		 EVP_PKEY_CTX_add1_tls1_prf_seed(pc, seed, (int)seedlen) > 0 &&
 		 EVP_PKEY_derive(pc, out, &outlen) > 0;
@@ -63,11 +66,12 @@ int main(void)
 		{5, "SRTP_AEAD_AES_256_GCM", 32, 12},
 	};
 	static const char label[] = "EXTRACTOR-dtls_srtp";
-	int p, c, first = 1;
+	int p, c, h, first = 1;
 
 	printf("{\"generator\":\"oracle/gen_dtls_prf.c (%s EVP_PKEY_TLS1_PRF, "
-	       "SHA-256)\",\"label\":\"%s\",\"cases\":[\n",
+	       "SHA-256 and SHA-384)\",\"label\":\"%s\",\"cases\":[\n",
 	       OPENSSL_VERSION_TEXT, label);
+	for (h = 0; h < 2; h++)
 	for (p = 0; p < 4; p++) {
 		for (c = 0; c < 8; c++) {
 			uint8_t ms[48], cr[32], sr[32], seed[128], km[256];
@@ -81,7 +85,8 @@ int main(void)
 			sl = strlen(label);
 			memcpy(seed + sl, cr, 32); sl += 32;
 			memcpy(seed + sl, sr, 32); sl += 32;
-			if (prf(ms, 48, seed, sl, km, 2 * size)) {
+			if (prf(h ? EVP_sha384() : EVP_sha256(), ms, 48, seed,
+				sl, km, 2 * size)) {
 				fprintf(stderr, "PRF failed\n");
 				return 1;
 			}
@@ -91,8 +96,8 @@ int main(void)
 			memcpy(cli + P[p].key, km + 2 * P[p].key, P[p].salt);
 			memcpy(srv + P[p].key, km + 2 * P[p].key + P[p].salt,
 			       P[p].salt);
-			printf("%s{\"suite\":%d,\"profile\":\"%s\",", first ? "" :
-			       ",\n", P[p].suite, P[p].profile);
+			printf("%s{\"suite\":%d,\"profile\":\"%s\",\"prf\":%d,",
+			       first ? "" : ",\n", P[p].suite, P[p].profile, h);
 			first = 0;
 			hex("master", ms, 48, 1);
 			hex("client_random", cr, 32, 1);

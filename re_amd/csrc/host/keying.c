@@ -56,8 +56,8 @@ int srtp_keyinfo_split(enum srtp_suite suite, const uint8_t *keymat,
 	return 0;
 }
 
-int sgpu_dtls_prf(const uint8_t *in, uint32_t n, uint32_t outlen,
-		  uint8_t *out);
+int sgpu_dtls_prf(const uint8_t *in, uint32_t n, uint32_t stride,
+		  uint32_t outlen, uint8_t *out);
 
 int srtp_dtls_keying_many(const struct srtp_dtls_secret *sec, size_t n,
 			  enum srtp_suite suite, uint8_t *cli_keys,
@@ -74,11 +74,15 @@ int srtp_dtls_keying_many(const struct srtp_dtls_secret *sec, size_t n,
 		return ENOSYS;
 	if (!n)
 		return 0;
+	for (i = 0; i < n; i++)
+		if (sec[i].prf != SRTP_DTLS_PRF_SHA256 &&
+		    sec[i].prf != SRTP_DTLS_PRF_SHA384)
+			return EINVAL;
 	km = malloc(n * 2 * size);
 	if (!km)
 		return ENOMEM;
 	err = sgpu_dtls_prf((const uint8_t *)sec, (uint32_t)n,
-			    (uint32_t)(2 * size), km);
+			    (uint32_t)sizeof(*sec), (uint32_t)(2 * size), km);
 	for (i = 0; !err && i < n; i++)
 		err = srtp_keyinfo_split(suite, km + i * 2 * size,
 					 cli_keys + i * size, size,

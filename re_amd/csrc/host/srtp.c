@@ -147,6 +147,10 @@ static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
+/* fault injection (srtp_gpu_tune "fail_grow", like the reference's
+ * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
+ * now fails with ENOMEM */
+static long g_fail_grow;
 
 static void count(uint64_t *c, uint64_t v)
 {
@@ -197,6 +201,9 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.chunk = value >= 64 ? (size_t)value : (size_t)1 << 18;
 	else if (!strcmp(name, "par_min"))
 		g_env.par_min = value > 0 ? (size_t)value : 4096;
+	else if (!strcmp(name, "fail_grow"))
+		__atomic_store_n(&g_fail_grow, value > 0 ? value : 0,
+				 __ATOMIC_RELAXED);
 	else
 		return EINVAL;
 	return 0;
@@ -1202,6 +1209,9 @@ static int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
 	size_t c;
 	if (bytes <= p->cap)
 		return 0;
+	if (__atomic_load_n(&g_fail_grow, __ATOMIC_RELAXED) > 0 &&
+	    __atomic_sub_fetch(&g_fail_grow, 1, __ATOMIC_RELAXED) == 0)
+		return ENOMEM;
 	c = bytes + bytes / 2 + 4096;
 	sgpu_stream_sync(w->stream);
 	sgpu_host_free(p->h);
@@ -2478,6 +2488,11 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 
 	while (bits < 32 && ((size_t)1 << bits) < nsess)
 		bits++;
+	/* the original windows first: the caller restores them from up_h on
+	 * any error below (run_fast's `touched`) */
+	memcpy(up_h, b->pos, n * 4);
+	memcpy(up_h + n, b->end, n * 4);
+	memcpy(up_h + 2 * n, b->sess, n * 4);
 	scr = sgpu_mplan_scratch((uint32_t)n, (uint32_t)nsess);
 	err = pool_reserve(w, &w->ms, nsess * 2 * sizeof(struct sgpu_sstate));
 	if (!err)   /* scratch, then the launch order (n words) */
@@ -2500,9 +2515,6 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 	in.need = need;
 	in.maxlen = SGPU_CACHED_MAX(c0->mode);
 	in.key_bits = bits;
-	memcpy(up_h, b->pos, n * 4);
-	memcpy(up_h + n, b->end, n * 4);
-	memcpy(up_h + 2 * n, b->sess, n * 4);
 	err = sgpu_memcpy_h2d(w->cm.d, w->cm.h, nsess * 4, stream);
 	if (!err)
 		err = sgpu_memcpy_h2d(sin_d, sin_h,

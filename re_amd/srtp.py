@@ -80,7 +80,11 @@ class DtlsSecret(ctypes.Structure):
     """struct srtp_dtls_secret (include/re_srtp_keying.h)"""
     _fields_ = [("master", ctypes.c_uint8 * 48),
                 ("client_random", ctypes.c_uint8 * 32),
-                ("server_random", ctypes.c_uint8 * 32)]
+                ("server_random", ctypes.c_uint8 * 32),
+                ("prf", ctypes.c_uint32)]
+
+
+PRF_SHA256, PRF_SHA384 = 0, 1
 
 
 class StreamState(ctypes.Structure):
@@ -315,12 +319,15 @@ def sockaddr_in(host, port):
 
 
 def dtls_secrets(items):
-    """[(master 48 B, client_random 32 B, server_random 32 B)] -> array"""
+    """[(master 48 B, client_random 32 B, server_random 32 B[, prf])] ->
+    array (prf: PRF_SHA256 (default) or PRF_SHA384)"""
     arr = (DtlsSecret * max(1, len(items)))()
-    for i, (m, c, r) in enumerate(items):
+    for i, it in enumerate(items):
+        m, c, r = it[:3]
         ctypes.memmove(arr[i].master, m, 48)
         ctypes.memmove(arr[i].client_random, c, 32)
         ctypes.memmove(arr[i].server_random, r, 32)
+        arr[i].prf = it[3] if len(it) > 3 else PRF_SHA256
     return arr
 
 

@@ -1,9 +1,10 @@
 """DTLS-SRTP keying on the GPU (include/re_srtp_keying.h, dtls_prf.hip)
 through the C-ABI library:
 
-  * srtp_dtls_keying_many() on all 32 golden connections (OpenSSL's TLS 1.2
-    PRF with the "EXTRACTOR-dtls_srtp" label, split like tls_srtp_keyinfo,
-    src/tls/openssl/tls.c:1083-1157) at once: bit-exact client/server keys;
+  * srtp_dtls_keying_many() on all 64 golden connections (OpenSSL's TLS 1.2
+    PRF with the "EXTRACTOR-dtls_srtp" label, P_SHA256 and P_SHA384, split
+    like tls_srtp_keyinfo, src/tls/openssl/tls.c:1083-1157): bit-exact
+    client/server keys, per PRF and with both PRFs mixed in one call;
   * srtp_alloc_dtls_many(): the client's sender interoperates with the
     server's receiver and back (test/dtls.c:346-368 checks the same with a
     real handshake), and a protected packet equals the oracle's
@@ -41,16 +42,29 @@ def cases():
 
 def items(cs):
     return [(bytes.fromhex(c["master"]), bytes.fromhex(c["client_random"]),
-             bytes.fromhex(c["server_random"])) for c in cs]
+             bytes.fromhex(c["server_random"]), c["prf"]) for c in cs]
 
 
-def test_keying_many_vs_golden(torch_cuda, cases):
+@pytest.mark.parametrize("prf", [0, 1, "mixed"])
+def test_keying_many_vs_golden(torch_cuda, cases, prf):
     for suite in sorted({c["suite"] for c in cases}):
-        cs = [c for c in cases if c["suite"] == suite]
+        cs = [c for c in cases if c["suite"] == suite and
+              (prf == "mixed" or c["prf"] == prf)]
+        if prf == "mixed":          # interleave the two PRFs in one call
+            cs = cs[0::2] + cs[1::2]
+            assert {c["prf"] for c in cs} == {0, 1}
         e, cli, srv = P.dtls_keying_many(suite, items(cs))
         assert e == 0, P.lib().srtp_gpu_error()
         assert [k.hex() for k in cli] == [c["cli_key"] for c in cs]
         assert [k.hex() for k in srv] == [c["srv_key"] for c in cs]
+
+
+def test_keying_bad_prf(torch_cuda, cases):
+    import errno
+    it = items(cases[:2])
+    it[1] = it[1][:3] + (2,)
+    e, _, _ = P.dtls_keying_many(1, it)
+    assert e == errno.EINVAL
 
 
 def rtp(seq, n=200):

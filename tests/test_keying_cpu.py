@@ -24,22 +24,32 @@ def cases():
         return json.load(f)["cases"]
 
 
-def p_sha256(secret, seed, n):
+def p_hash(secret, seed, n, hash_=hashlib.sha256):
     """RFC 5246 5 -- test restatement, not the product (GPU, dtls_prf.hip)"""
     out, a = b"", seed
     while len(out) < n:
-        a = hmac.new(secret, a, hashlib.sha256).digest()
-        out += hmac.new(secret, a + seed, hashlib.sha256).digest()
+        a = hmac.new(secret, a, hash_).digest()
+        out += hmac.new(secret, a + seed, hash_).digest()
     return out[:n]
 
 
+def p_sha256(secret, seed, n):
+    return p_hash(secret, seed, n, hashlib.sha256)
+
+
+def p_sha384(secret, seed, n):
+    return p_hash(secret, seed, n, hashlib.sha384)
+
+
 def test_prf_restatement_vs_openssl(cases):
-    assert len(cases) == 32
+    assert len(cases) == 64
+    assert sorted({c["prf"] for c in cases}) == [0, 1]
     for c in cases:
         seed = b"EXTRACTOR-dtls_srtp" + bytes.fromhex(c["client_random"]) + \
             bytes.fromhex(c["server_random"])
         km = bytes.fromhex(c["keymat"])
-        assert p_sha256(bytes.fromhex(c["master"]), seed, len(km)) == km
+        f = p_sha384 if c["prf"] else p_sha256
+        assert f(bytes.fromhex(c["master"]), seed, len(km)) == km
 
 
 def test_split_vs_golden(cases):

@@ -66,15 +66,49 @@ def cpu_info():
     return nproc, usable, model
 
 
+def cpu_quota():
+    """(cores, source) this process may use: the cgroup CPU quota (v2
+    cpu.max, v1 cpu.cfs_quota_us / cfs_period_us), else the OMP_NUM_THREADS
+    share the box sets for a job, else the affinity mask"""
+    _, usable, _ = cpu_info()
+    for path, parse in (
+            ("/sys/fs/cgroup/cpu.max",
+             lambda t: (t.split()[0], t.split()[1])),
+            ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        if parse:
+            q, p = parse(txt)
+        else:
+            q = txt
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    p = f.read().strip()
+            except OSError:
+                continue
+        if q not in ("max", "-1"):
+            cores = max(1, int(int(q) / int(p)))
+            return min(usable, cores), "%s=%s/%s" % (path, q, p)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        return min(usable, int(omp)), "OMP_NUM_THREADS=%s (no cgroup " \
+            "quota visible)" % omp
+    return usable, "sched_getaffinity"
+
+
 def cpu_baseline(cfg, rtcp=False):
     """Reference src/srtp (oracle/_ref/ref_bench: the reference sources
     compiled with the box's libcrypto) on the host cores, bounded sample,
-    on 1 core and on all usable cores (<= 16: the box's CPU quota), one
-    struct srtp pair per thread; falls back to the portable restatement
-    (kind "port").  A run with errors fails loudly."""
+    on 1 core and on every core this job may use (cpu_quota(): the cgroup
+    quota, or the box's per-job share), one struct srtp pair per thread;
+    falls back to the portable restatement (kind "port").  A run with
+    errors fails loudly."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     nproc, usable, model = cpu_info()
-    threads = max(1, min(16, usable))
+    threads, limit = cpu_quota()
     length = cfg["length"] or 0          # 0 = mixed 200/1400 in ref_bench
     if os.path.exists(ref) and not rtcp:
         runs = {}
@@ -97,6 +131,7 @@ def cpu_baseline(cfg, rtcp=False):
                 "value_1core": round(r1["gib_s"], 4),
                 "mpkt_s_1core": round(r1["mpairs_s"], 4),
                 "kind": "reference", "nproc": nproc, "usable_cores": usable,
+                "cores_limit": limit,
                 "cpu_model": model, "openssl": r.get("openssl"),
                 "sample": "%d protect+unprotect pairs of %s-B RTP packets "
                           "on %d threads (%d pairs on 1), %d session(s) "
@@ -261,11 +296,13 @@ def main():
                          "timed batch (default: announced before it, like "
                          "SDP a=ssrc, by srtp_stream_import of a fresh "
                          "stream state)")
-    ap.add_argument("--sq-json", default=None,
-                    help="SQ-counter summary to attach as int_frac/lds_frac "
-                         "(scripts/pmc_sq_summary.py --json)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC traffic summary to attach (profiles/*.json)")
+                    help="PMC summary (traffic, integer roofline) to "
+                         "attach; default profiles/r03_pmc.json")
+    ap.add_argument("--room", type=int, default=None,
+                    help="A/B: bytes of slack per packet slot (default 16: "
+                         "1216-B slots for 1200-B packets; 80: 1280-B, "
+                         "128-B aligned slots)")
     ap.add_argument("--dry-run", action="store_true",
                     help="testing only (CPU): rank plumbing, no GPU work")
     args = ap.parse_args()
@@ -355,7 +392,8 @@ def main():
         arena_h, pos, end, cap = W.make_arena(
             n, lengths, s0=s0 & 0xffff,
             sess=(gsess if gsess is not None else sess) if K == 1 else
-            np.arange(n, dtype=np.uint32) % K, idx=gidx)
+            np.arange(n, dtype=np.uint32) % K, idx=gidx,
+            room=args.room or 16)
     OPS = ("srtcp_encrypt", "srtcp_decrypt") if args.rtcp else \
         ("srtp_encrypt", "srtp_decrypt")
     log("workload built (%d packets)" % n)
@@ -558,7 +596,7 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    prof = P.prof_read()
+    prof = P.prof_read_named()
     P.prof_enable(False)
     elapsed = t1 - t0
     if use_dev:
@@ -610,49 +648,45 @@ def main():
 
     # ---- roofline of the dominant kernel ----
     kern = []
-    for slot, (ms, launches, jobs) in prof.items():
+    for slot, (ms, launches, jobs, kname) in prof.items():
         prot = slot >= 16
         pkt = jobs / launches
         nbytes = pkt * (2 * L + tag)
         avg_ms = ms / launches
-        kern.append({"slot": slot, "dir": "protect" if prot else "unprotect",
+        kern.append({"slot": slot, "kernel": kname,
+                     "dir": "protect" if prot else "unprotect",
                      "avg_ms": avg_ms, "launches": launches,
                      "pkts_per_launch": pkt, "bytes_per_launch": nbytes,
                      "gbs": nbytes / (avg_ms * 1e-3) / 1e9})
     kern.sort(key=lambda d: -d["avg_ms"] * d["launches"])
     dom = kern[0] if kern else None
-    # HBM bytes per launch of the same kernel, from the committed PMC
-    # passes of this configuration (scripts/gpu_pmc.sh, pmc_summary.py);
-    # scaled if this run's launches carry a different packet count
-    traffic = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles",
-                                           "r02_pmc_traffic.json")
-    sq = None
-    if dom and os.path.exists(tj):
-        ent = json.load(open(tj)).get("config%d" % cfg_id, {}).get(dom["dir"])
-        if ent:
-            traffic = round(ent["traffic_bytes_per_launch"] *
-                            dom["pkts_per_launch"] / ent["grid"])
-    # integer roofline of the same kernel (VALU issue, LDS array), from the
-    # committed SQ-counter passes of this configuration
-    sj = args.sq_json or os.path.join(ROOT, "profiles", "r02_pmc_sq.json")
-    if dom and os.path.exists(sj):
-        sq = json.load(open(sj)).get("config%d" % cfg_id, {}).get(dom["dir"])
+    # HBM traffic and the integer roofline of the SAME kernel on the SAME
+    # workload, from the committed rocprofv3 PMC passes (scripts/
+    # gpu_pmc_r03.sh -> scripts/pmc_r03.py); omitted when no pass matches
+    # the dominant kernel's name and this workload
+    wl = "config%d%s%s%s" % (cfg_id, "_rtcp" if args.rtcp else "",
+                             "_ssrc%d" % K if K > 1 else "",
+                             "_room%d" % args.room if args.room else "")
+    pj = args.traffic_json or os.path.join(ROOT, "profiles", "r03_pmc.json")
+    ent = None
+    if dom and os.path.exists(pj):
+        for e in json.load(open(pj)).get("entries", []):
+            if e["kernel"] == dom["kernel"] and e["workload"] == wl:
+                ent = e
+    scale = dom["pkts_per_launch"] / ent["pkts_per_launch"] if ent else 0
     roof = None
     if dom:
         roof = {"bound": "hbm", "achieved": round(dom["gbs"], 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_src": os.path.basename(tj) if traffic else None,
-                "int_frac": round(sq["valu_frac"], 4) if sq and
-                "valu_frac" in sq else None,
-                "lds_frac": round(sq["lds_frac"], 4) if sq and
-                "lds_frac" in sq else None,
-                "int_src": os.path.basename(sj) if sq else None,
-                "kernel": (("k_ctr_fast_any" if nsess == 1 else "k_ctr_fast_mk")
-                           if (dom["slot"] & 8) == 0 else
-                           ("k_gcmu" if nsess == 1 else "k_gcm")),
+                "traffic": round(ent["traffic_bytes_per_launch"] * scale)
+                if ent and ent.get("traffic_bytes_per_launch") else None,
+                "int_frac": round(ent["int_frac"], 4)
+                if ent and ent.get("int_frac") is not None else None,
+                "lds_frac": round(ent["lds_frac"], 4)
+                if ent and ent.get("lds_frac") is not None else None,
+                "pmc_src": os.path.basename(pj) + ":" + wl if ent else None,
+                "kernel": dom["kernel"],
                 "dir": dom["dir"],
                 "avg_launch_ms": round(dom["avg_ms"], 4),
                 "pkts_per_launch": dom["pkts_per_launch"],
@@ -683,6 +717,7 @@ def main():
                    "packets_per_gpu": n, "pkt_len": cfg["length"] or
                    "200/1400", "suite": P.suite_name(suite),
                    "sessions": nsess, "ssrcs_per_session": K,
+                   "slot_bytes": int(cap[0] - pos[0]),
                    "streams_announced": K > 1 and not args.fresh_streams,
                    "steps_in_flight": 2 if pipelined else 1,
                    "parallelism": "shard%d" % world,

@@ -185,6 +185,11 @@ const char *srtp_gpu_error(void);
 void srtp_gpu_prof(int enable);
 void srtp_gpu_prof_read(double ms[32], uint64_t launches[32],
 			uint64_t jobs[32]);
+/** the same, plus the kernel each slot's launches ran, as
+ *  "name<rounds,protect>" (a trailing '+': launches of other kernels
+ *  shared the slot) */
+void srtp_gpu_prof_read_named(double ms[32], uint64_t launches[32],
+			      uint64_t jobs[32], char names[32][48]);
 
 #ifdef __cplusplus
 }

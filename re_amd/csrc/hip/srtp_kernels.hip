@@ -1028,11 +1028,16 @@ extern "C" int sgpu_setup_sessions(const struct sgpu_keyreq *req,
 #include <pthread.h>
 static pthread_mutex_t g_prof_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_prof_on;
-struct prof_ev { hipEvent_t a, b; int slot; uint32_t jobs; };
+struct prof_ev { hipEvent_t a, b; int slot; uint32_t jobs; const char *name;
+		  int nr, prot; };
 static struct prof_ev *g_pev;
 static size_t g_npev, g_pev_cap;
 static double g_prof_ms[32];
 static uint64_t g_prof_launch[32], g_prof_jobs[32];
+/* the kernel a slot's launches ran ("<name><nr,prot>"; "+" appended when
+ * launches of different kernels shared the slot since the last read) */
+static char g_prof_name[32][SGPU_PROF_NAME];
+static int g_prof_mixed[32];
 
 extern "C" void sgpu_prof_enable(int on)
 {
@@ -1047,9 +1052,17 @@ static void prof_drain_locked(void)
 		float ms = 0;
 		(void)hipEventSynchronize(g_pev[k].b);
 		(void)hipEventElapsedTime(&ms, g_pev[k].a, g_pev[k].b);
-		g_prof_ms[g_pev[k].slot] += ms;
-		g_prof_launch[g_pev[k].slot]++;
-		g_prof_jobs[g_pev[k].slot] += g_pev[k].jobs;
+		const int sl = g_pev[k].slot;
+		char nm[SGPU_PROF_NAME];
+		snprintf(nm, sizeof(nm), "%s<%d,%d>", g_pev[k].name,
+			 g_pev[k].nr, g_pev[k].prot);
+		if (!g_prof_name[sl][0])
+			snprintf(g_prof_name[sl], SGPU_PROF_NAME, "%s", nm);
+		else if (strcmp(g_prof_name[sl], nm))
+			g_prof_mixed[sl] = 1;
+		g_prof_ms[sl] += ms;
+		g_prof_launch[sl]++;
+		g_prof_jobs[sl] += g_pev[k].jobs;
 		(void)hipEventDestroy(g_pev[k].a);
 		(void)hipEventDestroy(g_pev[k].b);
 	}
@@ -1057,7 +1070,8 @@ static void prof_drain_locked(void)
 }
 
 /* slot = prot*16 + mode*8 + (nr==14)*4 + shift; reading resets */
-extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs)
+extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs,
+			       char (*names)[SGPU_PROF_NAME])
 {
 	pthread_mutex_lock(&g_prof_lock);
 	prof_drain_locked();
@@ -1065,14 +1079,20 @@ extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs)
 		if (ms) ms[k] = g_prof_ms[k];
 		if (launches) launches[k] = g_prof_launch[k];
 		if (jobs) jobs[k] = g_prof_jobs[k];
+		if (names)
+			snprintf(names[k], SGPU_PROF_NAME, "%s%s",
+				 g_prof_name[k], g_prof_mixed[k] ? "+" : "");
+		g_prof_mixed[k] = 0;
 		g_prof_ms[k] = 0;
 		g_prof_launch[k] = g_prof_jobs[k] = 0;
+		g_prof_name[k][0] = 0;
 	}
 	pthread_mutex_unlock(&g_prof_lock);
 }
 
 static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
-		  hipStream_t stream, uint32_t block = KBLOCK)
+		  hipStream_t stream, uint32_t block, const char *name,
+		  int nr, int prot)
 {
 	struct prof_ev pe;
 	int prof = 0;
@@ -1089,6 +1109,9 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		(void)hipEventRecord(pe.b, stream);
 		pe.slot = slot;
 		pe.jobs = n;
+		pe.name = name;
+		pe.nr = nr;
+		pe.prot = prot;
 		pthread_mutex_lock(&g_prof_lock);
 		if (g_npev == g_pev_cap) {
 			size_t nc = g_pev_cap ? 2 * g_pev_cap : 64;
@@ -1143,7 +1166,8 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	a.save = save;
 	return launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
 		      (hipStream_t)stream,
-		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK);
+		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK,
+		      mode == SGPU_MODE_GCM ? "k_gcm" : "k_ctr_hmac", nr, prot);
 }
 
 extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
@@ -1168,7 +1192,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		kfn_t ff = nr == 10 ? sgpu_pick_ctr10_fast(prot, 0)
 				    : sgpu_pick_ctr14_fast(prot, 0);
 		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
-			       (hipStream_t)stream, sgpu_ctr_fast_block(prot));
+			       (hipStream_t)stream, sgpu_ctr_fast_block(prot),
+			       "k_ctr_fast_any", nr, prot);
 		if (!e && !prot && c->flist) {
 			/* one workgroup per listed forged packet (grid-
 			 * strided past 1024); all exit at once if none */
@@ -1183,7 +1208,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 			e = launch(nr == 10 ? sgpu_pick_ctr10_fast(0, 1)
 					    : sgpu_pick_ctr14_fast(0, 1),
 				   a, c->n, -1, (hipStream_t)stream,
-				   sgpu_ctr_fast_block(1));
+				   sgpu_ctr_fast_block(1), "k_ctr_fast_restore", nr,
+				   0);
 		return e;
 	}
 	if (mode == SGPU_MODE_CTR && shift < 0 && c->uniform == 3 &&
@@ -1203,7 +1229,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		return launch(nr == 10 ? sgpu_pick_ctr10_fast_mk(prot)
 				       : sgpu_pick_ctr14_fast_mk(prot),
 			      a, c->n, prof_slot(mode, nr, 3, prot),
-			      (hipStream_t)stream, sgpu_ctr_fast_mk_block());
+			      (hipStream_t)stream, sgpu_ctr_fast_mk_block(),
+			      "k_ctr_fast_mk", nr, prot);
 	}
 	kfn_t f = mode == SGPU_MODE_GCM ?
 			  sgpu_pick_gcm(true, c->uniform != 0, nr, prot)
@@ -1228,7 +1255,14 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 					       prot),
 		      (hipStream_t)stream,
 		      mode == SGPU_MODE_GCM ? sgpu_gcm_block(c->uniform != 0)
-					    : sgpu_ctr_block(c->uniform != 0, prot));
+					    : sgpu_ctr_block(c->uniform != 0, prot),
+		      mode == SGPU_MODE_GCM ?
+			      (c->uniform ? "k_gcmu" : "k_gcm_compact") :
+		      shift < 0 ? (c->uniform ? "k_ctr_hmac_any_uni"
+					      : "k_ctr_hmac_any") :
+				  (c->uniform ? "k_ctr_hmac_uni"
+					      : "k_ctr_hmac_compact"),
+		      nr, prot);
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,

@@ -31,6 +31,7 @@
 #include "re_mbuf.h"
 #include "re_srtp.h"
 #include "re_srtp_batch.h"
+#include "re_rtcp_batch.h"
 #include "../srtpgpu.h"
 #include "pool.h"
 
@@ -4339,6 +4340,26 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 	return 0;
 }
 
+/* ---- RTCP compound decode (include/re_rtcp_batch.h) ------------------- */
+
+int rtcp_decode_batch_dev(const uint8_t *arena, size_t arena_size,
+			  const uint32_t *pos, const uint32_t *end, size_t n,
+			  struct rtcp_desc *descv, uint32_t maxmsg,
+			  uint32_t *nmsg, int32_t *err, uint32_t *stop,
+			  void *stream)
+{
+	if (!n)
+		return 0;
+	if (!arena || !pos || !end || !nmsg || !err || !stop ||
+	    (maxmsg && !descv) || n > UINT32_MAX ||
+	    (uint64_t)n * maxmsg > ((uint64_t)1 << 40))
+		return EINVAL;
+	if (!gpu_ready())
+		return ENOSYS;
+	return sgpu_rtcp_walk(arena, arena_size, pos, end, (uint32_t)n, descv,
+			      maxmsg, nmsg, err, stop, stream);
+}
+
 /* ---- diagnostics: per-kernel-class device time (HIP events) ----------- */
 
 void srtp_gpu_prof(int enable)
@@ -4349,5 +4370,11 @@ void srtp_gpu_prof(int enable)
 void srtp_gpu_prof_read(double ms[32], uint64_t launches[32],
 			uint64_t jobs[32])
 {
-	sgpu_prof_read(ms, launches, jobs);
+	sgpu_prof_read(ms, launches, jobs, NULL);
+}
+
+void srtp_gpu_prof_read_named(double ms[32], uint64_t launches[32],
+			      uint64_t jobs[32], char names[32][48])
+{
+	sgpu_prof_read(ms, launches, jobs, names);
 }

@@ -517,7 +517,16 @@ int   sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
 
 /* kernel timing (HIP events recorded on the launch stream) */
 void  sgpu_prof_enable(int on);
-void  sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs);
+/* RTCP compound decode (rtcp_walk.hip, include/re_rtcp_batch.h) */
+struct rtcp_desc;
+int sgpu_rtcp_walk(const uint8_t *arena, uint64_t arena_size,
+		   const uint32_t *pos, const uint32_t *end, uint32_t n,
+		   struct rtcp_desc *descv, uint32_t maxmsg, uint32_t *nmsg,
+		   int32_t *err, uint32_t *stop, void *stream);
+
+#define SGPU_PROF_NAME 48
+void  sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs,
+		     char (*names)[SGPU_PROF_NAME]);
 
 /* memory helpers (device / pinned host) */
 void *sgpu_malloc(size_t n);

@@ -110,7 +110,9 @@ EXPORTS = (
     "srtcp_decrypt_batch_dev", "srtp_encrypt_batch_dev_async",
     "srtp_decrypt_batch_dev_async", "srtp_batch_wait", "srtp_stream_export",
     "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
-    "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_tune", "srtp_gpu_counter",
+    "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_prof_read_named",
+    "srtp_gpu_tune", "srtp_gpu_counter",
+    "rtcp_decode_batch_dev",
     "srtp_udp_alloc", "srtp_udp_recv", "srtp_udp_send", "srtp_udp_stats",
     "srtp_dtls_key_size", "srtp_keyinfo_split", "srtp_dtls_keying_many",
     "srtp_alloc_dtls_many",
@@ -168,6 +170,8 @@ def load():
     L.srtp_gpu_prof_read.argtypes = [ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64),
                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.rtcp_decode_batch_dev.argtypes = [vp, sz, vp, vp, sz, vp,
+                                        ctypes.c_uint32, vp, vp, vp, vp]
     L.srtp_udp_alloc.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, vp,
                                  sz, sz, UDP_RECV_H, vp]
     L.srtp_udp_recv.argtypes = [vp, ctypes.c_int]
@@ -450,6 +454,16 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
                                                  ctypes.byref(b))
 
 
+def rtcp_decode_dev(arena_ptr, arena_size, pos_ptr, end_ptr, n, desc_ptr,
+                    maxmsg, nmsg_ptr, err_ptr, stop_ptr, stream=None):
+    """rtcp_decode_batch_dev (include/re_rtcp_batch.h): every pointer is
+    device memory; desc holds n * maxmsg struct rtcp_desc (5 x uint32:
+    off, size, pt | count << 8 | length << 16, ssrc, aux).  Returns rc."""
+    return lib().rtcp_decode_batch_dev(arena_ptr, arena_size, pos_ptr,
+                                       end_ptr, n, desc_ptr, maxmsg,
+                                       nmsg_ptr, err_ptr, stop_ptr, stream)
+
+
 def device_batch_dev_async(opname, sessions, arena_ptr, arena_size,
                            pos_ptr, end_ptr, cap_ptr, err_ptr, n,
                            sess_ptr=None, stream=None):
@@ -507,11 +521,18 @@ def prof_enable(on=True):
 def prof_read():
     """{slot: (ms, launches, jobs)} for kernel classes that ran.
     slot = protect*16 + gcm*8 + aes256*4 + shift"""
+    return {k: v[:3] for k, v in prof_read_named().items()}
+
+
+def prof_read_named():
+    """{slot: (ms, launches, jobs, kernel name)} (srtp_gpu_prof_read_named)"""
     ms = (ctypes.c_double * 32)()
     la = (ctypes.c_uint64 * 32)()
     jb = (ctypes.c_uint64 * 32)()
-    lib().srtp_gpu_prof_read(ms, la, jb)
-    return {k: (ms[k], la[k], jb[k]) for k in range(32) if la[k]}
+    nm = ((ctypes.c_char * 48) * 32)()
+    lib().srtp_gpu_prof_read_named(ms, la, jb, nm)
+    return {k: (ms[k], la[k], jb[k], nm[k].value.decode())
+            for k in range(32) if la[k]}
 
 
 __all__ = ["errno"]

@@ -42,6 +42,14 @@
 #define A_ADD(x) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "v"(b));
 #define A_BFE(x) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(x));
 #define A_PKADD(x) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(b));
+#define A_LSHL(x) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(x));
+#define A_LSHR(x) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(x));
+#define A_OR(x) asm volatile("v_or_b32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define A_AND(x) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define A_DPP(x) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x));
+#define A_LSHLADD(x) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x) : "v"(b));
+#define A_MIX_PX(x) asm volatile("v_perm_b32 %0, %0, %1, %2\n\tv_xor_b32 %0, %0, %1" : "+v"(x) : "v"(b), "v"(c));
+#define A_MIX_AX(x) asm volatile("v_alignbit_b32 %0, %0, %0, 27\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x) : "v"(b), "v"(c));
 
 DEFK(k_xor, A_XOR)
 DEFK(k_add3, A_ADD3)
@@ -53,6 +61,14 @@ DEFK(k_andor, A_ANDOR)
 DEFK(k_add, A_ADD)
 DEFK(k_bfe, A_BFE)
 DEFK(k_pkadd, A_PKADD)
+DEFK(k_lshl, A_LSHL)
+DEFK(k_lshr, A_LSHR)
+DEFK(k_or, A_OR)
+DEFK(k_and, A_AND)
+DEFK(k_dpp, A_DPP)
+DEFK(k_lshladd, A_LSHLADD)
+DEFK(k_mixpx, A_MIX_PX)
+DEFK(k_mixax, A_MIX_AX)
 
 // LDS: ds_read_b32 from a 32-replica image (conflict-free random reads)
 __global__ void k_lds(uint32_t *out, uint64_t *cyc, uint32_t s)
@@ -87,7 +103,9 @@ typedef void (*kf)(uint32_t *, uint64_t *, uint32_t);
 static void run(const char *name, kf f, int wps, double per_iter_instr,
 		double lds_per_iter)
 {
-	const int cus = 256, threads = 64 * 4 * wps;   // one block per CU
+	// one block per CU up to 4 waves/SIMD, two for 8
+	const int cus = 256 * (wps > 4 ? wps / 4 : 1),
+		  threads = 64 * 4 * (wps > 4 ? 4 : wps);
 	uint32_t *out;
 	uint64_t *cyc;
 	hipMalloc(&out, (size_t)cus * threads * 4);
@@ -123,7 +141,7 @@ static void run(const char *name, kf f, int wps, double per_iter_instr,
 
 int main()
 {
-	int wpss[] = {1, 2, 4};
+	int wpss[] = {1, 2, 4, 8};
 	for (int w : wpss) {
 		run("xor", k_xor, w, 8, 0);
 		run("add", k_add, w, 8, 0);
@@ -135,6 +153,14 @@ int main()
 		run("and_or", k_andor, w, 8, 0);
 		run("bfe", k_bfe, w, 8, 0);
 		run("pk_add", k_pkadd, w, 8, 0);
+		run("lshl", k_lshl, w, 8, 0);
+		run("lshr", k_lshr, w, 8, 0);
+		run("or", k_or, w, 8, 0);
+		run("and", k_and, w, 8, 0);
+		run("dpp_mov", k_dpp, w, 8, 0);
+		run("lshl_add", k_lshladd, w, 8, 0);
+		run("perm+xor", k_mixpx, w, 16, 0);
+		run("align+bitop3", k_mixax, w, 16, 0);
 		run("ds_b32", k_lds, w, 4, 4);
 	}
 	return 0;

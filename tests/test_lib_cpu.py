@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     names = set()
     for h in ("re_srtp.h", "re_srtp_batch.h", "re_srtp_udp.h",
-              "re_srtp_keying.h", "re_mbuf.h", "re_mem.h"):
+              "re_srtp_keying.h", "re_rtcp_batch.h", "re_mbuf.h",
+              "re_mem.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"static inline[^{]*\{[^}]*\}", "", src, flags=re.S)

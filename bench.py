@@ -267,6 +267,11 @@ def main():
                          "DESIGN.md, not the headline value")
     ap.add_argument("--udp-seconds", type=float, default=3.0)
     ap.add_argument("--udp-batch", type=int, default=1024)
+    ap.add_argument("--udp-pairs", type=int, default=4,
+                    help="--udp: socket pairs, each with a sender and a "
+                         "receiver thread")
+    ap.add_argument("--udp-sync", action="store_true",
+                    help="--udp: synchronous helpers (no pipelining)")
     ap.add_argument("--same-device", action="store_true",
                     help="testing only: all ranks on cuda:0, gloo counters")
     ap.add_argument("--sync", action="store_true",
@@ -303,6 +308,12 @@ def main():
                     help="A/B: bytes of slack per packet slot (default 16: "
                          "1216-B slots for 1200-B packets; 80: 1280-B, "
                          "128-B aligned slots)")
+    ap.add_argument("--percall", action="store_true",
+                    help="the unchanged per-packet API: srtp_encrypt + "
+                         "srtp_decrypt of one 1200-B mbuf per call "
+                         "(re_amd/bench/percall.c), latency percentiles "
+                         "and rates, beside the reference on 1 core")
+    ap.add_argument("--percall-calls", type=int, default=20000)
     ap.add_argument("--dry-run", action="store_true",
                     help="testing only (CPU): rank plumbing, no GPU work")
     args = ap.parse_args()
@@ -320,6 +331,8 @@ def main():
     if args.dry_run:
         return dry_run(args, int(os.environ.get("WORLD_SIZE", "1")),
                        int(os.environ.get("RANK", "0")))
+    if args.percall:
+        return percall_bench(args)
 
     import torch
     import torch.distributed as dist
@@ -743,11 +756,14 @@ def main():
 
 
 def udp_bench(args):
-    """Socket-to-socket rate of the batched UDP helper: a sender thread
-    protects config-2 packets (1200 B, AES_CM_128_HMAC_SHA1_80) on the GPU
-    and sendmmsg()s them over loopback; the receiving thread recvmmsg()s,
-    unprotects on the GPU and counts the authentic packets.  Loopback drops
-    what the receiver cannot absorb, so the rate is the receiver's."""
+    """Socket-to-socket rate of the batched UDP helper: --udp-pairs socket
+    pairs, each with a sender thread that protects config-2 packets (1200
+    B, AES_CM_128_HMAC_SHA1_80, its own session) on the GPU and
+    sendmmsg()s them over loopback, and a receiving thread that
+    recvmmsg()s, unprotects on the GPU and counts the authentic packets
+    (pipelined helpers by default: batch k+1 on the socket while batch k
+    is on the GPU).  Loopback drops what a receiver cannot absorb, so the
+    rate is the receivers'.  Per-stage times come from srtp_udp_times."""
     import ctypes
     import socket
     import threading
@@ -757,21 +773,29 @@ def udp_bench(args):
 
     torch.cuda.set_device(0)
     P.load()
-    n = args.packets or (1 << 20)
+    n = args.packets or (1 << 18)
+    T = max(1, args.udp_pairs)
+    pipe = not args.udp_sync
     arena, pos, end, cap = W.make_arena(n, 1200, s0=65000)
-    key = W.make_keys(1, 30)[0].tobytes()
-    a = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-    b = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-    a.bind(("127.0.0.1", 0))
-    b.bind(("127.0.0.1", 0))
-    for sk in (a, b):
-        for opt in (socket.SO_RCVBUF, socket.SO_SNDBUF):
-            sk.setsockopt(socket.SOL_SOCKET, opt, 1 << 26)
-    tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+    keys = W.make_keys(T, 30)
     B = args.udp_batch
-    st = P.SrtpUdp(a.fileno(), tx=tx, batch=B, slot=1280)
-    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=B, slot=1280)
-    assert st.err == 0 and sr.err == 0, P.lib().srtp_gpu_error()
+    pairs = []
+    for t in range(T):
+        a = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        b = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        a.bind(("127.0.0.1", 0))
+        b.bind(("127.0.0.1", 0))
+        for sk in (a, b):
+            for opt in (socket.SO_RCVBUF, socket.SO_SNDBUF):
+                sk.setsockopt(socket.SOL_SOCKET, opt, 1 << 26)
+        key = keys[t].tobytes()
+        tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+        st = P.SrtpUdp(a.fileno(), tx=tx, batch=B, slot=1280, pipeline=pipe)
+        sr = P.SrtpUdp(b.fileno(), rx=rx, batch=B, slot=1280, pipeline=pipe)
+        assert st.err == 0 and sr.err == 0, P.lib().srtp_gpu_error()
+        pairs.append(dict(a=a, b=b, tx=tx, rx=rx, st=st, sr=sr,
+                          addr=P.sockaddr_in(*b.getsockname()), sent=0,
+                          t_end=0.0, last=None))
     base = arena.ctypes.data
     mbs = []
     for i in range(n):                  # mbuf views into the arena
@@ -779,45 +803,98 @@ def udp_bench(args):
         m.buf = ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8))
         m.size, m.pos, m.end = int(cap[i]), int(pos[i]), int(end[i])
         mbs.append(ctypes.pointer(m))
-    addr = P.sockaddr_in(*b.getsockname())
-    sent = [0]
-    t_end = [0.0]
+    chunks = [(ctypes.POINTER(P.Mbuf) * len(mbs[k:k + B]))(*mbs[k:k + B])
+              for k in range(0, n, B)]
 
-    def sender():
-        k = 0
-        deadline = time.perf_counter() + args.udp_seconds
-        while time.perf_counter() < deadline and k < n:
-            r, _ = st.send(addr, mbs[k:k + B])
-            sent[0] += max(r, 0)
-            k += B
-        t_end[0] = time.perf_counter()
+    def sender(pr, deadline):
+        L = P.lib()
+        errs = (ctypes.c_int * B)()
+        for ch in chunks:
+            if time.perf_counter() >= deadline:
+                break
+            r = L.srtp_udp_send(pr["st"].ptr, pr["addr"], len(pr["addr"]),
+                                ch, errs, len(ch))
+            pr["sent"] += max(r, 0)
+        pr["t_end"] = time.perf_counter()
 
-    th = threading.Thread(target=sender)
+    def receiver(pr, done):
+        sr = pr["sr"]
+        while True:
+            got = sr.recv(200)
+            if got > 0:
+                pr["last"] = time.perf_counter()
+            elif done.is_set() and got == 0:
+                break
+
+    done = threading.Event()
     t0 = time.perf_counter()
-    th.start()
-    last = None
-    while True:
-        got = sr.recv(200)
-        if got > 0:
-            last = time.perf_counter()
-        elif not th.is_alive():
-            break
-    th.join()
-    rcv, ok, _ = sr.stats()
-    T = (last or t0) - t0
+    deadline = t0 + args.udp_seconds
+    ths = [threading.Thread(target=sender, args=(pr, deadline))
+           for pr in pairs]
+    rth = [threading.Thread(target=receiver, args=(pr, done))
+           for pr in pairs]
+    for th in rth + ths:
+        th.start()
+    for th in ths:
+        th.join()
+    time.sleep(0.3)
+    done.set()
+    for th in rth:
+        th.join()
+    ok = rcv = sent = 0
+    stages = {}
+    for pr in pairs:
+        r, o, _ = pr["sr"].stats()
+        rcv += r
+        ok += o
+        sent += pr["sent"]
+        for k, v in list(pr["sr"].times().items()) + \
+                list(pr["st"].times().items()):
+            stages[k] = stages.get(k, 0.0) + v
+    last = max([pr["last"] or t0 for pr in pairs])
+    T_s = last - t0
+    send_T = max(pr["t_end"] for pr in pairs) - t0
     line = {"metric": "socket-to-socket SRTP protect+send / recv+unprotect "
                       "over loopback UDP, 1200B RTP pkts (batched UDP helper)",
-            "value": round(ok * 1200 / T / 2**30, 4) if T > 0 else 0.0,
-            "unit": "GiB/s", "mpkt_s": round(ok / T / 1e6, 4) if T else 0.0,
-            "sent": sent[0], "received": rcv, "authentic": ok,
-            "seconds": round(T, 3), "batch": B,
-            "send_side_mpkt_s": round(sent[0] / (t_end[0] - t0) / 1e6, 4),
+            "value": round(ok * 1200 / T_s / 2**30, 4) if T_s > 0 else 0.0,
+            "unit": "GiB/s", "mpkt_s": round(ok / T_s / 1e6, 4) if T_s else
+            0.0, "sent": sent, "received": rcv, "authentic": ok,
+            "seconds": round(T_s, 3), "batch": B, "pairs": T,
+            "pipelined": pipe,
+            "send_side_mpkt_s": round(sent / send_T / 1e6, 4),
+            "stage_seconds_summed_over_threads":
+                {k: round(v, 3) for k, v in stages.items()},
             "data": "synthetic", "dtype": "u8",
             "config": {"workload": "config2 packets over loopback",
                        "suite": "AES_CM_128_HMAC_SHA1_80"}}
     print(json.dumps(line))
-    st.close()
-    sr.close()
+    for pr in pairs:
+        pr["st"].close()
+        pr["sr"].close()
+
+
+def percall_bench(args):
+    """per-packet drop-in path (one mbuf per srtp_encrypt / srtp_decrypt
+    call, what every libre caller does): re_amd/lib/percall, a C driver of
+    libre_srtp_amd.so, then the reference src/srtp on 1 core and on the
+    job's cores for the same packet size"""
+    exe = os.path.join(ROOT, "re_amd", "lib", "percall")
+    threads = sorted({4, 16, 64})
+    out = subprocess.run([exe, str(args.percall_calls)] +
+                         [str(t) for t in threads], capture_output=True,
+                         text=True, timeout=900, check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    line = {"metric": "per-call srtp_encrypt + srtp_decrypt of one 1200-B "
+                      "RTP packet (unchanged re_srtp.h API)",
+            "value": r["pairs_per_s_1thread"], "unit": "pairs/s",
+            "higher_is_better": True, "n_gpus": 1, "data": "synthetic",
+            "dtype": "u8", "percall": r,
+            "config": {"workload": "per-call, AES_CM_128_HMAC_SHA1_80, "
+                                   "1200 B"}}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(CONFIGS[2])
+    print(json.dumps(line))
+    return 0
 
 
 def ctypes_stream(stream):

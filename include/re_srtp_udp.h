@@ -57,15 +57,34 @@ int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
  * most timeout_ms for the first, then taking what is queued), one GPU
  * unprotect of all of them, the handler per datagram.  Returns the number
  * of datagrams handled (0 on timeout) or -errno.
+ *
+ * Pipelined (srtp_udp_pipeline): the round's batch is queued on the GPU
+ * and the previous round's batch is completed and handed to the handler
+ * -- batch k+1 is read from the socket while the GPU unprotects batch k.
+ * A round that receives nothing (timeout) hands over the batch in flight;
+ * handler calls keep datagram order.
  */
 int srtp_udp_recv(struct srtp_udp *su, int timeout_ms);
+
+/**
+ * Pipelining on (on != 0) or off (default) for both directions: two
+ * arenas per direction, asynchronous batch calls (re_srtp_batch.h).
+ * EBUSY while a received batch is still in flight (srtp_udp_recv until it
+ * returns 0 first).
+ */
+int srtp_udp_pipeline(struct srtp_udp *su, int on);
 
 /**
  * Protect mbv[0..n) (one GPU call per `batch` of them) and send each to
  * dst with sendmmsg().  The mbufs are not modified (the protected bytes
  * live in the send arena).  errv (optional): per packet srtp_encrypt()'s
- * errno -- packets with an error are not sent.  Returns the number of
- * datagrams sent or -errno.
+ * errno -- packets with an error are not sent.  Every mbuf is checked
+ * first (NULL, or longer than a slot: -EINVAL, nothing protected).
+ * Returns the number of datagrams sent; if a GPU or socket error stops
+ * the call after some were sent, that number, with errv[] holding the
+ * errno for every packet not sent; -errno if none was sent.  A full
+ * socket buffer is waited on for at most 2 s per sendmmsg.  Pipelined:
+ * chunk j+1 is protected on the GPU while chunk j is sent.
  */
 int srtp_udp_send(struct srtp_udp *su, const struct sockaddr *dst,
 		  socklen_t dstlen, struct mbuf **mbv, int *errv, size_t n);
@@ -73,6 +92,19 @@ int srtp_udp_send(struct srtp_udp *su, const struct sockaddr *dst,
 /** counters: datagrams received / unprotected ok / sent */
 void srtp_udp_stats(const struct srtp_udp *su, uint64_t *rx, uint64_t *rx_ok,
 		    uint64_t *tx);
+
+/** where the time goes (nanoseconds, summed over the helper's life) */
+enum {
+	SRTP_UDP_RX_SYSCALL = 0,  /**< recvmmsg                            */
+	SRTP_UDP_RX_GPU,          /**< waiting for unprotect + copies back  */
+	SRTP_UDP_RX_DELIVER,      /**< the receive handler calls            */
+	SRTP_UDP_TX_STAGE,        /**< mbufs into the pinned send arena     */
+	SRTP_UDP_TX_GPU,          /**< waiting for protect + copies back    */
+	SRTP_UDP_TX_SYSCALL,      /**< sendmmsg                             */
+	SRTP_UDP_NSTAGE
+};
+void srtp_udp_times(const struct srtp_udp *su,
+		    uint64_t ns[SRTP_UDP_NSTAGE]);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,165 @@
+/*
+ * percall.c -- the per-packet drop-in path, measured (bench.py --percall).
+ *
+ * Every existing libre/baresip caller protects and unprotects one mbuf per
+ * call (the reference API, src/srtp/srtp.c:183-432; baresip's SRTP media
+ * helper calls it from the UDP helper chain, one datagram at a time).
+ * This program times exactly that through libre_srtp_amd.so: srtp_encrypt
+ * then srtp_decrypt of one 1200-byte RTP packet per call
+ * (AES_CM_128_HMAC_SHA1_80, seq from 65000), per-call latency percentiles
+ * and the single-thread rate, then T threads with a context pair each
+ * (struct srtp is single-threaded, like the reference's).  Every packet's
+ * round trip is checked.
+ *
+ *   percall <calls per thread> <threads...>   -> one JSON line
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "re_mbuf.h"
+#include "re_mem.h"
+#include "re_srtp.h"
+#include "re_srtp_batch.h"
+
+static double now_us(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e6 + ts.tv_nsec / 1e3;
+}
+
+static int cmpd(const void *a, const void *b)
+{
+	const double x = *(const double *)a, y = *(const double *)b;
+	return x < y ? -1 : x > y;
+}
+
+struct job {
+	long calls;
+	int id;
+	double *lat_e, *lat_d;          /* or NULL */
+	long errors;
+	double t0, t1;
+};
+
+static void *run(void *arg)
+{
+	struct job *j = arg;
+	uint8_t key[30], pkt[1200];
+	struct srtp *tx = NULL, *rx = NULL;
+	struct mbuf *mb = mbuf_alloc(1400);
+	long i;
+	int k;
+
+	for (k = 0; k < 30; k++)
+		key[k] = (uint8_t)(17 * k + j->id);
+	if (!mb || srtp_alloc(&tx, SRTP_AES_CM_128_HMAC_SHA1_80, key, 30, 0) ||
+	    srtp_alloc(&rx, SRTP_AES_CM_128_HMAC_SHA1_80, key, 30, 0)) {
+		j->errors = -1;
+		return NULL;
+	}
+	for (k = 12; k < 1200; k++)
+		pkt[k] = (uint8_t)(k * 7 + j->id);
+	pkt[0] = 0x80;
+	pkt[1] = 0;
+	pkt[8] = 0x0B; pkt[9] = 0xAD; pkt[10] = 0xCA; pkt[11] = (uint8_t)j->id;
+	j->t0 = now_us();
+	for (i = 0; i < j->calls; i++) {
+		const uint16_t seq = (uint16_t)(65000 + i);
+		double a, b, c;
+		pkt[2] = (uint8_t)(seq >> 8);
+		pkt[3] = (uint8_t)seq;
+		pkt[4] = (uint8_t)(i >> 24); pkt[5] = (uint8_t)(i >> 16);
+		pkt[6] = (uint8_t)(i >> 8); pkt[7] = (uint8_t)i;
+		mb->pos = 0;
+		mb->end = 0;
+		memcpy(mb->buf, pkt, sizeof(pkt));
+		mb->end = sizeof(pkt);
+		a = now_us();
+		if (srtp_encrypt(tx, mb))
+			j->errors++;
+		b = now_us();
+		mb->pos = 0;
+		if (srtp_decrypt(rx, mb))
+			j->errors++;
+		c = now_us();
+		if (mb->end != sizeof(pkt) || memcmp(mb->buf, pkt, sizeof(pkt)))
+			j->errors++;
+		if (j->lat_e) {
+			j->lat_e[i] = b - a;
+			j->lat_d[i] = c - b;
+		}
+	}
+	j->t1 = now_us();
+	mem_deref(tx);
+	mem_deref(rx);
+	mem_deref(mb);
+	return NULL;
+}
+
+static double pct(double *v, long n, double p)
+{
+	return v[(long)(p * (n - 1))];
+}
+
+int main(int argc, char **argv)
+{
+	const long calls = argc > 1 ? atol(argv[1]) : 20000;
+	struct job j0;
+	int a;
+
+	/* single thread, latency per call */
+	memset(&j0, 0, sizeof(j0));
+	j0.calls = calls;
+	j0.lat_e = calloc(calls, sizeof(double));
+	j0.lat_d = calloc(calls, sizeof(double));
+	{       /* warm up: workspaces, table, code objects */
+		struct job w = {200, 99, NULL, NULL, 0, 0, 0};
+		run(&w);
+	}
+	run(&j0);
+	if (j0.errors) {
+		fprintf(stderr, "percall: %ld errors (%s)\n", j0.errors,
+			srtp_gpu_error());
+		return 1;
+	}
+	qsort(j0.lat_e, calls, sizeof(double), cmpd);
+	qsort(j0.lat_d, calls, sizeof(double), cmpd);
+	printf("{\"calls\":%ld,\"pkt_len\":1200,"
+	       "\"suite\":\"AES_CM_128_HMAC_SHA1_80\","
+	       "\"encrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
+	       "\"decrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
+	       "\"pairs_per_s_1thread\":%.0f,\"threads\":[",
+	       calls, pct(j0.lat_e, calls, 0.5), pct(j0.lat_e, calls, 0.99),
+	       j0.lat_e[0], pct(j0.lat_d, calls, 0.5),
+	       pct(j0.lat_d, calls, 0.99), j0.lat_d[0],
+	       calls / ((j0.t1 - j0.t0) * 1e-6));
+	for (a = 2; a < argc; a++) {
+		const int T = atoi(argv[a]);
+		struct job *js = calloc(T, sizeof(*js));
+		pthread_t *th = calloc(T, sizeof(*th));
+		double t0 = 1e300, t1 = 0;
+		long err = 0;
+		int t;
+		for (t = 0; t < T; t++) {
+			js[t].calls = calls / 4 > 1000 ? calls / 4 : 1000;
+			js[t].id = t;
+			pthread_create(&th[t], NULL, run, &js[t]);
+		}
+		for (t = 0; t < T; t++) {
+			pthread_join(th[t], NULL);
+			t0 = js[t].t0 < t0 ? js[t].t0 : t0;
+			t1 = js[t].t1 > t1 ? js[t].t1 : t1;
+			err += js[t].errors;
+		}
+		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld}",
+		       a > 2 ? "," : "", T, T * js[0].calls / ((t1 - t0) * 1e-6),
+		       err);
+		free(js);
+		free(th);
+	}
+	printf("]}\n");
+	return 0;
+}

@@ -17,6 +17,8 @@ kfn_t sgpu_pick_ctr10_any(bool uni, int prot)
 /* lean kernels of device-planned single-key batches (k_ctr_fast.h) */
 kfn_t sgpu_pick_ctr10_fast(int prot, int refix)
 {
+	if (refix == 3)         /* multi-session: per-packet keys */
+		return k_ctr_refix_list<10, true>;
 	if (refix == 2)
 		return k_ctr_refix_list<10>;
 	if (refix)

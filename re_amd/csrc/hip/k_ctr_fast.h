@@ -420,7 +420,7 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
  * a full-grid pass where each forged packet runs its whole keystream on
  * one lane.  Bytes [hl, A) only: the ROC at A stays (srtp.c:342-344).
  */
-template <int NR>
+template <int NR, bool MK = false>
 __global__ void __launch_bounds__(256)
 k_ctr_refix_list(const KArgs a)
 {
@@ -431,14 +431,49 @@ k_ctr_refix_list(const KArgs a)
 	tt4_fill(smem, a.t0);
 	__syncthreads();
 	uint32_t rk[4 * (NR + 1)];
-	const struct sgpu_comp *cp = fast_keys<NR>(a, rk);
+	/* MK (multi-session batches): the forged packet's own session
+	 * context, uniform over the workgroup, loaded per packet below */
+	const struct sgpu_comp *cp = MK ? a.comps : fast_keys<NR>(a, rk);
 	const uint32_t lo = (threadIdx.x & 31u) * 4u;
-	const uint32_t T = __builtin_amdgcn_readfirstlane(cp->tag_len);
 	for (uint32_t q = blockIdx.x; q < nf; q += gridDim.x) {
 		const uint32_t p = a.c.flist[q];
 		FastPkt f;
-		if (!fast_pkt(a.c, p - a.c.base, f))
+		if (!MK && !fast_pkt(a.c, p - a.c.base, f))
 			continue;
+		if (MK) {
+			/* the fast kernel walked c.idx (launch order): the
+			 * listed p is a packet index, so read it directly */
+			const uint64_t d = a.c.desc[p];
+			const uint32_t fl = (uint32_t)(d >> 48);
+			if (!(fl & SD_RUN))
+				continue;
+			f.p = p;
+			f.off = a.c.pos[p];
+			f.L = a.c.end[p] - f.off;
+			const uint32_t *hw = (const uint32_t *)(a.c.hdr + p);
+			f.ssrc = hw[0];
+			f.hl = hw[2];
+			f.ixhi = (uint32_t)(d >> 16);
+			f.ixlo = (uint32_t)(d & 0xffffu);
+			f.roc = f.ixhi + ((fl & SD_ROC_P1) ? 1u : 0u) -
+				((fl & SD_ROC_M1) ? 1u : 0u);
+			const uint32_t ci = __builtin_amdgcn_readfirstlane(
+				a.c.compmap[a.c.sess[p]]);
+			cp = a.comps + ci;
+#pragma unroll
+			for (int k = 0; k < NR + 1; k++) {
+				const uint4 v = *(const uint4 *)&cp->rk[4 * k];
+				rk[4 * k] = v.x; rk[4 * k + 1] = v.y;
+				rk[4 * k + 2] = v.z; rk[4 * k + 3] = v.w;
+			}
+#pragma unroll
+			for (int k = 4; k < 4 * NR; k++)
+				rk[k] = rot16(rk[k]);
+#pragma unroll
+			for (int k = 0; k < 4 * (NR + 1); k++)
+				rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
+		}
+		const uint32_t T = __builtin_amdgcn_readfirstlane(cp->tag_len);
 		uint8_t *pkt = a.arena + f.off;
 		const uint32_t A = f.L - T;
 		uint32_t iv[4];

@@ -22,6 +22,10 @@
 #include <stdio.h>
 #include "../srtpgpu.h"
 
+#ifndef EAUTH
+#define EAUTH 217               /* include/re_types.h:215-217 */
+#endif
+
 #define MP_BLOCK 256
 
 __device__ __forceinline__ uint64_t mp_desc(uint64_t ix, uint32_t flags)
@@ -446,6 +450,232 @@ k_mp_oscatter(const uint32_t *pos, const uint32_t *end,
 	}
 }
 
+/*
+ * Verdict fold of a multi-session unprotect (sgpu_mfold_rtp): the
+ * single-stream fold (srtp_kernels.hip k_fold_*) per session segment of
+ * the sorted order.  The planner speculated that every tag verifies; a
+ * forged packet still bumps the ROC on a rollover but never sets s_l
+ * (srtp.c:310-321, 342-359, 426-427), so the packets after it in its
+ * segment may see another s_l than the plan assumed.  Packet k sees the
+ * value left by the last "event" before it in its segment -- an authentic
+ * packet (s_l = seq) or a rollover (s_l = 0 if forged) -- or the
+ * session's stored s_l; the fold checks that every rollover decision,
+ * ETIMEDOUT and index estimate is unchanged under it, and only then
+ * writes the EAUTH results, each touched session's s_l and replay window.
+ * The sort is still in the planner's scratch: val (sorted packet index),
+ * sseq, segf / segl; the session of a sorted position is sess[val[k]].
+ */
+struct mf_ctx {
+	const uint32_t *val, *sess, *sseq, *segf;
+	const struct sgpu_sstate *st;
+	const uint8_t *vd;
+	uint32_t n, nsess;
+};
+
+__device__ __forceinline__ uint32_t mf_key(const mf_ctx &c, uint32_t k)
+{
+	const uint32_t s = c.sess[c.val[k]];
+	return s < c.nsess ? s : c.nsess - 1u;
+}
+
+/* the s_l the segment starts from (stream_get_seq sets it to the first
+ * packet's seq for a new stream, stream.c:87-109) */
+__device__ __forceinline__ uint32_t mf_sl0(const mf_ctx &c, uint32_t s,
+					   uint32_t f)
+{
+	const struct sgpu_sstate &S = c.st[s];
+	return (S.flags & SST_SL_SET) ? S.s_l : c.sseq[f];
+}
+
+__device__ __forceinline__ bool mf_auth(const mf_ctx &c, uint32_t k)
+{
+	return (c.vd[c.val[k]] & SV_TAG_OK) != 0;
+}
+
+/* speculated s_l of position k (segment start f, session s) */
+__device__ __forceinline__ uint32_t mf_sb(const mf_ctx &c, uint32_t k,
+					  uint32_t f, uint32_t s)
+{
+	return k == f ? mf_sl0(c, s, f) : c.sseq[k - 1];
+}
+
+__device__ __forceinline__ bool mf_event(const mf_ctx &c, uint32_t k)
+{
+	const uint32_t s = mf_key(c, k), f = c.segf[s];
+	return mf_auth(c, k) || mp_wrap(c.sseq[k], mf_sb(c, k, f, s));
+}
+
+/* true s_l after event position e (-1 or outside the segment: the
+ * session's start value) */
+__device__ __forceinline__ uint32_t mf_slv(const mf_ctx &c, int32_t e,
+					   uint32_t f, uint32_t s)
+{
+	if (e < (int32_t)f)
+		return mf_sl0(c, s, f);
+	return mf_auth(c, (uint32_t)e) ? c.sseq[e] : 0u;
+}
+
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mf_count(mf_ctx c, int32_t *blast)
+{
+	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	int32_t last = (k < c.n && mf_event(c, k)) ? (int32_t)k : -1;
+	for (int o = 32; o > 0; o >>= 1)
+		last = max(last, __shfl_xor(last, o));
+	__shared__ int32_t wl[MP_BLOCK / 64];
+	if ((threadIdx.x & 63u) == 0)
+		wl[threadIdx.x >> 6] = last;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int32_t m = -1;
+		for (int w = 0; w < MP_BLOCK / 64; w++)
+			m = max(m, wl[w]);
+		blast[blockIdx.x] = m;
+	}
+}
+
+/* exclusive prefix maximum of the block maxima (one workgroup) */
+__global__ void __launch_bounds__(1024)
+k_mf_scan(const int32_t *blast, int32_t *bprev, uint32_t nb)
+{
+	__shared__ int32_t part[1024];
+	const uint32_t per = (nb + 1023u) / 1024u;
+	const uint32_t a = threadIdx.x * per;
+	int32_t m = -1;
+	for (uint32_t k = a; k < a + per && k < nb; k++)
+		m = max(m, blast[k]);
+	part[threadIdx.x] = m;
+	__syncthreads();
+	for (uint32_t d = 1; d < 1024; d <<= 1) {
+		int32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : -1;
+		__syncthreads();
+		part[threadIdx.x] = max(part[threadIdx.x], v);
+		__syncthreads();
+	}
+	int32_t run = threadIdx.x ? part[threadIdx.x - 1] : -1;
+	for (uint32_t k = a; k < a + per && k < nb; k++) {
+		bprev[k] = run;
+		run = max(run, blast[k]);
+	}
+}
+
+/* per sorted position: the speculation under the true s_l; at a
+ * segment's last position, the session's s_l after the batch */
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mf_check(mf_ctx c, const int32_t *bprev, struct sgpu_sstate *st_out,
+	   struct sgpu_fold_out *out)
+{
+	__shared__ int32_t sc[MP_BLOCK];
+	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
+	const bool ev = k < c.n && mf_event(c, k);
+	sc[threadIdx.x] = ev ? (int32_t)k : -1;
+	__syncthreads();
+	for (uint32_t d = 1; d < MP_BLOCK; d <<= 1) {
+		int32_t v = threadIdx.x >= d ? sc[threadIdx.x - d] : -1;
+		__syncthreads();
+		sc[threadIdx.x] = max(sc[threadIdx.x], v);
+		__syncthreads();
+	}
+	if (k >= c.n)
+		return;
+	const int32_t e = max(bprev[blockIdx.x],
+			      threadIdx.x ? sc[threadIdx.x - 1] : -1);
+	const uint32_t s = mf_key(c, k), f = c.segf[s];
+	const uint32_t seq = c.sseq[k];
+	const uint32_t sb = mf_sb(c, k, f, s);          /* speculated */
+	const uint32_t sl = mf_slv(c, e, f, s);         /* true */
+	const bool wrap = mp_wrap(seq, sb);
+	bool bad = mp_wrap(seq, sl) != wrap ||
+		   (int)seq - (int)sl > 32768;          /* ETIMEDOUT */
+	if (!bad && !wrap) {
+		/* same index estimate (misc.c:22-41) at any ROC */
+		bad = mp_v(65536u, sl, seq) != mp_v(65536u, sb, seq);
+		/* an authentic packet sets s_l = seq only if seq > s_l
+		 * (srtp.c:426-427); the events assume it does */
+		if (mf_auth(c, k) && seq < sl)
+			bad = true;
+	}
+	if (bad)
+		atomicOr(&out->fail, 1u);
+	if (k + 1 == c.n || mf_key(c, k + 1) != s)
+		st_out[s].s_l = mf_slv(c, ev ? (int32_t)k : e, f, s);
+}
+
+/* forged packets: EAUTH like srtp_decrypt (srtp.c:342-359, 404-411) */
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mf_results(const uint8_t *vd, const struct sgpu_hdr *hdr,
+	     const uint32_t *end0, uint32_t *pos, uint32_t *end, int32_t *err,
+	     uint32_t n, int gcm, const struct sgpu_fold_out *out)
+{
+	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (i >= n || out->fail || (vd[i] & SV_TAG_OK))
+		return;
+	err[i] = EAUTH;
+	pos[i] += hdr[i].hdr_len;
+	if (gcm)
+		end[i] = end0[i];
+}
+
+/* each touched session's replay window after the batch (replay.c:32-62):
+ * the authentic packets of its segment, every index new and increasing,
+ * so the window after the last authentic one j holds the authentic
+ * packets j-63 .. j (and, close to the segment start, the stored window) */
+__global__ void __launch_bounds__(MP_BLOCK)
+k_mf_final(mf_ctx c, const uint32_t *segl, const uint64_t *desc,
+	   struct sgpu_sstate *st_out, const struct sgpu_fold_out *out)
+{
+	const uint32_t s = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (s >= c.nsess || out->fail)
+		return;
+	const uint32_t l = segl[s];
+	if (l == 0xffffffffu)
+		return;
+	const uint32_t f = c.segf[s];
+	const struct sgpu_sstate &S = c.st[s];
+	int32_t j = (int32_t)l;
+	while (j >= (int32_t)f && !mf_auth(c, (uint32_t)j))
+		j--;
+	uint64_t lix = S.lix, bm = S.bitmap;
+	if (j >= (int32_t)f) {
+		uint32_t q = f;
+		if ((uint32_t)j - f >= 64u) {
+			q = (uint32_t)j - 63u;
+			const uint64_t d = desc[c.val[q - 1]];
+			lix = (d & 0xffffull) | ((d >> 16) & 0xffffffffull) << 16;
+			bm = 0;
+		}
+		for (; q <= (uint32_t)j; q++) {
+			if (!mf_auth(c, q))
+				continue;
+			const uint64_t d = desc[c.val[q]];
+			const uint64_t ix = (d & 0xffffull) |
+					    ((d >> 16) & 0xffffffffull) << 16;
+			if (ix > lix) {
+				const uint64_t dl = ix - lix;
+				bm = dl < 64 ? (bm << dl) | 1ull : 1ull;
+				lix = ix;
+			}
+			else {
+				bm |= 1ull << (lix - ix);
+			}
+		}
+	}
+	st_out[s].lix = lix;
+	st_out[s].bitmap = bm;
+}
+
+__global__ void k_mf_init(struct sgpu_fold_out *out)
+{
+	out->fail = 0;
+	out->nok = 0;
+	out->first_ok = 0xffffffffu;
+	out->last_ok = 0xffffffffu;
+	out->s_l = 0;
+	out->pad = 0;
+	out->lix = 0;
+	out->bitmap = 0;
+}
+
 /* ---- host side ------------------------------------------------------ */
 
 static size_t mp_align(size_t x)
@@ -585,5 +815,56 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 				   st, pos, end, (const uint32_t *)pex, kout,
 				   order, n);
 	}
+	return hipGetLastError() == hipSuccess ? 0 : EIO;
+}
+
+extern "C" size_t sgpu_mfold_scratch(uint32_t n)
+{
+	return 2 * ((size_t)(n + MP_BLOCK - 1) / MP_BLOCK + 2) * 4;
+}
+
+extern "C" int sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
+			      const struct sgpu_hdr *hdr, const uint32_t *sess,
+			      const uint64_t *desc, const uint8_t *verdict,
+			      const uint32_t *end0, uint32_t *pos,
+			      uint32_t *end, int32_t *err, int gcm,
+			      const struct sgpu_sstate *st_in,
+			      struct sgpu_sstate *st_out, void *scratch,
+			      size_t scratch_bytes, uint32_t *fscratch,
+			      struct sgpu_fold_out *out, void *stream)
+{
+	hipStream_t st = (hipStream_t)stream;
+	const uint32_t n = in->n, nb = (n + MP_BLOCK - 1) / MP_BLOCK;
+	uint8_t *p = (uint8_t *)scratch;
+	/* the planner's scratch layout (sgpu_mplan_rtp_phase) */
+	p += mp_align((size_t)n * 4);                                   /* kout */
+	p += mp_align((size_t)n * 4);                                   /* vin */
+	const uint32_t *vout = (const uint32_t *)p;  p += mp_align((size_t)n * 4);
+	p += mp_align((size_t)n * 4);                                   /* pex */
+	const uint32_t *sseq = (const uint32_t *)p;  p += mp_align((size_t)n * 4);
+	p += mp_align((size_t)n * 4);                                   /* sssrc */
+	p += mp_align((size_t)nb * 4 + 64);                             /* bcnt */
+	const uint32_t *segf = (const uint32_t *)p;
+	p += mp_align((size_t)in->nsess * 4);
+	const uint32_t *segl = (const uint32_t *)p;
+	p += mp_align((size_t)in->nsess * 4);
+	if (!n || !in->nsess || (size_t)(p - (uint8_t *)scratch) > scratch_bytes)
+		return EINVAL;
+	int32_t *blast = (int32_t *)fscratch, *bprev = blast + nb + 2;
+	mf_ctx c = {vout, sess, sseq, segf, st_in, verdict, n, in->nsess};
+	hipLaunchKernelGGL(k_mf_init, dim3(1), dim3(1), 0, st, out);
+	hipLaunchKernelGGL(k_mf_count, dim3(nb), dim3(MP_BLOCK), 0, st, c,
+			   blast);
+	hipLaunchKernelGGL(k_mf_scan, dim3(1), dim3(1024), 0, st,
+			   (const int32_t *)blast, bprev, nb);
+	hipLaunchKernelGGL(k_mf_check, dim3(nb), dim3(MP_BLOCK), 0, st, c,
+			   (const int32_t *)bprev, st_out, out);
+	hipLaunchKernelGGL(k_mf_results, dim3(nb), dim3(MP_BLOCK), 0, st,
+			   verdict, hdr, end0, pos, end, err, n, gcm,
+			   (const struct sgpu_fold_out *)out);
+	hipLaunchKernelGGL(k_mf_final,
+			   dim3((in->nsess + MP_BLOCK - 1) / MP_BLOCK),
+			   dim3(MP_BLOCK), 0, st, c, segl, desc, st_out,
+			   (const struct sgpu_fold_out *)out);
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

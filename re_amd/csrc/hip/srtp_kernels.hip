@@ -1226,11 +1226,23 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		a.save = c->save;
 		a.c = *c;
 		a.c.uniform = 0;
-		return launch(nr == 10 ? sgpu_pick_ctr10_fast_mk(prot)
+		int e = launch(nr == 10 ? sgpu_pick_ctr10_fast_mk(prot)
 				       : sgpu_pick_ctr14_fast_mk(prot),
 			      a, c->n, prof_slot(mode, nr, 3, prot),
 			      (hipStream_t)stream, sgpu_ctr_fast_mk_block(),
 			      "k_ctr_fast_mk", nr, prot);
+		if (!e && !prot && c->flist) {
+			/* forged packets back to their ciphertext, each with
+			 * its own session's keys (the device verdict fold of
+			 * multi-session batches); exits at once if none */
+			const uint32_t g = c->n < 1024u ? c->n : 1024u;
+			hipLaunchKernelGGL(nr == 10 ? sgpu_pick_ctr10_fast(0, 3)
+						    : sgpu_pick_ctr14_fast(0, 3),
+					   dim3(g), dim3(256), 0,
+					   (hipStream_t)stream, a);
+			e = herr(hipGetLastError(), "refix mk launch");
+		}
+		return e;
 	}
 	kfn_t f = mode == SGPU_MODE_GCM ?
 			  sgpu_pick_gcm(true, c->uniform != 0, nr, prot)

@@ -3666,13 +3666,15 @@ static int dev_mplanned_issue(struct dcall *k)
 	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
 	if (!err)
 		err = pool_reserve(w, &w->dsc, n * 12);
-	if (!err)
-		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)   /* verdict | save | nfail | forged list */
+		err = pool_reserve(w, &w->vs, n * 9 + 72);
 	if (!err)
 		err = pool_reserve(w, &w->cm, nsess * 4);
+	/* pl: plan out | fold out | fold scratch (multi-session fold) */
+	k->foff = (sizeof(struct sgpu_plan_out) + 63) & ~(size_t)63;
 	if (!err)
-		err = pool_reserve(w, &w->pl,
-				   sizeof(struct sgpu_plan_out) + 64);
+		err = pool_reserve(w, &w->pl, k->foff + 64 +
+				   sgpu_mfold_scratch((uint32_t)n));
 	if (!err)
 		err = pool_reserve(w, &w->es, n * 4);
 	if (!err)
@@ -3762,10 +3764,15 @@ static int dev_mplanned_issue(struct dcall *k)
 					   sout_d, desc_d, w->mscr.d, scr, po_d,
 					   order_d, stream);
 	if (!err) {
+		/* unprotect (CTR): forged packets are listed and restored
+		 * behind the kernel, for the device fold (dev_mplanned_finish) */
+		uint32_t *flist_d = (uint32_t *)(w->vs.d +
+						 ((64 + n * 5 + 3) & ~(size_t)3));
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL, 0, NULL};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0,
+			!prot && !gcm && !g_env.nodevfold ? flist_d : NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -3823,8 +3830,49 @@ static int dev_mplanned_finish(struct dcall *k)
 	if (!nfail)
 		return 0;
 	count(&g_cnt_misses, nfail);
+	/* a forged packet: fold the verdicts on the device, per session
+	 * (sgpu_mfold_rtp).  The kernels left each forged packet as
+	 * srtp_decrypt does (HMAC: ciphertext restored, the ROC over the tag;
+	 * GCM: decrypted in place); the fold checks the speculation under the
+	 * true s_l and writes the EAUTH results and the touched sessions'
+	 * states, which then replace the resident ones. */
+	if (!prot && !g_env.nodevfold) {
+		const size_t foff = k->foff;
+		struct sgpu_fold_out *fo = (struct sgpu_fold_out *)(w->pl.h + foff);
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(w->pl.d + foff);
+		struct sgpu_sstate *sin_d = (struct sgpu_sstate *)w->ms.d;
+		struct sgpu_sstate *sout_d = sin_d + k->nsess;
+		struct sgpu_mplan_in in;
+		size_t scr = sgpu_mplan_scratch((uint32_t)n,
+						(uint32_t)k->nsess);
+		memset(&in, 0, sizeof(in));
+		in.n = (uint32_t)n;
+		in.nsess = (uint32_t)k->nsess;
+		err = sgpu_mfold_rtp(&in, hd_d, d->sess, desc_d, vd_d, es_d,
+				     d->pos, d->end, d->err,
+				     c0->mode == SGPU_MODE_GCM, sin_d, sout_d,
+				     w->mscr.d, scr,
+				     (uint32_t *)(w->pl.d + foff + 64), fo_d,
+				     stream);
+		/* commit on the fold's verdict (pad: a zero word) */
+		if (!err)
+			err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
+					      (uint32_t)k->nsess, &fo_d->fail,
+					      &fo_d->pad, stream);
+		if (!err)
+			err = sgpu_memcpy_d2h(fo, fo_d, sizeof(*fo), stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		if (err)
+			return err;
+		if (!fo->fail) {
+			count(&g_cnt_devfolds, 1);
+			return 0;
+		}
+	}
 	count(&g_cnt_folds, 1);
-	/* a forged packet: undo on the device, fold on the host engine */
+	/* undo on the device, fold on the host engine */
 	{
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,

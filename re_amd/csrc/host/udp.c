@@ -7,8 +7,16 @@
  * (src/udp/udp.c:484-507) runs the send hooks (srtp_encrypt) before
  * sendto().  Here a batch of datagrams lands with one recvmmsg() directly
  * in pinned host slots, crosses PCIe in one copy, is unprotected by one
- * srtp_decrypt_batch_dev() call and comes back in one copy; the send side
- * mirrors it with srtp_encrypt_batch_dev() and sendmmsg().
+ * device batch call and comes back in one copy; the send side mirrors it
+ * with the protect batch call and sendmmsg().
+ *
+ * Pipelined mode (srtp_udp_pipeline): two arenas per direction.  Receive:
+ * batch k+1 is read from the socket while the GPU unprotects batch k
+ * (asynchronous batch call, srtp_batch_wait); batch k is handed to the
+ * handler one call later.  Send: chunk j+1 is staged and queued while chunk
+ * j is still on the GPU, and chunk j's datagrams go out while j+1 runs.
+ * Results stay those of srtp_decrypt()/srtp_encrypt() in datagram order
+ * (the asynchronous calls keep issue order on the contexts).
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -17,6 +25,7 @@
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
+#include <time.h>
 #include "re_mem.h"
 #include "re_mbuf.h"
 #include "re_srtp.h"
@@ -24,25 +33,41 @@
 #include "re_srtp_udp.h"
 #include "../srtpgpu.h"
 
-struct dir {                    /* one direction's arena and windows */
+#define SEND_RETRY_MS 2000      /* bound on a full socket buffer */
+
+struct dir {                    /* one arena: slots, windows, results */
 	uint8_t *h, *d;         /* pinned host / device arena */
 	uint32_t *hw, *dw;      /* pos | end | cap, pinned / device */
 	int32_t *he, *de;       /* per-packet errno, pinned / device */
+	struct mmsghdr *msg;
+	struct iovec *iov;
+	struct sockaddr_storage *src;
+	size_t n;               /* packets staged / in flight */
+	struct srtp_batch_ticket *tk;   /* in flight (pipelined) */
+	struct srtp_batch_dev b;
 };
 
 struct srtp_udp {
 	int fd;
 	struct srtp *rx, *tx;
 	size_t batch, slot;
-	struct dir in, out;
-	struct mmsghdr *msg;
-	struct iovec *iov;
-	struct sockaddr_storage *src;
-	void *stream;
+	struct dir in[2], out[2];
+	int pipeline;
+	int rcur;               /* receive arena to fill next */
+	int rpend;              /* receive arena in flight, or -1 */
+	void *stream, *cstream; /* batch calls / result copies */
 	srtp_udp_recv_h *rh;
 	void *arg;
 	uint64_t n_rx, n_rx_ok, n_tx;
+	uint64_t ns[SRTP_UDP_NSTAGE];
 };
+
+static uint64_t now_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 static void dir_free(struct dir *d)
 {
@@ -52,6 +77,9 @@ static void dir_free(struct dir *d)
 	sgpu_free(d->d);
 	sgpu_free(d->dw);
 	sgpu_free(d->de);
+	free(d->msg);
+	free(d->iov);
+	free(d->src);
 }
 
 static int dir_alloc(struct dir *d, size_t batch, size_t slot)
@@ -62,20 +90,33 @@ static int dir_alloc(struct dir *d, size_t batch, size_t slot)
 	d->dw = sgpu_malloc(batch * 12);
 	d->he = sgpu_host_alloc(batch * 4);
 	d->de = sgpu_malloc(batch * 4);
-	return d->h && d->d && d->hw && d->dw && d->he && d->de ? 0 : ENOMEM;
+	d->msg = calloc(batch, sizeof(*d->msg));
+	d->iov = calloc(batch, sizeof(*d->iov));
+	d->src = calloc(batch, sizeof(*d->src));
+	return d->h && d->d && d->hw && d->dw && d->he && d->de && d->msg &&
+	       d->iov && d->src ? 0 : ENOMEM;
 }
 
 static void destructor(void *arg)
 {
 	struct srtp_udp *su = arg;
+	int k;
+	for (k = 0; k < 2; k++) {
+		if (su->in[k].tk)
+			(void)srtp_batch_wait(su->in[k].tk);
+		if (su->out[k].tk)
+			(void)srtp_batch_wait(su->out[k].tk);
+	}
 	if (su->stream)
 		sgpu_stream_sync(su->stream);
-	dir_free(&su->in);
-	dir_free(&su->out);
+	if (su->cstream)
+		sgpu_stream_sync(su->cstream);
+	for (k = 0; k < 2; k++) {
+		dir_free(&su->in[k]);
+		dir_free(&su->out[k]);
+	}
 	sgpu_stream_destroy(su->stream);
-	free(su->msg);
-	free(su->iov);
-	free(su->src);
+	sgpu_stream_destroy(su->cstream);
 }
 
 int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
@@ -83,7 +124,7 @@ int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
 		   srtp_udp_recv_h *rh, void *arg)
 {
 	struct srtp_udp *su;
-	int err;
+	int err, k;
 
 	if (!sup || fd < 0 || !batch || batch > (1u << 20) || slot < 64 ||
 	    slot > 65536 || (!rx && !tx))
@@ -101,19 +142,19 @@ int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
 	su->slot = slot;
 	su->rh = rh;
 	su->arg = arg;
+	su->rpend = -1;
 	su->stream = sgpu_stream_create();
-	su->msg = calloc(batch, sizeof(*su->msg));
-	su->iov = calloc(batch, sizeof(*su->iov));
-	su->src = calloc(batch, sizeof(*su->src));
-	if (!su->stream) {
+	su->cstream = su->stream ? sgpu_stream_create() : NULL;
+	if (!su->stream || !su->cstream) {
 		err = ENOSYS;           /* no usable HIP device */
 		goto out;
 	}
-	err = dir_alloc(&su->in, batch, slot);
-	if (!err)
-		err = dir_alloc(&su->out, batch, slot);
-	if (!err && (!su->msg || !su->iov || !su->src))
-		err = ENOMEM;
+	err = 0;
+	for (k = 0; k < 2 && !err; k++) {
+		err = dir_alloc(&su->in[k], batch, slot);
+		if (!err)
+			err = dir_alloc(&su->out[k], batch, slot);
+	}
  out:
 	if (err)
 		mem_deref(su);
@@ -122,14 +163,22 @@ int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
 	return err;
 }
 
-/* one GPU call over n packets laid out in d's slots: windows up, batch,
- * arena and results down (the caller's stream, one sync) */
-static int gpu_batch(struct srtp_udp *su, struct dir *d, size_t n,
-		     int (*fn)(struct srtp **, size_t, struct srtp_batch_dev *),
+int srtp_udp_pipeline(struct srtp_udp *su, int on)
+{
+	if (!su)
+		return EINVAL;
+	if (su->rpend >= 0 || su->in[0].tk || su->in[1].tk)
+		return EBUSY;   /* a receive batch is in flight: flush first */
+	su->pipeline = on != 0;
+	return 0;
+}
+
+/* windows + arena up, then the batch call (asynchronous when pipelined) */
+static int gpu_issue(struct srtp_udp *su, struct dir *d, int prot,
 		     struct srtp *ctx)
 {
-	struct srtp_batch_dev b;
-	size_t used = n * su->slot;
+	struct srtp_batch_dev *b = &d->b;
+	const size_t n = d->n, used = n * su->slot;
 	int err;
 
 	err = sgpu_memcpy_h2d(d->d, d->h, used, su->stream);
@@ -137,75 +186,92 @@ static int gpu_batch(struct srtp_udp *su, struct dir *d, size_t n,
 		err = sgpu_memcpy_h2d(d->dw, d->hw, n * 12, su->stream);
 	if (err)
 		return err;
-	memset(&b, 0, sizeof(b));
-	b.arena = d->d;
-	b.arena_size = used;
-	b.pos = d->dw;
-	b.end = d->dw + n;
-	b.cap = d->dw + 2 * n;
-	b.err = d->de;
-	b.n = n;
-	b.stream = su->stream;
-	err = fn(&ctx, 1, &b);
+	memset(b, 0, sizeof(*b));
+	b->arena = d->d;
+	b->arena_size = used;
+	b->pos = d->dw;
+	b->end = d->dw + n;
+	b->cap = d->dw + 2 * n;
+	b->err = d->de;
+	b->n = n;
+	b->stream = su->stream;
+	if (su->pipeline)
+		return prot ? srtp_encrypt_batch_dev_async(&ctx, 1, b, &d->tk)
+			    : srtp_decrypt_batch_dev_async(&ctx, 1, b, &d->tk);
+	return prot ? srtp_encrypt_batch_dev(&ctx, 1, b)
+		    : srtp_decrypt_batch_dev(&ctx, 1, b);
+}
+
+/* ... its completion, then arena, windows and results down (on the copy
+ * stream when pipelined: the next batch may already run on the other) */
+static int gpu_finish(struct srtp_udp *su, struct dir *d, int stage)
+{
+	const size_t n = d->n, used = n * su->slot;
+	void *st = su->pipeline ? su->cstream : su->stream;
+	const uint64_t t0 = now_ns();
+	int err = 0;
+
+	if (d->tk) {
+		err = srtp_batch_wait(d->tk);
+		d->tk = NULL;
+	}
 	if (!err)
-		err = sgpu_memcpy_d2h(d->h, d->d, used, su->stream);
+		err = sgpu_memcpy_d2h(d->h, d->d, used, st);
 	if (!err)
-		err = sgpu_memcpy_d2h(d->hw, d->dw, n * 8, su->stream);
+		err = sgpu_memcpy_d2h(d->hw, d->dw, n * 8, st);
 	if (!err)
-		err = sgpu_memcpy_d2h(d->he, d->de, n * 4, su->stream);
+		err = sgpu_memcpy_d2h(d->he, d->de, n * 4, st);
 	if (!err)
-		err = sgpu_stream_sync(su->stream);
+		err = sgpu_stream_sync(st);
+	su->ns[stage] += now_ns() - t0;
 	return err;
 }
 
-int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
+/* recvmmsg into d (non-blocking); number of datagrams or -errno */
+static int rx_read(struct srtp_udp *su, struct dir *d)
 {
-	struct dir *d;
-	struct pollfd pfd;
+	const uint64_t t0 = now_ns();
 	size_t i, n;
-	int r, err;
+	int r;
 
-	if (!su || !su->rx)
-		return -EINVAL;
-	d = &su->in;
-	pfd.fd = su->fd;
-	pfd.events = POLLIN;
-	r = poll(&pfd, 1, timeout_ms);
-	if (r < 0)
-		return -errno;
-	if (r == 0)
-		return 0;
 	for (i = 0; i < su->batch; i++) {
-		su->iov[i].iov_base = d->h + i * su->slot;
-		su->iov[i].iov_len = su->slot;
-		memset(&su->msg[i].msg_hdr, 0, sizeof(su->msg[i].msg_hdr));
-		su->msg[i].msg_hdr.msg_iov = &su->iov[i];
-		su->msg[i].msg_hdr.msg_iovlen = 1;
-		su->msg[i].msg_hdr.msg_name = &su->src[i];
-		su->msg[i].msg_hdr.msg_namelen = sizeof(su->src[i]);
+		d->iov[i].iov_base = d->h + i * su->slot;
+		d->iov[i].iov_len = su->slot;
+		memset(&d->msg[i].msg_hdr, 0, sizeof(d->msg[i].msg_hdr));
+		d->msg[i].msg_hdr.msg_iov = &d->iov[i];
+		d->msg[i].msg_hdr.msg_iovlen = 1;
+		d->msg[i].msg_hdr.msg_name = &d->src[i];
+		d->msg[i].msg_hdr.msg_namelen = sizeof(d->src[i]);
 	}
-	r = recvmmsg(su->fd, su->msg, (unsigned)su->batch, MSG_DONTWAIT,
-		     NULL);
+	r = recvmmsg(su->fd, d->msg, (unsigned)su->batch, MSG_DONTWAIT, NULL);
+	su->ns[SRTP_UDP_RX_SYSCALL] += now_ns() - t0;
 	if (r < 0)
 		return (errno == EAGAIN || errno == EWOULDBLOCK) ? 0 : -errno;
 	n = (size_t)r;
 	for (i = 0; i < n; i++) {
 		const uint32_t base = (uint32_t)(i * su->slot);
-		uint32_t len = su->msg[i].msg_len;
-		if (su->msg[i].msg_hdr.msg_flags & MSG_TRUNC)
-			len = 0;        /* reported as EMSGSIZE below */
+		uint32_t len = d->msg[i].msg_len;
+		if (d->msg[i].msg_hdr.msg_flags & MSG_TRUNC)
+			len = 0;        /* reported as EMSGSIZE */
 		d->hw[i] = base;
 		d->hw[n + i] = base + len;
 		d->hw[2 * n + i] = base + (uint32_t)su->slot;
 	}
-	err = gpu_batch(su, d, n, srtp_decrypt_batch_dev, su->rx);
-	if (err)
-		return -err;
+	d->n = n;
+	return (int)n;
+}
+
+static void rx_deliver(struct srtp_udp *su, struct dir *d)
+{
+	const uint64_t t0 = now_ns();
+	const size_t n = d->n;
+	size_t i;
+
 	su->n_rx += n;
 	for (i = 0; i < n; i++) {
 		struct mbuf mb;
-		int e = (su->msg[i].msg_hdr.msg_flags & MSG_TRUNC) ? EMSGSIZE
-								   : d->he[i];
+		int e = (d->msg[i].msg_hdr.msg_flags & MSG_TRUNC) ? EMSGSIZE
+								  : d->he[i];
 		mb.buf = d->h;
 		mb.size = (i + 1) * su->slot;
 		mb.pos = d->hw[i];
@@ -213,74 +279,198 @@ int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
 		if (!e)
 			su->n_rx_ok++;
 		if (su->rh)
-			su->rh(&su->src[i], su->msg[i].msg_hdr.msg_namelen, &mb,
+			su->rh(&d->src[i], d->msg[i].msg_hdr.msg_namelen, &mb,
 			       e, su->arg);
 	}
-	return (int)n;
+	d->n = 0;
+	su->ns[SRTP_UDP_RX_DELIVER] += now_ns() - t0;
+}
+
+int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
+{
+	struct dir *d;
+	struct pollfd pfd;
+	int r, n, err, prev, done = 0;
+
+	if (!su || !su->rx)
+		return -EINVAL;
+	d = &su->in[su->rcur];
+	pfd.fd = su->fd;
+	pfd.events = POLLIN;
+	/* a batch in flight: take what is queued now, do not wait */
+	r = poll(&pfd, 1, su->rpend >= 0 ? 0 : timeout_ms);
+	if (r < 0)
+		return -errno;
+	n = r > 0 ? rx_read(su, d) : 0;
+	if (n < 0)
+		return n;
+	prev = su->rpend;
+	su->rpend = -1;
+	if (n > 0) {
+		/* batch k+1 queued behind batch k on the GPU */
+		err = gpu_issue(su, d, 0, su->rx);
+		if (err)
+			return -err;
+		if (su->pipeline) {
+			su->rpend = su->rcur;
+			su->rcur ^= 1;
+		}
+		else {
+			err = gpu_finish(su, d, SRTP_UDP_RX_GPU);
+			if (err)
+				return -err;
+			done = n;
+			rx_deliver(su, d);
+		}
+	}
+	if (prev >= 0) {
+		/* batch k: complete and hand over (k+1 was read meanwhile and
+		 * runs on the GPU now) */
+		struct dir *p = &su->in[prev];
+		err = gpu_finish(su, p, SRTP_UDP_RX_GPU);
+		if (err)
+			return -err;
+		done = (int)p->n;
+		rx_deliver(su, p);
+	}
+	return done;
+}
+
+/* sendmmsg of chunk d's protected datagrams; sent count or -errno */
+static long tx_send(struct srtp_udp *su, struct dir *d,
+		    const struct sockaddr *dst, socklen_t dstlen, int *errv)
+{
+	const uint64_t t0 = now_ns();
+	const size_t m = d->n;
+	size_t i, k, waited = 0;
+
+	for (i = 0, k = 0; i < m; i++) {
+		if (errv)
+			errv[i] = d->he[i];
+		if (d->he[i])
+			continue;
+		d->iov[k].iov_base = d->h + d->hw[i];
+		d->iov[k].iov_len = d->hw[m + i] - d->hw[i];
+		memset(&d->msg[k].msg_hdr, 0, sizeof(d->msg[k].msg_hdr));
+		d->msg[k].msg_hdr.msg_iov = &d->iov[k];
+		d->msg[k].msg_hdr.msg_iovlen = 1;
+		d->msg[k].msg_hdr.msg_name = (void *)dst;
+		d->msg[k].msg_hdr.msg_namelen = dstlen;
+		k++;
+	}
+	for (i = 0; i < k;) {
+		int r = sendmmsg(su->fd, d->msg + i, (unsigned)(k - i), 0);
+		if (r < 0) {
+			if (errno == EINTR)
+				continue;
+			if ((errno == EAGAIN || errno == EWOULDBLOCK ||
+			     errno == ENOBUFS) && waited < SEND_RETRY_MS) {
+				struct pollfd pfd = {su->fd, POLLOUT, 0};
+				(void)poll(&pfd, 1, 10);
+				waited += 10;
+				continue;
+			}
+			su->ns[SRTP_UDP_TX_SYSCALL] += now_ns() - t0;
+			su->n_tx += i;
+			return -errno;
+		}
+		i += (size_t)r;
+	}
+	su->ns[SRTP_UDP_TX_SYSCALL] += now_ns() - t0;
+	su->n_tx += k;
+	return (long)k;
+}
+
+static void tx_stage(struct srtp_udp *su, struct dir *d, struct mbuf **mbv,
+		     size_t m)
+{
+	const uint64_t t0 = now_ns();
+	size_t i;
+	for (i = 0; i < m; i++) {
+		const struct mbuf *mb = mbv[i];
+		const uint32_t base = (uint32_t)(i * su->slot);
+		const size_t len = mb->end > mb->pos ? mb->end - mb->pos : 0;
+		memcpy(d->h + base, mb->buf + mb->pos, len);
+		d->hw[i] = base;
+		d->hw[m + i] = base + (uint32_t)len;
+		d->hw[2 * m + i] = base + (uint32_t)su->slot;
+	}
+	d->n = m;
+	su->ns[SRTP_UDP_TX_STAGE] += now_ns() - t0;
 }
 
 int srtp_udp_send(struct srtp_udp *su, const struct sockaddr *dst,
 		  socklen_t dstlen, struct mbuf **mbv, int *errv, size_t n)
 {
-	struct dir *d;
-	size_t done = 0, sent = 0;
-	int err;
+	size_t done = 0, sent = 0, i, j, nch;
+	int err = 0;
 
 	if (!su || !su->tx || !dst || (!mbv && n))
 		return -EINVAL;
-	d = &su->out;
-	while (done < n) {
-		const size_t m = n - done < su->batch ? n - done : su->batch;
-		size_t i, k;
-		for (i = 0; i < m; i++) {
-			const struct mbuf *mb = mbv[done + i];
-			const uint32_t base = (uint32_t)(i * su->slot);
-			size_t len = mb && mb->end > mb->pos ? mb->end - mb->pos
-							     : 0;
-			if (!mb || len > su->slot)
-				return -EINVAL;
-			memcpy(d->h + base, mb->buf + mb->pos, len);
-			d->hw[i] = base;
-			d->hw[m + i] = base + (uint32_t)len;
-			d->hw[2 * m + i] = base + (uint32_t)su->slot;
-		}
-		err = gpu_batch(su, d, m, srtp_encrypt_batch_dev, su->tx);
-		if (err)
-			return -err;
-		for (i = 0, k = 0; i < m; i++) {
-			if (errv)
-				errv[done + i] = d->he[i];
-			if (d->he[i])
-				continue;
-			su->iov[k].iov_base = d->h + d->hw[i];
-			su->iov[k].iov_len = d->hw[m + i] - d->hw[i];
-			memset(&su->msg[k].msg_hdr, 0, sizeof(su->msg[k].msg_hdr));
-			su->msg[k].msg_hdr.msg_iov = &su->iov[k];
-			su->msg[k].msg_hdr.msg_iovlen = 1;
-			su->msg[k].msg_hdr.msg_name = (void *)dst;
-			su->msg[k].msg_hdr.msg_namelen = dstlen;
-			k++;
-		}
-		for (i = 0; i < k;) {
-			int r = sendmmsg(su->fd, su->msg + i, (unsigned)(k - i), 0);
-			if (r < 0) {
-				if (errno == EINTR)
-					continue;
-				if (errno == EAGAIN || errno == EWOULDBLOCK ||
-				    errno == ENOBUFS) {
-					struct pollfd pfd = {su->fd, POLLOUT, 0};
-					(void)poll(&pfd, 1, 10);
-					continue;
-				}
-				return -errno;
-			}
-			i += (size_t)r;
-		}
-		sent += k;
-		su->n_tx += k;
-		done += m;
+	/* every packet is checked before anything is protected or sent */
+	for (i = 0; i < n; i++) {
+		const struct mbuf *mb = mbv[i];
+		if (!mb || (mb->end > mb->pos ? mb->end - mb->pos : 0) >
+		    su->slot)
+			return -EINVAL;
 	}
-	return (int)sent;
+	nch = (n + su->batch - 1) / su->batch;
+	/* chunk j on arena j % 2: stage + issue j, then finish + send j-1
+	 * (pipelined: j-1's datagrams go out while j runs on the GPU) */
+	for (j = 0; j <= nch && !err; j++) {
+		if (j < nch) {
+			struct dir *d = &su->out[j & 1];
+			const size_t a = j * su->batch;
+			const size_t m = n - a < su->batch ? n - a : su->batch;
+			tx_stage(su, d, mbv + a, m);
+			err = gpu_issue(su, d, 1, su->tx);
+			if (err)
+				break;
+			if (!su->pipeline) {
+				long r;
+				err = gpu_finish(su, d, SRTP_UDP_TX_GPU);
+				if (err)
+					break;
+				r = tx_send(su, d, dst, dstlen,
+					    errv ? errv + a : NULL);
+				if (r < 0) {
+					err = (int)-r;
+					break;
+				}
+				sent += (size_t)r;
+				done = a + m;
+				continue;
+			}
+		}
+		if (su->pipeline && j > 0) {
+			struct dir *p = &su->out[(j - 1) & 1];
+			long r;
+			err = gpu_finish(su, p, SRTP_UDP_TX_GPU);
+			if (err)
+				break;
+			r = tx_send(su, p, dst, dstlen,
+				    errv ? errv + (j - 1) * su->batch : NULL);
+			if (r < 0) {
+				err = (int)-r;
+				break;
+			}
+			sent += (size_t)r;
+			done = (j - 1) * su->batch + p->n;
+		}
+	}
+	if (!err)
+		return (int)sent;
+	/* drain what is still in flight; the packets not sent get the errno
+	 * (the ones before them went out and advanced the sender state) */
+	for (i = 0; i < 2; i++)
+		if (su->out[i].tk) {
+			(void)srtp_batch_wait(su->out[i].tk);
+			su->out[i].tk = NULL;
+		}
+	if (errv)
+		for (i = done; i < n; i++)
+			errv[i] = err;
+	return sent ? (int)sent : -err;
 }
 
 void srtp_udp_stats(const struct srtp_udp *su, uint64_t *rx, uint64_t *rx_ok,
@@ -292,4 +482,13 @@ void srtp_udp_stats(const struct srtp_udp *su, uint64_t *rx, uint64_t *rx_ok,
 		*rx_ok = su ? su->n_rx_ok : 0;
 	if (tx)
 		*tx = su ? su->n_tx : 0;
+}
+
+void srtp_udp_times(const struct srtp_udp *su, uint64_t ns[SRTP_UDP_NSTAGE])
+{
+	int k;
+	if (!ns)
+		return;
+	for (k = 0; k < SRTP_UDP_NSTAGE; k++)
+		ns[k] = su ? su->ns[k] : 0;
 }

@@ -460,6 +460,21 @@ int   sgpu_fold_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
 		    int32_t *err, int gcm, uint32_t *scratch,
 		    struct sgpu_fold_out *out, void *stream);
 
+/* verdict fold of a multi-session unprotect planned by sgpu_mplan_rtp
+ * (same scratch, still holding the sort): per session segment what
+ * sgpu_fold_rtp does for one stream.  Writes the EAUTH results and the
+ * touched sessions' s_l / replay window into st_out only if the fold holds
+ * (out->fail == 0); fscratch: sgpu_mfold_scratch(n) bytes. */
+size_t sgpu_mfold_scratch(uint32_t n);
+int   sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
+		     const struct sgpu_hdr *hdr, const uint32_t *sess,
+		     const uint64_t *desc, const uint8_t *verdict,
+		     const uint32_t *end0, uint32_t *pos, uint32_t *end,
+		     int32_t *err, int gcm, const struct sgpu_sstate *st_in,
+		     struct sgpu_sstate *st_out, void *scratch,
+		     size_t scratch_bytes, uint32_t *fscratch,
+		     struct sgpu_fold_out *out, void *stream);
+
 /* guarded per-packet results of a device-planned batch (device arrays):
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */
 /* sgpu_plan_results, and in the same launch: *gate = *guard || *nfail

@@ -114,6 +114,7 @@ EXPORTS = (
     "srtp_gpu_tune", "srtp_gpu_counter",
     "rtcp_decode_batch_dev",
     "srtp_udp_alloc", "srtp_udp_recv", "srtp_udp_send", "srtp_udp_stats",
+    "srtp_udp_pipeline", "srtp_udp_times",
     "srtp_dtls_key_size", "srtp_keyinfo_split", "srtp_dtls_keying_many",
     "srtp_alloc_dtls_many",
     "mbuf_alloc", "mbuf_resize", "mbuf_write_mem", "mem_deref", "mem_zalloc",
@@ -180,6 +181,8 @@ def load():
                                 ctypes.POINTER(ctypes.c_int), sz]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.srtp_udp_stats.argtypes = [vp, u64p, u64p, u64p]
+    L.srtp_udp_pipeline.argtypes = [vp, ctypes.c_int]
+    L.srtp_udp_times.argtypes = [vp, u64p]
     L.srtp_dtls_key_size.argtypes = [ctypes.c_int]
     L.srtp_dtls_key_size.restype = sz
     L.srtp_keyinfo_split.argtypes = [ctypes.c_int, ctypes.c_char_p,
@@ -278,14 +281,25 @@ class SrtpUdp:
     socket and the RTP layer.  handler(src_bytes, mbuf, err) per datagram;
     the mbuf views the receive arena only during the call."""
 
+    STAGES = ("rx_syscall", "rx_gpu", "rx_deliver", "tx_stage", "tx_gpu",
+              "tx_syscall")
+
     def __init__(self, fd, rx=None, tx=None, batch=256, slot=1536,
-                 handler=None):
+                 handler=None, pipeline=False):
         self._cb = UDP_RECV_H(self._recv)
         self.handler = handler
         self.ptr = ctypes.c_void_p()
         self.err = lib().srtp_udp_alloc(
             ctypes.byref(self.ptr), fd, rx.ptr if rx else None,
             tx.ptr if tx else None, batch, slot, self._cb, None)
+        if not self.err and pipeline:
+            self.err = lib().srtp_udp_pipeline(self.ptr, 1)
+
+    def times(self):
+        """seconds per stage (srtp_udp_times)"""
+        ns = (ctypes.c_uint64 * len(self.STAGES))()
+        lib().srtp_udp_times(self.ptr, ns)
+        return {k: ns[i] * 1e-9 for i, k in enumerate(self.STAGES)}
 
     def _recv(self, src, srclen, mb, err, arg):
         if self.handler:

@@ -12,7 +12,12 @@ through the C-ABI library on the GPU.
     plaintext packets with err 0, and the receive slots and final receiver
     state match the reference's unprotect digests;
   * errors: forged and replayed datagrams reach the handler with the
-    oracle's errno (EAUTH, EALREADY), in datagram order.
+    oracle's errno (EAUTH, EALREADY), in datagram order;
+  * both synchronous and pipelined (srtp_udp_pipeline: batch k+1 read
+    while batch k is on the GPU; chunk j+1 protected while chunk j is
+    sent);
+  * send argument checks: a bad mbuf anywhere fails the call before any
+    packet is protected or sent.
 """
 import socket
 
@@ -63,7 +68,19 @@ def state_of(ctx):
                            st.replay_rtp_bitmap)])
 
 
-def test_udp_send_and_receive_vs_reference(torch_cuda):
+def drain(sr, got, want):
+    """srtp_udp_recv rounds until `want` datagrams reached the handler
+    (pipelined: a round hands over the previous round's batch; a round
+    that receives nothing flushes the batch in flight)"""
+    for _ in range(10000):
+        if len(got) >= want:
+            return
+        assert sr.recv(200) >= 0
+    raise AssertionError("datagrams missing: %d of %d" % (len(got), want))
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_udp_send_and_receive_vs_reference(torch_cuda, pipeline):
     ref = F.load()[1]
     arena, pos, end, cap, _, keys = W.build_config(1)
     n, slot = ref["n"], ref["slot"]
@@ -73,7 +90,8 @@ def test_udp_send_and_receive_vs_reference(torch_cuda):
 
     # ---- send: GPU protect + sendmmsg -> plain socket ----
     tx = P.Srtp(1, key)
-    su = P.SrtpUdp(a.fileno(), tx=tx, batch=64, slot=256)
+    su = P.SrtpUdp(a.fileno(), tx=tx, batch=64, slot=256,
+                   pipeline=pipeline)
     assert su.err == 0, P.lib().srtp_gpu_error()
     wire = []
     for c0 in range(0, n, CHUNK):
@@ -103,15 +121,14 @@ def test_udp_send_and_receive_vs_reference(torch_cuda):
         got.append(slot_view(mb, err))
 
     rx = P.Srtp(1, key)
-    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=64, slot=256, handler=handler)
+    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=64, slot=256, handler=handler,
+                   pipeline=pipeline)
     assert sr.err == 0
     addr_a = b.getsockname()
     for c0 in range(0, n, CHUNK):
         for d in wire[c0:c0 + CHUNK]:
             a.sendto(d, addr_a)
-        want = min(n, c0 + CHUNK)
-        while len(got) < want:
-            assert sr.recv(1000) > 0
+        drain(sr, got, min(n, c0 + CHUNK))
     assert [g[0] for g in got] == [0] * n
     unp = np.zeros(n * slot, dtype=np.uint8)
     uend = np.zeros(n, dtype=np.uint32)
@@ -130,7 +147,8 @@ def test_udp_send_and_receive_vs_reference(torch_cuda):
     b.close()
 
 
-def test_udp_receive_errors_vs_oracle(torch_cuda):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_udp_receive_errors_vs_oracle(torch_cuda, pipeline):
     key = W.CONFIG1_KEY
     arena, pos, end, cap, _, _ = W.build_config(1, n=300)
     ob = O.OracleBackend()
@@ -158,17 +176,36 @@ def test_udp_receive_errors_vs_oracle(torch_cuda):
         got.append(slot_view(mb, err))
 
     rx = P.Srtp(1, key)
-    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=100, slot=256, handler=handler)
+    sr = P.SrtpUdp(b.fileno(), rx=rx, batch=100, slot=256, handler=handler,
+                   pipeline=pipeline)
     for c0 in range(0, len(wire), CHUNK):
         for d in wire[c0:c0 + CHUNK]:
             a.sendto(d, b.getsockname())
-        while len(got) < min(len(wire), c0 + CHUNK):
-            assert sr.recv(1000) > 0
+        drain(sr, got, min(len(wire), c0 + CHUNK))
     for i, (g, w) in enumerate(zip(got, want)):
         assert g[:3] == w[:3], i
         assert g[3][:len(w[3])] == w[3], i
     assert sorted({g[0] for g in got}) == sorted({0, P.EAUTH, 114}) or \
         sorted({g[0] for g in got}) == sorted({0, P.EAUTH, 215})
     sr.close()
+    a.close()
+    b.close()
+
+
+def test_udp_send_checks_every_mbuf_first(torch_cuda):
+    a, b = udp_pair()
+    tx = P.Srtp(1, W.CONFIG1_KEY)
+    su = P.SrtpUdp(a.fileno(), tx=tx, batch=4, slot=256)
+    pkt = bytes([0x80, 0, 0, 1]) + bytes(8) + bytes(100)
+    mbs = [P.new_mbuf(pkt, 512) for _ in range(9)]
+    big = P.new_mbuf(bytes([0x80, 0, 0, 2]) + bytes(400), 512)
+    r, errs = su.send(P.sockaddr_in(*b.getsockname()), mbs + [big])
+    assert r == -22                       # -EINVAL, nothing went out
+    assert su.stats()[2] == 0
+    e, st = tx.export(0)
+    assert e != 0                         # no stream created: nothing ran
+    for m in mbs + [big]:
+        P.free_mbuf(m)
+    su.close()
     a.close()
     b.close()

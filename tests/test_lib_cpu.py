@@ -15,9 +15,9 @@ import re_amd.srtp as P
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
+def declared_functions(headers=None):
     names = set()
-    for h in ("re_srtp.h", "re_srtp_batch.h", "re_srtp_udp.h",
+    for h in headers or ("re_srtp.h", "re_srtp_batch.h", "re_srtp_udp.h",
               "re_srtp_keying.h", "re_rtcp_batch.h", "re_mbuf.h",
               "re_mem.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
@@ -64,7 +64,12 @@ def test_libre_build_links_against_libre_only():
     lib = os.path.join(ROOT, "re_amd", "lib", "libre_srtp_amd_libre.so")
     srtp_only = [n for n in declared_functions()
                  if not n.startswith(("mem_", "mbuf_"))]
-    assert dynsyms(lib, True) == srtp_only
+    # + the libre UDP helper (include/re_srtp_libre.h): LIBRE=1 only
+    helper = declared_functions(("re_srtp_libre.h",))
+    assert helper == ["srtp_udp_helper_alloc", "srtp_udp_helper_flush",
+                      "srtp_udp_helper_stats"]
+    assert dynsyms(lib, True) == sorted(srtp_only + helper)
+    assert not set(helper) & set(dynsyms(P.LIB_PATH, True))
     undef = [u for u in dynsyms(lib, False) if u.startswith(("mem_", "mbuf_"))]
     assert undef, "expected libre's mem_/mbuf_ imports"
     assert set(undef) <= set(declared_functions()), undef

@@ -45,6 +45,8 @@ struct dir {                    /* one arena: slots, windows, results */
 	size_t n;               /* packets staged / in flight */
 	struct srtp_batch_ticket *tk;   /* in flight (pipelined) */
 	struct srtp_batch_dev b;
+	struct srtp *ctx;       /* the call's session array (one entry): it
+				   must outlive an asynchronous call */
 };
 
 struct srtp_udp {
@@ -195,11 +197,12 @@ static int gpu_issue(struct srtp_udp *su, struct dir *d, int prot,
 	b->err = d->de;
 	b->n = n;
 	b->stream = su->stream;
+	d->ctx = ctx;
 	if (su->pipeline)
-		return prot ? srtp_encrypt_batch_dev_async(&ctx, 1, b, &d->tk)
-			    : srtp_decrypt_batch_dev_async(&ctx, 1, b, &d->tk);
-	return prot ? srtp_encrypt_batch_dev(&ctx, 1, b)
-		    : srtp_decrypt_batch_dev(&ctx, 1, b);
+		return prot ? srtp_encrypt_batch_dev_async(&d->ctx, 1, b, &d->tk)
+			    : srtp_decrypt_batch_dev_async(&d->ctx, 1, b, &d->tk);
+	return prot ? srtp_encrypt_batch_dev(&d->ctx, 1, b)
+		    : srtp_decrypt_batch_dev(&d->ctx, 1, b);
 }
 
 /* ... its completion, then arena, windows and results down (on the copy

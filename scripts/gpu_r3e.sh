@@ -1,15 +1,14 @@
 #!/bin/bash
-# round-3 check: new GPU tests, byte-1 bitop3 A/B, per-call latency,
-# config-4 forged-packet lines.  Each GPU step under its own limit.
+# round-3 measurements, part 2
 set -o pipefail
-O=gpurun_out/r3d
+O=gpurun_out/r3e
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_libre.py > $O/tests.log 2>&1 || exit $?
 b() { local n=$1; shift; timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > $O/$n.json 2> $O/$n.err || exit $?; }
-b c4 --config 4
 b c4_forge1 --config 4 --forge 1
 b c4_forge001 --config 4 --forge 0.001
+b c2_forge1 --forge 1
+b c4_nopipe --config 4 --no-pipeline
 b c2 --steps 10
 RE_SRTP_LIB=$PWD/re_amd/lib/variants/b1bitop3.so b c2_b1 --steps 10
 b c3 --config 3 --steps 10

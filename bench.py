@@ -456,6 +456,10 @@ def main():
         if sess is not None:
             sess_d = i32(sess)
         p_d, e_d = torch.empty_like(pos_d), torch.empty_like(end_d)
+        # two steps in flight: each in-flight call keeps its own windows
+        # until it is waited for (re_srtp_batch.h: the device arrays of an
+        # asynchronous call stay untouched by other calls until then)
+        win2 = [(p_d, e_d), (torch.empty_like(pos_d), torch.empty_like(end_d))]
         # per-step result arrays: the API fills them inside the timed
         # region; the bench tallies them after it (verification, not path)
         errbuf = torch.zeros((2, max(1, args.steps, args.warmup), n), dtype=torch.int32,
@@ -522,8 +526,9 @@ def main():
             e2e_pass(OPS[1], rx, err_dd)
             return 0
         if use_dev:
-            p_d.copy_(pos_d)
-            e_d.copy_(end_d)
+            pw, ew = win2[k & 1] if inflight is not None else (p_d, e_d)
+            pw.copy_(pos_d)
+            ew.copy_(end_d)
             pend = []
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
@@ -534,7 +539,7 @@ def main():
                     # check after the timed region would fail)
                     arena.index_put_((forge_idx,), arena[forge_idx] ^ 0x40)
                 a = (opname, ss, arena.data_ptr(), arena.numel(),
-                     p_d.data_ptr(), e_d.data_ptr(), cap_d.data_ptr(),
+                     pw.data_ptr(), ew.data_ptr(), cap_d.data_ptr(),
                      er.data_ptr(), n,
                      sess_d.data_ptr() if sess_d is not None else None, sptr)
                 if use_async:

@@ -105,6 +105,8 @@ static struct {
 	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
 	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
 				   device-planned single-key batches */
+	int nocombine;          /* srtp_gpu_tune nocombine: per-packet calls
+				   of different threads do not share launches */
 	int nomk;               /* srtp_gpu_tune nomk: multi-session plans on
 				   the general per-lane-key kernel */
 	int splan;              /* srtp_gpu_tune splan: single-session RTP
@@ -148,6 +150,8 @@ static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
+static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
+static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
 /* fault injection (srtp_gpu_tune "fail_grow", like the reference's
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
  * now fails with ENOMEM */
@@ -172,6 +176,10 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_devfolds, __ATOMIC_RELAXED);
 	if (!strcmp(name, "splans"))
 		return __atomic_load_n(&g_cnt_splans, __ATOMIC_RELAXED);
+	if (!strcmp(name, "pcbatches"))
+		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
+	if (!strcmp(name, "pcpackets"))
+		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
 	return 0;
 }
 
@@ -194,6 +202,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.splan = value > 0;
 	else if (!strcmp(name, "nomk"))
 		g_env.nomk = value > 0;
+	else if (!strcmp(name, "nocombine"))
+		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -302,6 +312,7 @@ static void slot_put(uint32_t s)
 /* srtp_alloc (srtp.c:88-180)                                          */
 
 static void tk_drain(void);
+static int tk_pending(void);
 
 static void destructor(void *arg)
 {
@@ -1473,7 +1484,8 @@ static int sess_host(struct srtp **sessv, size_t nsess)
 	return err;
 }
 
-static int run_mbufs_(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
+static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
+		      const uint32_t *sidx, struct mbuf **mbv, int *errv,
 		      size_t n)
 {
 	const int prot = op == OP_RTP_ENC || op == OP_RTCP_ENC;
@@ -1485,12 +1497,12 @@ static int run_mbufs_(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 	size_t *koff = NULL, i, round;
 	int err, snapped = 0;
 
-	if (!srtp || !mbv)
+	if (!sessv || !mbv)
 		return EINVAL;
 	for (i = 0; i < n; i++)
 		if (!mbv[i])
 			return EINVAL;
-	err = engine_init(&E, op, n, &srtp, 1, NULL);
+	err = engine_init(&E, op, n, sessv, nsess, sidx);
 	if (err)
 		goto out;
 	outp = calloc(n ? n : 1, sizeof(*outp));
@@ -1633,13 +1645,128 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 		     size_t n)
 {
 	int err;
+	if (!srtp)
+		return EINVAL;
 	tk_drain();
 	table_rdlock();
-	err = srtp ? sess_host(&srtp, 1) : 0;
+	err = sess_host(&srtp, 1);
 	if (!err)
-		err = run_mbufs_(op, srtp, mbv, errv, n);
+		err = run_mbufs_(op, &srtp, 1, NULL, mbv, errv, n);
 	table_unlock();
 	return err;
+}
+
+/*
+ * Per-packet calls from many threads (the unchanged re_srtp.h API: every
+ * libre caller protects one mbuf per call, src/srtp/srtp.c:183-432)
+ * share GPU launches: a calling thread queues its packet; if no thread is
+ * running a batch it becomes the runner, takes everything queued (the
+ * packets of other threads that arrived meanwhile) and runs it as one
+ * multi-session batch per operation, then wakes their callers.  No timer
+ * and no waiting at low load: a lone caller runs its packet at once.  A
+ * struct srtp is used by one thread at a time (the reference's contract),
+ * so the packets of one batch belong to distinct sessions, and each
+ * thread's calls stay in its own order.
+ */
+struct pc_req {
+	struct pc_req *next;
+	int op;
+	struct srtp *s;
+	struct mbuf *mb;
+	int err;
+	int done;
+};
+
+static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t pc_cond = PTHREAD_COND_INITIALIZER;
+static struct pc_req *pc_head, *pc_tail;
+static int pc_running;
+
+static void pc_run(struct pc_req *list)
+{
+	enum { MAXB = 1024 };
+	struct srtp *sv[MAXB];
+	struct mbuf *mv[MAXB];
+	struct pc_req *rq[MAXB];
+	int ev[MAXB];
+	int op;
+
+	for (op = 0; op < 4; op++) {
+		struct pc_req *r = list;
+		while (r) {
+			size_t n = 0, i;
+			int err;
+			for (; r && n < MAXB; r = r->next) {
+				if (r->op != op)
+					continue;
+				rq[n] = r;
+				sv[n] = r->s;
+				mv[n++] = r->mb;
+			}
+			if (!n)
+				break;
+			count(&g_cnt_pcbatch, 1);
+			count(&g_cnt_pcpkts, n);
+			table_rdlock();
+			err = sess_host(sv, n);
+			if (!err) {
+				uint32_t *idx = malloc(n * sizeof(*idx));
+				if (!idx)
+					err = ENOMEM;
+				for (i = 0; !err && i < n; i++)
+					idx[i] = (uint32_t)i;
+				if (!err)
+					err = run_mbufs_(op, sv, n, idx, mv, ev, n);
+				free(idx);
+			}
+			table_unlock();
+			for (i = 0; i < n; i++)
+				rq[i]->err = err ? err : ev[i];
+		}
+	}
+}
+
+static int one(int op, struct srtp *srtp, struct mbuf *mb)
+{
+	struct pc_req req;
+	int e = 0, err;
+
+	if (!srtp || !mb)
+		return EINVAL;
+	if (g_env.nocombine || tk_pending()) {
+		err = run_mbufs(op, srtp, &mb, &e, 1);
+		return err ? err : e;
+	}
+	memset(&req, 0, sizeof(req));
+	req.op = op;
+	req.s = srtp;
+	req.mb = mb;
+	pthread_mutex_lock(&pc_lock);
+	if (pc_tail)
+		pc_tail->next = &req;
+	else
+		pc_head = &req;
+	pc_tail = &req;
+	while (!req.done) {
+		if (!pc_running) {
+			struct pc_req *list = pc_head, *r, *nx;
+			pc_head = pc_tail = NULL;
+			pc_running = 1;
+			pthread_mutex_unlock(&pc_lock);
+			pc_run(list);
+			pthread_mutex_lock(&pc_lock);
+			for (r = list; r; r = nx) {
+				nx = r->next;
+				r->done = 1;    /* r may be gone once woken */
+			}
+			pc_running = 0;
+			pthread_cond_broadcast(&pc_cond);
+			continue;
+		}
+		pthread_cond_wait(&pc_cond, &pc_lock);
+	}
+	pthread_mutex_unlock(&pc_lock);
+	return req.err;
 }
 
 int srtp_encrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
@@ -1666,14 +1793,6 @@ int srtcp_decrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
 	return run_mbufs(OP_RTCP_DEC, srtp, mbv, errv, n);
 }
 
-static int one(int op, struct srtp *srtp, struct mbuf *mb)
-{
-	int e = 0, err;
-	if (!srtp || !mb)
-		return EINVAL;
-	err = run_mbufs(op, srtp, &mb, &e, 1);
-	return err ? err : e;
-}
 
 int srtp_encrypt(struct srtp *srtp, struct mbuf *mb)
 {
@@ -3985,6 +4104,13 @@ static void tk_finish_one(void)
 
 /* complete every pending call of this thread (before any other entry
  * point: those see the sessions as the calls in order leave them) */
+/* this thread has asynchronous calls pending (their sessions must not
+ * be handed to another thread's shared launch) */
+static int tk_pending(void)
+{
+	return t_tk_head != NULL;
+}
+
 static void tk_drain(void)
 {
 	while (t_tk_head)

@@ -14,7 +14,7 @@ bench.py builds ("config2", "config3_rtcp", ...).
               opcode mix (profiles/r03_isa_mix.json, scripts/isa_mix.py)
               of fraction / issue rate, the rates measured per opcode at 4
               waves/SIMD (scripts/ubench_valu.hip, profiles/
-              r03_ubench_valu.log); opcodes not measured take the v_xor
+              r03_ubench_valu.txt); opcodes not measured take the v_xor
               rate (the fastest: the floor is not overstated)
   lds_frac  = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE / 8 x 256 CUs)
 """
@@ -96,7 +96,7 @@ def counters(d):
 def main():
     out, wl, fdir, wdir, sdir = sys.argv[1:6]
     mix = json.load(open(os.path.join(ROOT, "profiles", "r03_isa_mix.json")))
-    rt = rates(os.path.join(ROOT, "profiles", "r03_ubench_valu.log"))
+    rt = rates(os.path.join(ROOT, "profiles", "r03_ubench_valu.txt"))
     xor = rt["v_xor_b32_e32"]
     fa, _, grid = counters(fdir)
     wa, _, _ = counters(wdir)

@@ -1,0 +1,132 @@
+"""Per-packet calls (the unchanged re_srtp.h API) from many threads at once
+share GPU launches (srtp.c `one`: a runner takes every queued packet and
+runs them as one multi-session batch per operation).  Each of 16 threads
+owns its context pair (struct srtp is single-threaded, like the
+reference's) and runs an interleaved srtp_encrypt / srtp_decrypt /
+srtcp_encrypt / srtcp_decrypt sequence with ROC wrap, a replay and a
+forgery; every call's errno, pos/end and bytes must equal the oracle's
+(the C restatement, pinned to the reference goldens), whatever packets of
+other threads shared its launch.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import re_amd.srtp as P
+from tests import oracle_lib as O
+from tests.test_gpu_fastpath import rtp_packet
+
+pytestmark = pytest.mark.gpu
+
+SUITES = [1, 0, 5, 4]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    P.load()
+    return torch
+
+
+def rtcp_packet(rng, ssrc, n):
+    return bytes([0x80, 200, 0, (8 + n) // 4 - 1]) + ssrc.to_bytes(4, "big") \
+        + rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def script(t):
+    """thread t's call sequence: (op, packet bytes or index of an earlier
+    protected packet to replay / forge)"""
+    rng = np.random.default_rng(100 + t)
+    ssrc = 0x10000 + t
+    out = []
+    for k in range(120):
+        seq = (65500 + k) & 0xffff
+        out.append(("srtp_encrypt", rtp_packet(rng, seq, ssrc,
+                                               plen=int(rng.integers(0, 300)))))
+        out.append(("srtp_decrypt", ("prot", len(out) - 1)))
+        if k % 10 == 3:
+            out.append(("srtcp_encrypt", rtcp_packet(rng, ssrc, 4 * int(
+                rng.integers(1, 20)))))
+            out.append(("srtcp_decrypt", ("prot", len(out) - 1)))
+    out.append(("srtp_decrypt", ("prot", 0)))              # replay
+    out.append(("srtp_decrypt", ("forge", 2)))             # forgery
+    return out
+
+
+def run_thread(t, suite, key, backend, results):
+    tx, rx = backend(suite, key)
+    res, prot = [], {}
+    for i, (op, arg) in enumerate(script(t)):
+        if isinstance(arg, tuple):
+            kind, j = arg
+            data = bytearray(prot[j])
+            if kind == "forge":
+                data[-1] ^= 1
+            data = bytes(data)
+        else:
+            data = arg
+        ctx = tx if op.endswith("encrypt") else rx
+        e, po, en, b = ctx(op, data)
+        prot[i] = b[:en] if op.endswith("encrypt") else None
+        res.append((e, po, en, b[:max(en, len(data))]))
+    results[t] = res
+
+
+def dev_backend(suite, key):
+    def ctx_of(c):
+        def call(op, data):
+            mb = P.new_mbuf(data, len(data) + 64)
+            e = c._op(op, mb)
+            m = mb.contents
+            out = (e, m.pos, m.end, P.mbuf_bytes(mb, m.size))
+            P.free_mbuf(mb)
+            return out
+        return call
+    return ctx_of(P.Srtp(suite, key)), ctx_of(P.Srtp(suite, key))
+
+
+def oracle_backend(suite, key):
+    ob = O.OracleBackend()
+
+    def ctx_of(c):
+        def call(op, data):
+            e, po, en, so, buf = ob.call(c, op, len(data) + 64, 0,
+                                         len(data), data, len(data) + 64)
+            return (e, po, en, bytes(buf[:so]))
+        return call
+    return ctx_of(ob.alloc(suite, key, 0)[0]), ctx_of(ob.alloc(suite, key,
+                                                               0)[0])
+
+
+def test_threads_share_launches_exactly(torch_cuda):
+    T = 16
+    keys = [bytes((13 * t + i) & 0xff for i in range(46)) for t in range(T)]
+    want, got = {}, {}
+    for t in range(T):
+        s = SUITES[t % 4]
+        k = keys[t][:P.key_len(s) + P.salt_len(s)]
+        run_thread(t, s, k, oracle_backend, want)
+    b0, p0 = P.counter("pcbatches"), P.counter("pcpackets")
+    ths = []
+    for t in range(T):
+        s = SUITES[t % 4]
+        k = keys[t][:P.key_len(s) + P.salt_len(s)]
+        ths.append(threading.Thread(target=run_thread,
+                                    args=(t, s, k, dev_backend, got)))
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(120)
+    assert len(got) == T
+    for t in range(T):
+        for i, (g, w) in enumerate(zip(got[t], want[t])):
+            assert g[:3] == w[:3], (t, i)
+            assert g[3][:len(w[3])] == w[3][:len(g[3])], (t, i)
+    batches = P.counter("pcbatches") - b0
+    packets = P.counter("pcpackets") - p0
+    assert packets == sum(len(v) for v in got.values())
+    assert batches <= packets

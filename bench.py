@@ -447,7 +447,7 @@ def main():
     use_dev = not args.host_arrays
     # asynchronous pair (srtp_*_batch_dev_async) for the RTP device path
     use_async = use_dev and not args.sync and not args.e2e and not args.rtcp
-    pipelined = use_async and not args.no_pipeline
+    pipelined = use_async and not args.no_pipeline and not args.forge
     sess_d = None
     if use_dev:
         i32 = lambda a: torch.from_numpy(
@@ -533,10 +533,11 @@ def main():
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
                 if forge_idx is not None and opname == OPS[1]:
-                    # the forgery is queued on the library's stream behind
-                    # protect's kernels (stream order; a protect completed
-                    # on the host instead would overwrite it and the EAUTH
-                    # check after the timed region would fail)
+                    # the forgery modifies protect's output: protect is
+                    # waited for first (an asynchronous call's arena is the
+                    # library's until then, re_srtp_batch.h)
+                    if pend:
+                        assert P.batch_wait(pend.pop()[0]) == 0
                     arena.index_put_((forge_idx,), arena[forge_idx] ^ 0x40)
                 a = (opname, ss, arena.data_ptr(), arena.numel(),
                      pw.data_ptr(), ew.data_ptr(), cap_d.data_ptr(),

@@ -4102,8 +4102,6 @@ static void tk_finish_one(void)
 	table_unlock();         /* held since the call was issued */
 }
 
-/* complete every pending call of this thread (before any other entry
- * point: those see the sessions as the calls in order leave them) */
 /* this thread has asynchronous calls pending (their sessions must not
  * be handed to another thread's shared launch) */
 static int tk_pending(void)
@@ -4111,6 +4109,8 @@ static int tk_pending(void)
 	return t_tk_head != NULL;
 }
 
+/* complete every pending call of this thread (before any other entry
+ * point: those see the sessions as the calls in order leave them) */
 static void tk_drain(void)
 {
 	while (t_tk_head)

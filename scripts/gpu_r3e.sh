@@ -5,7 +5,7 @@ O=gpurun_out/r3e
 mkdir -p $O
 export TMPDIR=/tmp
 b() { local n=$1; shift; timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > $O/$n.json 2> $O/$n.err || exit $?; }
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_percall.py tests/test_gpu_mfold.py > $O/tests.log 2>&1 || exit $?
+
 b c4_forge1 --config 4 --forge 1
 b c4_forge001 --config 4 --forge 0.001
 b c2_forge1 --forge 1

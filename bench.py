@@ -447,7 +447,7 @@ def main():
     use_dev = not args.host_arrays
     # asynchronous pair (srtp_*_batch_dev_async) for the RTP device path
     use_async = use_dev and not args.sync and not args.e2e and not args.rtcp
-    pipelined = use_async and not args.no_pipeline and not args.forge
+    pipelined = use_async and not args.no_pipeline
     sess_d = None
     if use_dev:
         i32 = lambda a: torch.from_numpy(
@@ -533,12 +533,17 @@ def main():
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
                 if forge_idx is not None and opname == OPS[1]:
-                    # the forgery modifies protect's output: protect is
-                    # waited for first (an asynchronous call's arena is the
-                    # library's until then, re_srtp_batch.h)
-                    if pend:
-                        assert P.batch_wait(pend.pop()[0]) == 0
-                    arena.index_put_((forge_idx,), arena[forge_idx] ^ 0x40)
+                    # the forgery flips one byte of protect's output on the
+                    # call stream, between protect and unprotect.  An
+                    # asynchronous call's arena is the library's until it is
+                    # waited for because a call the device could not complete
+                    # is re-run from it on the host (re_srtp_batch.h): the
+                    # line is only valid if no call was (checked below)
+                    with torch.cuda.stream(stream):
+                        if use_async and not pipelined:
+                            assert P.batch_wait(pend.pop()[0]) == 0
+                        arena.index_put_((forge_idx,),
+                                         arena[forge_idx] ^ 0x40)
                 a = (opname, ss, arena.data_ptr(), arena.numel(),
                      pw.data_ptr(), ew.data_ptr(), cap_d.data_ptr(),
                      er.data_ptr(), n,
@@ -611,6 +616,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    c_rerun0 = (P.counter("rejects"), P.counter("folds"), P.counter("gated"))
     t0 = time.perf_counter()
     errors = run_steps(sess_sets)
     torch.cuda.synchronize()
@@ -620,6 +626,13 @@ def main():
     prof = P.prof_read_named()
     P.prof_enable(False)
     elapsed = t1 - t0
+    if forge_pk is not None and pipelined:
+        # the forgery rode the stream between protect and unprotect: valid
+        # only if no call was completed on the host (a host re-run reads
+        # the arena as the stream left it)
+        assert (P.counter("rejects"), P.counter("folds"),
+                P.counter("gated")) == c_rerun0, \
+            "a call was re-run on the host: forged-packet line invalid"
     if use_dev:
         if forge_pk is not None:
             # exactly the forged packets fail, with EAUTH

@@ -1,6 +1,6 @@
 /**
  * @file re_mbuf.h  Packet buffer -- standalone subset, layout-identical to
- * libre's struct mbuf (/root/reference/include/re_mbuf.h:43-48).  When this
+ * libre's struct mbuf (baresip/re v4.10.0 include/re_mbuf.h:43-48).  When this
  * library is built inside libre, libre's own re_mbuf.h/mbuf.c are used.
  */
 #ifndef RE_MBUF_H

@@ -3,7 +3,7 @@
  *
  * MI355X-native replacement for libre's src/srtp.  The six declarations
  * below are the reference interface, unchanged
- * (/root/reference/include/re_srtp.h:8-30): same enum values, same
+ * (baresip/re v4.10.0 include/re_srtp.h:8-30): same enum values, same
  * signatures, same ownership (struct srtp is allocated with mem_zalloc and
  * released with mem_deref) and the same errno results, bit-exact outputs.
  *

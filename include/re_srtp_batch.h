@@ -111,6 +111,11 @@ int srtcp_decrypt_batch_dev(struct srtp **sessv, size_t nsess,
  * (their results stay in the tickets).  At most 4 calls are pending per
  * thread (a fifth completes the oldest first).  Returns 0 with *tp set
  * (the call may already have completed), or EINVAL / ENOMEM.
+ *
+ * A session with calls of one thread pending is busy for every other
+ * thread until the issuing thread has completed them: calls of this API
+ * from another thread that name it return (or, asynchronous, complete
+ * with) EBUSY and change nothing.
  */
 struct srtp_batch_ticket;
 
@@ -168,7 +173,10 @@ int srtp_gpu_tune(const char *name, long value);
  * speculation failed -- forged or mis-planned), "folds" (batches re-run to
  * fold such verdicts exactly on the host), "devfolds" (batches whose
  * verdicts folded on the device, no re-run), "rejects" (device plans
- * rejected: the host planned instead).  0 for an unknown name.
+ * rejected: the host planned instead), "splans" (per-stream device plans),
+ * "pcbatches" / "pcpackets" (shared launches of per-packet calls and the
+ * packets they carried), "gated" (asynchronous calls queued behind one
+ * the host completed, re-run when waited for).  0 for an unknown name.
  */
 uint64_t srtp_gpu_counter(const char *name);
 

@@ -470,7 +470,14 @@ struct mf_ctx {
 	const struct sgpu_sstate *st;
 	const uint8_t *vd;
 	uint32_t n, nsess;
+	const uint32_t *nfail;  /* queued behind the crypto kernels: the
+				   kernels' miss count (0: nothing to fold) */
 };
+
+__device__ __forceinline__ bool mf_idle(const mf_ctx &c)
+{
+	return c.nfail && *c.nfail == 0u;
+}
 
 __device__ __forceinline__ uint32_t mf_key(const mf_ctx &c, uint32_t k)
 {
@@ -516,8 +523,21 @@ __device__ __forceinline__ uint32_t mf_slv(const mf_ctx &c, int32_t e,
 }
 
 __global__ void __launch_bounds__(MP_BLOCK)
-k_mf_count(mf_ctx c, int32_t *blast)
+k_mf_count(mf_ctx c, int32_t *blast, struct sgpu_fold_out *out)
 {
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		/* the verdict starts held (also when there is nothing to fold) */
+		out->fail = 0;
+		out->nok = 0;
+		out->first_ok = 0xffffffffu;
+		out->last_ok = 0xffffffffu;
+		out->s_l = 0;
+		out->pad = 0;
+		out->lix = 0;
+		out->bitmap = 0;
+	}
+	if (mf_idle(c))
+		return;
 	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
 	int32_t last = (k < c.n && mf_event(c, k)) ? (int32_t)k : -1;
 	for (int o = 32; o > 0; o >>= 1)
@@ -536,8 +556,11 @@ k_mf_count(mf_ctx c, int32_t *blast)
 
 /* exclusive prefix maximum of the block maxima (one workgroup) */
 __global__ void __launch_bounds__(1024)
-k_mf_scan(const int32_t *blast, int32_t *bprev, uint32_t nb)
+k_mf_scan(const int32_t *blast, int32_t *bprev, uint32_t nb,
+	  const uint32_t *nfail)
 {
+	if (nfail && *nfail == 0u)
+		return;
 	__shared__ int32_t part[1024];
 	const uint32_t per = (nb + 1023u) / 1024u;
 	const uint32_t a = threadIdx.x * per;
@@ -566,6 +589,8 @@ k_mf_check(mf_ctx c, const int32_t *bprev, struct sgpu_sstate *st_out,
 	   struct sgpu_fold_out *out)
 {
 	__shared__ int32_t sc[MP_BLOCK];
+	if (mf_idle(c))
+		return;
 	const uint32_t k = blockIdx.x * MP_BLOCK + threadIdx.x;
 	const bool ev = k < c.n && mf_event(c, k);
 	sc[threadIdx.x] = ev ? (int32_t)k : -1;
@@ -605,10 +630,12 @@ k_mf_check(mf_ctx c, const int32_t *bprev, struct sgpu_sstate *st_out,
 __global__ void __launch_bounds__(MP_BLOCK)
 k_mf_results(const uint8_t *vd, const struct sgpu_hdr *hdr,
 	     const uint32_t *end0, uint32_t *pos, uint32_t *end, int32_t *err,
-	     uint32_t n, int gcm, const struct sgpu_fold_out *out)
+	     uint32_t n, int gcm, const struct sgpu_fold_out *out,
+	     const uint32_t *nfail)
 {
 	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
-	if (i >= n || out->fail || (vd[i] & SV_TAG_OK))
+	if ((nfail && *nfail == 0u) || i >= n || out->fail ||
+	    (vd[i] & SV_TAG_OK))
 		return;
 	err[i] = EAUTH;
 	pos[i] += hdr[i].hdr_len;
@@ -625,7 +652,7 @@ k_mf_final(mf_ctx c, const uint32_t *segl, const uint64_t *desc,
 	   struct sgpu_sstate *st_out, const struct sgpu_fold_out *out)
 {
 	const uint32_t s = blockIdx.x * MP_BLOCK + threadIdx.x;
-	if (s >= c.nsess || out->fail)
+	if (mf_idle(c) || s >= c.nsess || out->fail)
 		return;
 	const uint32_t l = segl[s];
 	if (l == 0xffffffffu)
@@ -662,18 +689,6 @@ k_mf_final(mf_ctx c, const uint32_t *segl, const uint64_t *desc,
 	}
 	st_out[s].lix = lix;
 	st_out[s].bitmap = bm;
-}
-
-__global__ void k_mf_init(struct sgpu_fold_out *out)
-{
-	out->fail = 0;
-	out->nok = 0;
-	out->first_ok = 0xffffffffu;
-	out->last_ok = 0xffffffffu;
-	out->s_l = 0;
-	out->pad = 0;
-	out->lix = 0;
-	out->bitmap = 0;
 }
 
 /* ---- host side ------------------------------------------------------ */
@@ -823,7 +838,8 @@ extern "C" size_t sgpu_mfold_scratch(uint32_t n)
 	return 2 * ((size_t)(n + MP_BLOCK - 1) / MP_BLOCK + 2) * 4;
 }
 
-extern "C" int sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
+extern "C" int sgpu_mfold_rtp(int phase, const uint32_t *nfail,
+			      const struct sgpu_mplan_in *in,
 			      const struct sgpu_hdr *hdr, const uint32_t *sess,
 			      const uint64_t *desc, const uint8_t *verdict,
 			      const uint32_t *end0, uint32_t *pos,
@@ -851,20 +867,26 @@ extern "C" int sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
 	if (!n || !in->nsess || (size_t)(p - (uint8_t *)scratch) > scratch_bytes)
 		return EINVAL;
 	int32_t *blast = (int32_t *)fscratch, *bprev = blast + nb + 2;
-	mf_ctx c = {vout, sess, sseq, segf, st_in, verdict, n, in->nsess};
-	hipLaunchKernelGGL(k_mf_init, dim3(1), dim3(1), 0, st, out);
-	hipLaunchKernelGGL(k_mf_count, dim3(nb), dim3(MP_BLOCK), 0, st, c,
-			   blast);
-	hipLaunchKernelGGL(k_mf_scan, dim3(1), dim3(1024), 0, st,
-			   (const int32_t *)blast, bprev, nb);
-	hipLaunchKernelGGL(k_mf_check, dim3(nb), dim3(MP_BLOCK), 0, st, c,
-			   (const int32_t *)bprev, st_out, out);
-	hipLaunchKernelGGL(k_mf_results, dim3(nb), dim3(MP_BLOCK), 0, st,
-			   verdict, hdr, end0, pos, end, err, n, gcm,
-			   (const struct sgpu_fold_out *)out);
-	hipLaunchKernelGGL(k_mf_final,
-			   dim3((in->nsess + MP_BLOCK - 1) / MP_BLOCK),
-			   dim3(MP_BLOCK), 0, st, c, segl, desc, st_out,
-			   (const struct sgpu_fold_out *)out);
+	mf_ctx c = {vout, sess, sseq, segf, st_in, verdict, n, in->nsess, nfail};
+	if (phase != 2) {
+		/* the verdict: out->fail (0 also when nothing is to fold) */
+		hipLaunchKernelGGL(k_mf_count, dim3(nb), dim3(MP_BLOCK), 0, st,
+				   c, blast, out);
+		hipLaunchKernelGGL(k_mf_scan, dim3(1), dim3(1024), 0, st,
+				   (const int32_t *)blast, bprev, nb, nfail);
+		hipLaunchKernelGGL(k_mf_check, dim3(nb), dim3(MP_BLOCK), 0, st,
+				   c, (const int32_t *)bprev, st_out, out);
+	}
+	if (phase != 1) {
+		/* on a held fold: the forged packets' results (over those of
+		 * sgpu_plan_finish) and the touched sessions' windows */
+		hipLaunchKernelGGL(k_mf_results, dim3(nb), dim3(MP_BLOCK), 0,
+				   st, verdict, hdr, end0, pos, end, err, n, gcm,
+				   (const struct sgpu_fold_out *)out, nfail);
+		hipLaunchKernelGGL(k_mf_final,
+				   dim3((in->nsess + MP_BLOCK - 1) / MP_BLOCK),
+				   dim3(MP_BLOCK), 0, st, c, segl, desc, st_out,
+				   (const struct sgpu_fold_out *)out);
+	}
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

@@ -3,7 +3,7 @@
  *
  * What libre's receive path does with a (decrypted) RTCP compound packet,
  * rtcp_recv_handler: `while (0 == rtcp_decode(&msg, mb))`
- * (/root/reference/src/rtp/rtp.c:164), for a whole batch at once.  One lane
+ * (reference src/rtp/rtp.c:164), for a whole batch at once.  One lane
  * walks one packet from its start, message by message, with exactly the
  * reference's cursor rules -- the walk advances by what each body parse
  * reads, not by the header length (pkt.c:369-538), a read past the end

@@ -1489,9 +1489,24 @@ __device__ __forceinline__ bool fold_event(const struct sgpu_plan_in &in,
 
 __global__ void __launch_bounds__(PLAN_BLOCK)
 k_fold_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
-	     const uint8_t *vd, int32_t *blast, int32_t *bred)
+	     const uint8_t *vd, int32_t *blast, int32_t *bred,
+	     const uint32_t *nfail, struct sgpu_fold_out *out)
 {
 	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	if (i == 0) {
+		/* the verdict starts held (also when there is nothing to
+		 * fold: nfail, queued behind the kernels, is 0) */
+		out->fail = 0;
+		out->nok = 0;
+		out->first_ok = 0xffffffffu;
+		out->last_ok = 0xffffffffu;
+		out->s_l = 0;
+		out->pad = 0;
+		out->lix = 0;
+		out->bitmap = 0;
+	}
+	if (nfail && *nfail == 0u)
+		return;
 	int32_t last = -1, fok = 0x7fffffff, lok = -1;
 	bool ok = false;
 	if (i < in.n) {
@@ -1535,10 +1550,12 @@ k_fold_count(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 /* exclusive prefix maximum of the block maxima (one workgroup) */
 __global__ void __launch_bounds__(1024)
 k_fold_scan(const int32_t *blast, const int32_t *bred, int32_t *bprev,
-	    uint32_t nb, struct sgpu_fold_out *out)
+	    uint32_t nb, struct sgpu_fold_out *out, const uint32_t *nfail)
 {
 	__shared__ int32_t part[1024];
 	__shared__ int32_t red[3];
+	if (nfail && *nfail == 0u)
+		return;
 	const uint32_t per = (nb + 1023u) / 1024u;
 	const uint32_t a = threadIdx.x * per;
 	int32_t m = -1, f = 0x7fffffff, l = -1, c = 0;
@@ -1593,10 +1610,12 @@ __device__ __forceinline__ uint32_t fold_sl(const struct sgpu_plan_in &in,
 __global__ void __launch_bounds__(PLAN_BLOCK)
 k_fold_check(const struct sgpu_plan_in in, const struct sgpu_hdr *hdr,
 	     const uint8_t *vd, const int32_t *bprev,
-	     struct sgpu_fold_out *out)
+	     struct sgpu_fold_out *out, const uint32_t *nfail)
 {
 	__shared__ int32_t sc[PLAN_BLOCK];
 	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
+	if (nfail && *nfail == 0u)
+		return;
 	const bool ev = i < in.n && fold_event(in, hdr, vd, i);
 	/* inclusive prefix max of event indices inside the block */
 	sc[threadIdx.x] = ev ? (int32_t)i : -1;
@@ -1635,10 +1654,11 @@ __global__ void k_fold_results(const struct sgpu_plan_in in,
 			       const uint64_t *desc, const uint32_t *end0,
 			       const int32_t *blast, const int32_t *bprev,
 			       uint32_t nb, uint32_t *pos, uint32_t *end,
-			       int32_t *err, int gcm, struct sgpu_fold_out *out)
+			       int32_t *err, int gcm, struct sgpu_fold_out *out,
+			       const uint32_t *nfail)
 {
 	const uint32_t i = blockIdx.x * PLAN_BLOCK + threadIdx.x;
-	if (out->fail)
+	if ((nfail && *nfail == 0u) || out->fail)
 		return;
 	if (i < in.n && !(vd[i] & SV_TAG_OK)) {
 		err[i] = EAUTH;
@@ -1705,19 +1725,8 @@ __global__ void k_fold_first(const struct sgpu_plan_in in,
 		atomicOr(&out->fail, 2u);
 }
 
-__global__ void k_fold_init(struct sgpu_fold_out *out)
-{
-	out->fail = 0;
-	out->nok = 0;
-	out->first_ok = 0xffffffffu;
-	out->last_ok = 0xffffffffu;
-	out->s_l = 0;
-	out->pad = 0;
-	out->lix = 0;
-	out->bitmap = 0;
-}
-
-extern "C" int sgpu_fold_rtp(const struct sgpu_plan_in *in,
+extern "C" int sgpu_fold_rtp(int phase, const uint32_t *nfail,
+			     const struct sgpu_plan_in *in,
 			     const struct sgpu_hdr *hdr, const uint64_t *desc,
 			     const uint8_t *verdict, const uint32_t *end0,
 			     uint32_t *pos, uint32_t *end, int32_t *err,
@@ -1730,19 +1739,23 @@ extern "C" int sgpu_fold_rtp(const struct sgpu_plan_in *in,
 	int32_t *bred = bprev + nb + 2;
 	if (!in->n)
 		return EINVAL;
-	hipLaunchKernelGGL(k_fold_init, dim3(1), dim3(1), 0, st, out);
-	hipLaunchKernelGGL(k_fold_count, dim3(nb), dim3(PLAN_BLOCK), 0, st,
-			   *in, hdr, verdict, blast, bred);
-	hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, blast,
-			   (const int32_t *)bred, bprev, nb, out);
-	hipLaunchKernelGGL(k_fold_check, dim3(nb), dim3(PLAN_BLOCK), 0, st, *in,
-			   hdr, verdict, (const int32_t *)bprev, out);
-	hipLaunchKernelGGL(k_fold_first, dim3(1), dim3(1), 0, st, *in, desc,
-			   out);
-	hipLaunchKernelGGL(k_fold_results, dim3(nb), dim3(PLAN_BLOCK), 0, st,
-			   *in, hdr, verdict, desc, end0,
-			   (const int32_t *)blast, (const int32_t *)bprev, nb,
-			   pos, end, err, gcm, out);
+	if (phase != 2) {
+		hipLaunchKernelGGL(k_fold_count, dim3(nb), dim3(PLAN_BLOCK), 0,
+				   st, *in, hdr, verdict, blast, bred, nfail, out);
+		hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st,
+				   blast, (const int32_t *)bred, bprev, nb, out,
+				   nfail);
+		hipLaunchKernelGGL(k_fold_check, dim3(nb), dim3(PLAN_BLOCK), 0,
+				   st, *in, hdr, verdict, (const int32_t *)bprev,
+				   out, nfail);
+		hipLaunchKernelGGL(k_fold_first, dim3(1), dim3(1), 0, st, *in,
+				   desc, out);
+	}
+	if (phase != 1)
+		hipLaunchKernelGGL(k_fold_results, dim3(nb), dim3(PLAN_BLOCK), 0,
+				   st, *in, hdr, verdict, desc, end0,
+				   (const int32_t *)blast, (const int32_t *)bprev,
+				   nb, pos, end, err, gcm, out, nfail);
 	return herr(hipGetLastError(), "fold launch");
 }
 
@@ -1781,14 +1794,15 @@ __global__ void __launch_bounds__(256)
 k_plan_finish(const uint32_t *__restrict__ guard,
 	      const uint32_t *__restrict__ end0, uint32_t *__restrict__ end,
 	      int32_t *__restrict__ err, uint32_t n, int32_t delta,
-	      const uint32_t *nfail, uint32_t *gate, uint32_t *nfail_out)
+	      const uint32_t *nfail, uint32_t *gate, uint32_t *nfail_out,
+	      const uint32_t *ffail)
 {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	const uint32_t g = *guard;
 	if (i == 0) {
 		const uint32_t nf = nfail ? *nfail : 0u;
 		if (gate)
-			*gate = g || nf;
+			*gate = g || (nf && (!ffail || *ffail));
 		if (nfail_out)
 			*nfail_out = nf;
 	}
@@ -1802,12 +1816,12 @@ extern "C" int sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
 				uint32_t *end, int32_t *err, uint32_t n,
 				int32_t delta, const uint32_t *nfail,
 				uint32_t *gate, uint32_t *nfail_out,
-				void *stream)
+				const uint32_t *ffail, void *stream)
 {
 	const uint32_t nb = n ? (n + 255) / 256 : 1;
 	hipLaunchKernelGGL(k_plan_finish, dim3(nb), dim3(256), 0,
 			   (hipStream_t)stream, guard, end0, end, err, n, delta,
-			   nfail, gate, nfail_out);
+			   nfail, gate, nfail_out, ffail);
 	return herr(hipGetLastError(), "finish launch");
 }
 

@@ -85,7 +85,40 @@ struct srtp {
 	uint64_t pend_p;        /* async: last pending single-stream call on
 				   it (issuing thread's sequence number) */
 	uint64_t pend_m;        /* ... last pending multi-session call */
+	const struct tk_owner *pend_own; /* the thread that issued them */
 };
+
+/*
+ * Completion counter of one thread's asynchronous calls, readable by every
+ * thread: a session with calls of thread A pending is busy for thread B
+ * until A has completed them (srtp_batch_wait or any later entry point
+ * of A), and B's calls on it return EBUSY meanwhile (re_srtp_batch.h).
+ * Allocated on a thread's first asynchronous call and never freed
+ * (sessions may name it after the thread has exited).
+ */
+struct tk_owner {
+	uint64_t done;          /* sequence number of the last completed call */
+};
+
+static __thread struct tk_owner *t_own;
+
+static struct tk_owner *tk_me(void)
+{
+	if (!t_own)
+		t_own = calloc(1, sizeof(*t_own));
+	return t_own;
+}
+
+/* another thread's asynchronous call on s is still pending */
+static int sess_busy(const struct srtp *s)
+{
+	const struct tk_owner *o = s->pend_own;
+	uint64_t p;
+	if (!o || o == t_own)
+		return 0;
+	p = s->pend_p > s->pend_m ? s->pend_p : s->pend_m;
+	return __atomic_load_n(&o->done, __ATOMIC_ACQUIRE) < p;
+}
 
 /*
  * Resident state (sgpu_sst_*): multi-session device batches keep each
@@ -152,6 +185,8 @@ static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
 static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
 static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
+static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
+				   host completed, re-run when waited for */
 /* fault injection (srtp_gpu_tune "fail_grow", like the reference's
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
  * now fails with ENOMEM */
@@ -180,6 +215,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcpackets"))
 		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
+	if (!strcmp(name, "gated"))
+		return __atomic_load_n(&g_cnt_gated, __ATOMIC_RELAXED);
 	return 0;
 }
 
@@ -1428,9 +1465,12 @@ static int sess_host(struct srtp **sessv, size_t nsess)
 	size_t k, m = 0;
 	int err = 0;
 
-	for (k = 0; k < nsess; k++)
+	for (k = 0; k < nsess; k++) {
+		if (sessv[k] && sess_busy(sessv[k]))
+			return EBUSY;
 		if (sessv[k] && sessv[k]->dres == DRES_DEV)
 			m++;
+	}
 	if (m) {
 		lst = malloc(m * sizeof(*lst));
 		slots = malloc(m * sizeof(*slots));
@@ -1733,6 +1773,8 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 
 	if (!srtp || !mb)
 		return EINVAL;
+	if (sess_busy(srtp))
+		return EBUSY;   /* another thread's asynchronous call on it */
 	if (g_env.nocombine || tk_pending()) {
 		err = run_mbufs(op, srtp, &mb, &e, 1);
 		return err ? err : e;
@@ -2371,6 +2413,7 @@ struct mpg {
 	atomic_uint nup;        /* ... how many */
 	uint64_t pend, done;    /* async: this call's sequence number, the
 				   thread's last completed one */
+	const struct tk_owner *own;     /* ... and the issuing thread */
 };
 
 static void mplan_gather_part(void *arg, size_t a, size_t b)
@@ -2396,14 +2439,21 @@ static void mplan_gather_part(void *arg, size_t a, size_t b)
 		}
 		if (g->cm)
 			g->cm[k] = 2u * s->slot;        /* comp[0] = RTP */
+		/* another thread's pending call: not plannable here (the
+		 * host paths behind a rejected plan return EBUSY) */
+		if (s->pend_own && s->pend_own != g->own && sess_busy(s)) {
+			atomic_store(&g->bad, 1);
+			return;
+		}
 		if (g->pend) {
 			/* a pending single-stream call plans from host state
 			 * this call cannot see yet */
-			if (s->pend_p > g->done) {
+			if (s->pend_own == g->own && s->pend_p > g->done) {
 				atomic_store(&g->bad, 1);
 				return;
 			}
 			((struct srtp *)s)->pend_m = g->pend;
+			((struct srtp *)s)->pend_own = g->own;
 		}
 		if (g->need) {
 			/* resident states: upload only what the host changed
@@ -2436,7 +2486,7 @@ static int mplan_gather(struct srtp **sessv, size_t nsess,
 			struct sgpu_sstate *st, uint32_t *cm)
 {
 	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, NULL,
-			0, 0, 0};
+			0, 0, 0, t_own};
 	do {
 		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
 	} while (!g.epoch);
@@ -2457,7 +2507,7 @@ static int mplan_gather_res(struct srtp **sessv, size_t nsess,
 			    uint64_t done)
 {
 	struct mpg g = {sessv, st, NULL, cm, sessv[0]->suite, 0, 0, 0, need,
-			0, pend, done};
+			0, pend, done, t_own};
 	size_t k;
 	do {
 		g.epoch = __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELAXED);
@@ -2509,7 +2559,8 @@ static void mplan_apply_part(void *arg, size_t a, size_t b)
 static void mplan_apply(struct srtp **sessv, size_t nsess,
 			const struct sgpu_sstate *o, int prot)
 {
-	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0, NULL, 0, 0, 0};
+	struct mpg g = {sessv, NULL, o, NULL, 0, prot, 0, 0, NULL, 0, 0, 0,
+			t_own};
 	par_for(nsess, mplan_par(), mplan_apply_part, &g);
 }
 
@@ -3202,6 +3253,7 @@ struct dcall {
 	double t[3];
 	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
 	struct sgpu_splan_in sin; /* several streams: the plan input */
+	int devfold;            /* many sessions: fold queued on the device */
 };
 
 /* single-stream RTP batch planned and processed on the device: the
@@ -3218,6 +3270,7 @@ static int dev_planned_issue(struct dcall *k)
 	const uint32_t need = prot ? (c0->mode == SGPU_MODE_GCM ? 16u :
 			      (T > 4 ? T : 4u)) : 0u;
 	struct sgpu_plan_out *po, *po_d;
+	struct sgpu_fold_out *fo_d;
 	struct sgpu_hdr *hd_d;
 	uint64_t *desc_d;
 	uint32_t *scr, *es_d, *save_d, *nfail_d, *flist_d;
@@ -3278,15 +3331,35 @@ static int dev_planned_issue(struct dcall *k)
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
+	/* unprotect: the verdict fold queued behind the kernels (nothing to
+	 * do without a miss), so a forged packet neither gates the next
+	 * chained call nor waits for the host (sgpu_fold_rtp) */
+	k->devfold = !prot && !g_env.nodevfold;
+	fo_d = (struct sgpu_fold_out *)(w->pl.d + foff);
+	if (!err && k->devfold)
+		err = sgpu_fold_rtp(1, nfail_d, &k->in, hd_d, desc_d, vd_d, es_d,
+				    d->pos, d->end, d->err,
+				    c0->mode == SGPU_MODE_GCM,
+				    (uint32_t *)(w->pl.d + foff + 64), fo_d,
+				    stream);
 	/* results, gate word and the miss count next to the plan: one
 	 * launch, one copy into pinned memory */
 	if (!err)
 		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
 				       (uint32_t)n,
 				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
-				       k->gate, &po_d->nfail, stream);
+				       k->gate, &po_d->nfail,
+				       k->devfold ? &fo_d->fail : NULL, stream);
+	if (!err && k->devfold)
+		err = sgpu_fold_rtp(2, nfail_d, &k->in, hd_d, desc_d, vd_d, es_d,
+				    d->pos, d->end, d->err,
+				    c0->mode == SGPU_MODE_GCM,
+				    (uint32_t *)(w->pl.d + foff + 64), fo_d,
+				    stream);
+	/* plan out and fold out in one copy */
 	if (!err)
-		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+		err = sgpu_memcpy_d2h(po, po_d, k->devfold ? foff + sizeof(*fo_d)
+							  : sizeof(*po), stream);
 	return err;
 }
 
@@ -3335,22 +3408,11 @@ static int dev_planned_finish(struct dcall *k)
 	 * place); the fold checks that the speculated rollovers and indices
 	 * hold under the true s_l and writes the EAUTH results, s_l and the
 	 * replay window (sgpu_fold_rtp). */
-	if (!prot && !g_env.nodevfold) {
-		struct sgpu_fold_out *fo = (struct sgpu_fold_out *)(w->pl.h + foff);
-		struct sgpu_fold_out *fo_d =
-			(struct sgpu_fold_out *)(w->pl.d + foff);
-		err = sgpu_fold_rtp(&k->in, hd_d, desc_d, vd_d, es_d, d->pos,
-				    d->end, d->err, c0->mode == SGPU_MODE_GCM,
-				    (uint32_t *)(w->pl.d + foff + 64), fo_d,
-				    stream);
-		if (!err)
-			err = sgpu_memcpy_d2h(fo, fo_d, sizeof(*fo), stream);
-		if (!err)
-			err = sgpu_stream_sync(stream);
-		if (err) {
-			plan_unapply(s, ns0, &old);
-			return err;
-		}
+	if (!prot && k->devfold) {
+		/* folded on the device behind the kernels (dev_planned_issue);
+		 * its verdict came back with the plan */
+		const struct sgpu_fold_out *fo =
+			(const struct sgpu_fold_out *)(w->pl.h + foff);
 		if (!fo->fail) {
 			struct srtp_stream *st = &s->streams[0];
 			st->s_l = (uint16_t)fo->s_l;
@@ -3529,7 +3591,7 @@ static int dev_splanned_issue(struct dcall *k)
 		err = sgpu_plan_finish(&po_d->base.fail, es_d, d->end, d->err,
 				       (uint32_t)n,
 				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
-				       k->gate, &po_d->base.nfail, stream);
+				       k->gate, &po_d->base.nfail, NULL, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
 	return err;
@@ -3698,7 +3760,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
 				       (uint32_t)n,
 				       prot ? (int32_t)grow : -(int32_t)grow,
-				       nfail_d, NULL, &po_d->nfail, stream);
+				       nfail_d, NULL, &po_d->nfail, NULL, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
 	if (!err)
@@ -3756,6 +3818,30 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
  * The launches; -1: not plannable (after a synchronisation; nothing
  * modified).
  */
+/* the multi-session verdict fold over the call's planner scratch (phase:
+ * sgpu_mfold_rtp; nfail: the kernels' miss count, device, or NULL) */
+static int mfold(struct dcall *k, int phase, const uint32_t *nfail,
+		 const struct sgpu_sstate *sin_d, struct sgpu_sstate *sout_d,
+		 size_t scr)
+{
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const size_t n = d->n;
+	struct sgpu_mplan_in in;
+	memset(&in, 0, sizeof(in));
+	in.n = (uint32_t)n;
+	in.nsess = (uint32_t)k->nsess;
+	return sgpu_mfold_rtp(phase, nfail, &in, (const struct sgpu_hdr *)w->hd.d,
+			      d->sess, (const uint64_t *)w->dsc.d,
+			      w->vs.d + 64 + n * 4, (const uint32_t *)w->es.d,
+			      d->pos, d->end, d->err,
+			      k->sessv[0]->rtp.mode == SGPU_MODE_GCM, sin_d,
+			      sout_d, w->mscr.d, scr,
+			      (uint32_t *)(w->pl.d + k->foff + 64),
+			      (struct sgpu_fold_out *)(w->pl.d + k->foff),
+			      d->stream);
+}
+
 static int dev_mplanned_issue(struct dcall *k)
 {
 	const int prot = k->op == OP_RTP_ENC;
@@ -3768,6 +3854,7 @@ static int dev_mplanned_issue(struct dcall *k)
 	const uint32_t T = c0->mode == SGPU_MODE_GCM ? 16u : c0->tag_len;
 	const int gcm = c0->mode == SGPU_MODE_GCM;
 	struct sgpu_plan_out *po, *po_d;
+	struct sgpu_fold_out *fo_d;
 	struct sgpu_sstate *up_h, *up_d, *sin_d, *sout_d;
 	struct sgpu_mplan_in in;
 	struct sgpu_hdr *hd_d;
@@ -3895,19 +3982,32 @@ static int dev_mplanned_issue(struct dcall *k)
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
+	/* unprotect: the verdict fold queued behind the kernels (it does
+	 * nothing without a miss), so a forged packet neither gates the next
+	 * chained call nor waits for the host: srtp.c:310-321, 342-359,
+	 * 426-427 per session segment (sgpu_mfold_rtp) */
+	k->devfold = !prot && !g_env.nodevfold;
+	fo_d = (struct sgpu_fold_out *)(w->pl.d + k->foff);
+	if (!err && k->devfold)
+		err = mfold(k, 1, nfail_d, sin_d, sout_d, scr);
 	if (!err)
 		err = sgpu_plan_finish(&po_d->fail, es_d, d->end, d->err,
 				       (uint32_t)n,
 				       prot ? (int32_t)T : -(int32_t)T, nfail_d,
-				       k->gate, &po_d->nfail, stream);
-	/* the new states replace the resident ones if the plan held and every
-	 * tag verified (a forged packet: the host folds from the old ones) */
+				       k->gate, &po_d->nfail,
+				       k->devfold ? &fo_d->fail : NULL, stream);
+	if (!err && k->devfold)
+		err = mfold(k, 2, nfail_d, sin_d, sout_d, scr);
+	/* the new states replace the resident ones if the plan held and
+	 * every tag verified or the fold held (else the host folds from the
+	 * old ones) */
 	if (!err)
 		err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
-				      (uint32_t)nsess, &po_d->fail, nfail_d,
-				      stream);
+				      (uint32_t)nsess, &po_d->fail,
+				      k->devfold ? &fo_d->fail : nfail_d, stream);
+	/* plan out and fold out in one copy */
 	if (!err)
-		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+		err = sgpu_memcpy_d2h(po, po_d, k->foff + sizeof(*fo_d), stream);
 	k->t[2] = times ? now_ms() : 0;
 	return err;
 }
@@ -3955,36 +4055,11 @@ static int dev_mplanned_finish(struct dcall *k)
 	 * GCM: decrypted in place); the fold checks the speculation under the
 	 * true s_l and writes the EAUTH results and the touched sessions'
 	 * states, which then replace the resident ones. */
-	if (!prot && !g_env.nodevfold) {
-		const size_t foff = k->foff;
-		struct sgpu_fold_out *fo = (struct sgpu_fold_out *)(w->pl.h + foff);
-		struct sgpu_fold_out *fo_d =
-			(struct sgpu_fold_out *)(w->pl.d + foff);
-		struct sgpu_sstate *sin_d = (struct sgpu_sstate *)w->ms.d;
-		struct sgpu_sstate *sout_d = sin_d + k->nsess;
-		struct sgpu_mplan_in in;
-		size_t scr = sgpu_mplan_scratch((uint32_t)n,
-						(uint32_t)k->nsess);
-		memset(&in, 0, sizeof(in));
-		in.n = (uint32_t)n;
-		in.nsess = (uint32_t)k->nsess;
-		err = sgpu_mfold_rtp(&in, hd_d, d->sess, desc_d, vd_d, es_d,
-				     d->pos, d->end, d->err,
-				     c0->mode == SGPU_MODE_GCM, sin_d, sout_d,
-				     w->mscr.d, scr,
-				     (uint32_t *)(w->pl.d + foff + 64), fo_d,
-				     stream);
-		/* commit on the fold's verdict (pad: a zero word) */
-		if (!err)
-			err = sgpu_sst_commit((const uint32_t *)w->cm.d, sout_d,
-					      (uint32_t)k->nsess, &fo_d->fail,
-					      &fo_d->pad, stream);
-		if (!err)
-			err = sgpu_memcpy_d2h(fo, fo_d, sizeof(*fo), stream);
-		if (!err)
-			err = sgpu_stream_sync(stream);
-		if (err)
-			return err;
+	if (!prot && k->devfold) {
+		/* folded on the device behind the kernels (dev_mplanned_issue);
+		 * its verdict came back with the plan */
+		const struct sgpu_fold_out *fo =
+			(const struct sgpu_fold_out *)(w->pl.h + k->foff);
 		if (!fo->fail) {
 			count(&g_cnt_devfolds, 1);
 			return 0;
@@ -4079,12 +4154,14 @@ static void tk_finish_one(void)
 		t_tk_tail = NULL;
 	t_tk_n--;
 	t_tk_done = t->seq;
+	__atomic_store_n(&t_own->done, t->seq, __ATOMIC_RELEASE);
 	t_aws[t_naws++] = k->w;
 	sgpu_event_destroy(t->ev);
 	t->ev = NULL;
 	if (r == -2) {
 		/* gated behind an earlier call that the host completed:
 		 * nothing was modified, run it now */
+		count(&g_cnt_gated, 1);
 		r = run_dev(k->op, k->sessv, k->nsess, &k->d);
 	}
 	else if (r == -1) {
@@ -4146,6 +4223,11 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 	t->owner = pthread_self();
 	*tp = t;
 	env_init();
+	if (!tk_me()) {
+		t->kind = TK_DONE;
+		t->result = ENOMEM;
+		return 0;
+	}
 	/* the chain's gate words are ordered by the stream */
 	if (t_tk_n && t_tk_stream != d->stream)
 		tk_drain();
@@ -4171,8 +4253,9 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 		struct srtp *s = sessv[0];
 		uint64_t p = s->pend_p > s->pend_m ? s->pend_p : s->pend_m;
 		/* plans from the host copy of its state: the pending calls
-		 * on it complete first */
-		if (p > t_tk_done)
+		 * on it complete first (this thread's; another thread's
+		 * make sess_host return EBUSY) */
+		if (s->pend_own == t_own && p > t_tk_done)
 			tk_drain_upto(p);
 		table_rdlock();
 		err = sess_host(&s, 1);
@@ -4236,8 +4319,10 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 	}
 	t_tk_seq = t->seq;
 	t->kind = kind;
-	if (kind == TK_PLANNED || kind == TK_SPLANNED)
+	if (kind == TK_PLANNED || kind == TK_SPLANNED) {
 		sessv[0]->pend_p = t->seq;
+		sessv[0]->pend_own = t_own;
+	}
 	if (t_tk_tail)
 		t_tk_tail->next = t;
 	else

@@ -4,7 +4,7 @@
  * libre's own headers and linked into libre.
  *
  * In libre an SRTP transform is a helper on the socket's chain
- * (udp_register_helper, /root/reference/src/udp/udp.c:830-860): udp_read()
+ * (udp_register_helper, reference src/udp/udp.c:830-860): udp_read()
  * (:149-211) receives one datagram per poll event into a fresh mbuf and
  * walks the receive hooks; udp_send() -> udp_send_internal() (:484-507)
  * walks the send hooks in reverse before sendto().  This helper's hooks

@@ -453,8 +453,11 @@ struct sgpu_fold_out {
 
 /* scratch: >= 5 * (n / 256 + 2) words.  gcm: EAUTH leaves end as is.
  * Runs after the crypto kernels (verdict[] complete); results written
- * only if the fold holds (out->fail == 0). */
-int   sgpu_fold_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
+ * only if the fold holds (out->fail == 0).  phase 0: all; 1: the verdict
+ * (out); 2: the forged packets' results.  nfail (device, may be NULL):
+ * the kernels' miss count -- the fold does nothing when it is 0. */
+int   sgpu_fold_rtp(int phase, const uint32_t *nfail,
+		    const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
 		    const uint64_t *desc, const uint8_t *verdict,
 		    const uint32_t *end0, uint32_t *pos, uint32_t *end,
 		    int32_t *err, int gcm, uint32_t *scratch,
@@ -464,9 +467,13 @@ int   sgpu_fold_rtp(const struct sgpu_plan_in *in, const struct sgpu_hdr *hdr,
  * (same scratch, still holding the sort): per session segment what
  * sgpu_fold_rtp does for one stream.  Writes the EAUTH results and the
  * touched sessions' s_l / replay window into st_out only if the fold holds
- * (out->fail == 0); fscratch: sgpu_mfold_scratch(n) bytes. */
+ * (out->fail == 0); fscratch: sgpu_mfold_scratch(n) bytes.  phase 0: all;
+ * 1: the verdict only (out->fail); 2: results and windows.  nfail (device,
+ * may be NULL): the crypto kernels' miss count -- queued behind them, the
+ * fold does nothing when it is 0 (out->fail = 0). */
 size_t sgpu_mfold_scratch(uint32_t n);
-int   sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
+int   sgpu_mfold_rtp(int phase, const uint32_t *nfail,
+		     const struct sgpu_mplan_in *in,
 		     const struct sgpu_hdr *hdr, const uint32_t *sess,
 		     const uint64_t *desc, const uint8_t *verdict,
 		     const uint32_t *end0, uint32_t *pos, uint32_t *end,
@@ -479,11 +486,14 @@ int   sgpu_mfold_rtp(const struct sgpu_mplan_in *in,
  * if *guard == 0: end[i] = end0[i] + delta, err[i] = 0 */
 /* sgpu_plan_results, and in the same launch: *gate = *guard || *nfail
  * (sgpu_gate_set; gate may be NULL) and *nfail_out = *nfail (next to the
- * plan, so one copy brings both back; nfail_out may be NULL) */
+ * plan, so one copy brings both back; nfail_out may be NULL).  ffail
+ * (may be NULL): the device fold's verdict word -- a miss then gates the
+ * next call only if the fold failed: *gate = *guard || (*nfail && *ffail) */
 int   sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
 		       uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
 		       const uint32_t *nfail, uint32_t *gate,
-		       uint32_t *nfail_out, void *stream);
+		       uint32_t *nfail_out, const uint32_t *ffail,
+		       void *stream);
 int   sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
 			uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
 			void *stream);

@@ -23,6 +23,7 @@ SRTP_AES_256_GCM = 5
 SUITES = range(6)
 SRTP_UNENCRYPTED_SRTCP = 1 << 1
 EAUTH = 217
+EBUSY = 16      # Linux errno.h
 
 _KEY = {0: 16, 1: 16, 2: 32, 3: 32, 4: 16, 5: 32}
 _SALT = {0: 14, 1: 14, 2: 14, 3: 14, 4: 12, 5: 12}

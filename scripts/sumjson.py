@@ -1,20 +1,14 @@
-#!/usr/bin/env python3
-"""One summary line per bench.py JSON line in the given files:
-value, Mpkt/s, ms/step, round-trip check and the two heaviest kernels."""
+"""one line per bench JSON file: value, step time, dominant kernel, folds"""
 import json
 import sys
 
-for path in sys.argv[1:]:
+for f in sys.argv[1:]:
     try:
-        lines = open(path).read().strip().splitlines()
-    except OSError as e:
-        print(path, "missing:", e)
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 -- a failed run's file
+        print(f"{f:40s} ERR {e}")
         continue
-    for l in lines:
-        if not l.startswith("{"):
-            continue
-        d = json.loads(l)
-        ks = (d.get("roofline") or {}).get("kernels", [])[:2]
-        print(path.split("/")[-1], d["value"], d.get("mpkt_s"),
-              d["ms_per_step"], d.get("verified_roundtrip"),
-              [(k["dir"], k["avg_ms"]) for k in ks])
+    r = d.get("roofline") or {}
+    print(f"{f:40s} {d.get('value')} {d.get('unit')} ms={d.get('ms_per_step')}"
+          f" {r.get('kernel')} {r.get('avg_launch_ms')} frac={r.get('frac')}"
+          f" folds={d.get('folds')} plans={d.get('plans')}")

@@ -193,3 +193,49 @@ def test_async_then_sync_calls_drain(torch_cuda):
     assert P.batch_wait(t) == 0
     assert not d.out()[3].any()
     tx.close()
+
+
+def test_async_pending_session_busy_for_other_threads(torch_cuda):
+    """a session with a pending asynchronous call of one thread is busy for
+    every other thread (EBUSY, nothing changed) until the issuing thread
+    completes the call; afterwards the other thread's calls run normally"""
+    import threading
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    key = keys_for(1, 1)[0]
+    tx = P.Srtp(1, key)
+    other = P.Srtp(1, key)
+    d1 = Dev(torch, *to_arena(seq_batch(rng, range(10, 1010)))[:4], None)
+    d2 = Dev(torch, *to_arena(seq_batch(rng, range(1010, 1110)))[:4], None)
+    d3 = Dev(torch, *to_arena(seq_batch(rng, range(10, 110)))[:4], None)
+    rc, t, keep = P.device_batch_dev_async("srtp_encrypt", [tx], *d1.args())
+    assert rc == 0
+    got = {}
+
+    def worker(tag):
+        got[tag + "_dev"] = P.device_batch_dev("srtp_encrypt", [tx],
+                                               *d2.args())
+        mb = P.new_mbuf(bytes.fromhex("80000001000000000000abcd") +
+                        b"\x11" * 40, 512)
+        got[tag + "_one"] = tx.encrypt(mb)
+        P.free_mbuf(mb)
+        # a session nobody else has pending calls on is not affected
+        got[tag + "_free"] = P.device_batch_dev("srtp_encrypt", [other],
+                                                *d3.args())
+
+    th = threading.Thread(target=worker, args=("busy",))
+    th.start()
+    th.join()
+    assert got["busy_dev"] == P.EBUSY and got["busy_one"] == P.EBUSY
+    assert got["busy_free"] == 0
+    torch.cuda.synchronize()
+    assert (d2.err.cpu().numpy() == -1).all()   # untouched
+    assert P.batch_wait(t) == 0
+    th = threading.Thread(target=worker, args=("done",))
+    th.start()
+    th.join()
+    assert got["done_dev"] == 0 and got["done_one"] == 0
+    e, st = tx.export(0x5151)
+    assert e == 0 and st.s_l == 1109
+    tx.close()
+    other.close()

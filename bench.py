@@ -719,6 +719,10 @@ def main():
                 if ent and ent.get("int_frac") is not None else None,
                 "lds_frac": round(ent["lds_frac"], 4)
                 if ent and ent.get("lds_frac") is not None else None,
+                "lds_floor_frac": round(ent["lds_floor_frac"], 4)
+                if ent and ent.get("lds_floor_frac") is not None else None,
+                "issue_frac": round(ent["issue_frac"], 4)
+                if ent and ent.get("issue_frac") is not None else None,
                 "pmc_src": os.path.basename(pj) + ":" + wl if ent else None,
                 "kernel": dom["kernel"],
                 "dir": dom["dir"],

@@ -37,6 +37,34 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x)
 }
 
 /* gfx950 v_bitop3_b32: bit = TT[(a << 2) | (b << 1) | c] */
+/*
+ * gfx950 VALU issue (scripts/ubench_ops.hip, profiles/r03_ubench_ops.txt):
+ * v_xor/or/and/add/mov/lshrrev_b32, v_lshlrev_b16 and v_bitop3_b32 with
+ * VGPR (or, VOP2, constant) operands issue at the full rate; any VALU op
+ * reading an SGPR, and v_perm, v_alignbit, v_add3, v_lshlrev_b32, v_bfe,
+ * DPP, at about 0.6 of it.  vreg() hands a uniform value (a round key, a
+ * mask) to its users through a VGPR (a pure asm: copies of one value are
+ * merged, loop-invariant ones hoisted), so e.g. the four blocks of a chunk
+ * XOR a round key with full-rate v_bitop3 (RK_VCOPY).
+ */
+#ifndef RK_VCOPY
+#define RK_VCOPY 0
+#endif
+__device__ __forceinline__ uint32_t vreg(uint32_t k)
+{
+	asm("" : "+v"(k));
+	return k;
+}
+
+__device__ __forceinline__ uint32_t rkv(uint32_t k)
+{
+#if RK_VCOPY
+	return vreg(k);
+#else
+	return k;
+#endif
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
 	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -54,18 +82,24 @@ __device__ __forceinline__ uint32_t sha_maj(uint32_t b, uint32_t c, uint32_t d)
 }
 
 /* LDS T-table address of byte k of x for this lane (laneoff = (lane&31)*4):
- * ((byte k of x) << 8) | laneoff, one v_perm_b32.  TT_B1_BITOP3: byte 1,
- * already in place, as one v_bitop3_b32 ((x & 0xff00) | laneoff), which
- * issues at twice the v_perm rate (profiles/r01_ubench_valu_rates.log) --
- * measured no faster in the kernels (same-box A/B): off */
+ * ((byte k of x) << 8) | laneoff, one v_perm_b32 (half rate).  Byte 1 is
+ * already in place: TT_B1_BITOP3 makes it one v_bitop3_b32 ((x & 0xff00) |
+ * laneoff) -- 1: the mask as a constant (the compiler puts it in an SGPR,
+ * which makes the op half rate again: no gain), 2 (default): the mask in
+ * a VGPR, full rate.  Same-box A/B (profiles/r03_ab_b1v.txt): config-2
+ * unprotect 1.244 -> 1.221 ms; GCM (LDS-bound) unchanged. */
 #ifndef TT_B1_BITOP3
-#define TT_B1_BITOP3 0
+#define TT_B1_BITOP3 2
 #endif
 template <int K>
 __device__ __forceinline__ uint32_t tt_addr(uint32_t x, uint32_t laneoff)
 {
-	if (K == 1 && TT_B1_BITOP3)
+	if (K == 1 && TT_B1_BITOP3 == 1)
 		return __builtin_amdgcn_bitop3_b32(x, 0xff00u, laneoff, 0xEA);
+	/* 2: the mask in a VGPR (full-rate v_bitop3, see vreg) */
+	if (K == 1 && TT_B1_BITOP3 == 2)
+		return __builtin_amdgcn_bitop3_b32(x, vreg(0xff00u), laneoff,
+						   0xEA);
 	return __builtin_amdgcn_perm(x, laneoff, 0x0C0C0000u | ((4u + K) << 8));
 }
 #define TT_ADDR(x, k, laneoff) tt_addr<(k)>((x), (laneoff))
@@ -108,10 +142,10 @@ __device__ __forceinline__ void aes_round(const uint8_t *smem, uint32_t lo,
 	uint32_t b0 = lds_u32(smem, TT_ADDR(s0, 1, lo) + 128);
 	uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
 	uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
-	s0 = xor3(a0, b1, rot16(xor3(c2, d3, k[0])));
-	s1 = xor3(a1, b2, rot16(xor3(c3, d0, k[1])));
-	s2 = xor3(a2, b3, rot16(xor3(c0, d1, k[2])));
-	s3 = xor3(a3, b0, rot16(xor3(c1, d2, k[3])));
+	s0 = xor3(a0, b1, rot16(xor3(c2, d3, rkv(k[0]))));
+	s1 = xor3(a1, b2, rot16(xor3(c3, d0, rkv(k[1]))));
+	s2 = xor3(a2, b3, rot16(xor3(c0, d1, rkv(k[2]))));
+	s3 = xor3(a3, b0, rot16(xor3(c1, d2, rkv(k[3]))));
 }
 
 /* final round (SubBytes, ShiftRows, AddRoundKey; k plain) */
@@ -138,13 +172,13 @@ __device__ __forceinline__ void aes_final(const uint8_t *smem, uint32_t lo,
 	uint32_t c1 = lds_u32(smem, TT_ADDR(s1, 2, lo));
 	uint32_t d2 = lds_u32(smem, TT_ADDR(s2, 3, lo) + 128);
 	s0 = xor3(__builtin_amdgcn_perm(a0, b1, 0x0C0C0105u),
-		  __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu), k[0]);
+		  __builtin_amdgcn_perm(c2, d3, 0x03060C0Cu), rkv(k[0]));
 	s1 = xor3(__builtin_amdgcn_perm(a1, b2, 0x0C0C0105u),
-		  __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu), k[1]);
+		  __builtin_amdgcn_perm(c3, d0, 0x03060C0Cu), rkv(k[1]));
 	s2 = xor3(__builtin_amdgcn_perm(a2, b3, 0x0C0C0105u),
-		  __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu), k[2]);
+		  __builtin_amdgcn_perm(c0, d1, 0x03060C0Cu), rkv(k[2]));
 	s3 = xor3(__builtin_amdgcn_perm(a3, b0, 0x0C0C0105u),
-		  __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu), k[3]);
+		  __builtin_amdgcn_perm(c1, d2, 0x03060C0Cu), rkv(k[3]));
 }
 
 /* rounds FIRST .. NR on a state that has been through rounds 0..FIRST-1 */
@@ -190,8 +224,15 @@ __device__ __forceinline__ void aes_block(const uint8_t *smem, uint32_t lo,
  */
 #define TT4_BYTES 131072u
 
-#define TT_ADDRH(x, k, hi) \
-	__builtin_amdgcn_perm((x), (hi), 0x0C020000u | ((4u + (k)) << 8))
+/* the same with bytes 0 and 2 of hi kept (hi < 2^24, byte 1 zero) */
+__device__ __forceinline__ uint32_t tt_addrh(uint32_t x, uint32_t k,
+					     uint32_t hi)
+{
+	if (k == 1 && TT_B1_BITOP3 == 2)
+		return __builtin_amdgcn_bitop3_b32(x, vreg(0xff00u), hi, 0xEA);
+	return __builtin_amdgcn_perm(x, hi, 0x0C020000u | ((4u + k) << 8));
+}
+#define TT_ADDRH(x, k, hi) tt_addrh((x), (k), (hi))
 
 __device__ __forceinline__ void tt4_fill(uint8_t *smem, const uint32_t *T0g)
 {
@@ -235,10 +276,10 @@ __device__ __forceinline__ void aes4_round(const Tt4 &T, const uint32_t *k,
 	const uint32_t a1 = T.t0(s1), b2 = T.t1(s2), c3 = T.t2(s3), d0 = T.t3(s0);
 	const uint32_t a2 = T.t0(s2), b3 = T.t1(s3), c0 = T.t2(s0), d1 = T.t3(s1);
 	const uint32_t a3 = T.t0(s3), b0 = T.t1(s0), c1 = T.t2(s1), d2 = T.t3(s2);
-	s0 = xor3(xor3(a0, b1, c2), d3, k[0]);
-	s1 = xor3(xor3(a1, b2, c3), d0, k[1]);
-	s2 = xor3(xor3(a2, b3, c0), d1, k[2]);
-	s3 = xor3(xor3(a3, b0, c1), d2, k[3]);
+	s0 = xor3(xor3(a0, b1, c2), d3, rkv(k[0]));
+	s1 = xor3(xor3(a1, b2, c3), d0, rkv(k[1]));
+	s2 = xor3(xor3(a2, b3, c0), d1, rkv(k[2]));
+	s3 = xor3(xor3(a3, b0, c1), d2, rkv(k[3]));
 }
 
 template <int NR, int FIRST>

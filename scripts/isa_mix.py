@@ -7,7 +7,13 @@ Compiles the kernel translation units to assembly (hipcc --cuda-device-only
 -S, the product's flags), finds each kernel's largest loop block (the
 steady 64-byte chunk) and records its opcode histogram.  scripts/pmc_r03.py
 weights the measured per-opcode issue rates (scripts/ubench_valu.hip) by
-this mix to get each kernel's VALU issue floor.
+this mix to get each kernel's VALU issue floor.  Each
+instruction is also classed by its measured gfx950 issue rate
+(scripts/ubench_ops.hip, profiles/r03_ubench_ops.txt): "fast" (full-rate
+VALU: v_xor/or/and/add/sub/mov/not/lshrrev_b32, v_ashrrev, v_lshlrev_b16,
+v_lshrrev_b16, v_bitop3 -- without an SGPR operand), "slow" (every other
+VALU op, and any VALU op reading an SGPR), "lds" (ds_read/ds_write),
+"lds_b128" (16-byte LDS reads, 4x the bytes).
 """
 import collections
 import json
@@ -43,6 +49,26 @@ def short(sym):
     else:
         prot = args[1]
     return "%s<%d,%d>" % (name, nr, 1 if prot == "true" else 0)
+
+
+FAST = {"v_xor_b32", "v_or_b32", "v_and_b32", "v_add_u32", "v_sub_u32",
+        "v_subrev_u32", "v_mov_b32", "v_not_b32", "v_lshrrev_b32",
+        "v_ashrrev_i32", "v_lshlrev_b16", "v_lshrrev_b16", "v_bitop3_b32"}
+
+
+def iclass(ins):
+    """issue class of one instruction (see the module docstring)"""
+    parts = ins.split(None, 1)
+    op, args = parts[0], parts[1] if len(parts) > 1 else ""
+    if op.startswith("ds_"):
+        return "lds_b128" if op.endswith("b128") else "lds"
+    if not op.startswith("v_") or op.startswith(("v_readfirstlane",
+                                                  "v_readlane",
+                                                  "v_writelane")):
+        return "other"
+    base = re.sub(r"_e(32|64)$", "", op)
+    sgpr = re.search(r"(?<![a-z_])s\[?\d", args) is not None
+    return "fast" if base in FAST and not sgpr else "slow"
 
 
 def blocks(lines, start, end):
@@ -94,8 +120,10 @@ def main():
                 continue
             big = max(loops, key=lambda b: len(bl[b]))
             ops = collections.Counter(x.split()[0] for x in bl[big])
+            cl = collections.Counter(iclass(x) for x in bl[big])
             res[short(sym)] = {"block": big, "n": len(bl[big]),
-                               "ops": dict(ops.most_common())}
+                               "ops": dict(ops.most_common()),
+                               "classes": dict(cl)}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, v in sorted(res.items()):
         print(k, v["n"])

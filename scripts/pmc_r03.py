@@ -10,49 +10,51 @@ bench.py builds ("config2", "config3_rtcp", ...).
               HBM / rocprofv3: KiB, separate passes, gfx950 FETCH_SIZE
               reports half of a wide streaming read)
   int_frac  = the kernel's VALU issue floor / its duration.  Floor =
-              SQ_INSTS_VALU / 1024 SIMDs x sum over the steady loop's
-              opcode mix (profiles/r03_isa_mix.json, scripts/isa_mix.py)
-              of fraction / issue rate, the rates measured per opcode at 4
-              waves/SIMD (scripts/ubench_valu.hip, profiles/
-              r03_ubench_valu.txt); opcodes not measured take the v_xor
-              rate (the fastest: the floor is not overstated)
+              SQ_INSTS_VALU x 64 lanes x (f_fast / R_fast + f_slow /
+              R_slow): f = the steady loop's full-rate / half-rate VALU
+              shares (profiles/r03_isa_mix.json "classes",
+              scripts/isa_mix.py), R = the chip-wide lane-op rates of the
+              two classes measured at 8 waves/SIMD (medians over the
+              instruction forms of scripts/ubench_ops.hip,
+              profiles/r03_ubench_ops.txt)
+  lds_floor_frac = SQ_INSTS_LDS x 64 x (f_b32 + 4 f_b128) / R_lds over the
+              duration, R_lds the conflict-free ds_read_b32 rate
+              (profiles/r03_ubench_sdwa.txt lds_fast, 8 waves/SIMD)
+  issue_frac = int_frac + lds_floor_frac (the two measured kernels run
+              close to the SUM of the floors, not their maximum)
   lds_frac  = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE / 8 x 256 CUs)
 """
 import csv
 import json
 import os
 import re
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIMDS = 1024
 CRYPTO = ("k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_hmac", "k_gcm")
-# ubench_valu.hip names -> gfx950 opcodes
-UB = {"xor": ["v_xor_b32_e32", "v_xor_b32_e64"],
-      "add": ["v_add_u32_e32", "v_add_u32_e64"],
-      "add3": ["v_add3_u32"], "perm": ["v_perm_b32"],
-      "align": ["v_alignbit_b32"], "bitop3": ["v_bitop3_b32"],
-      "lshl_or": ["v_lshl_or_b32"], "and_or": ["v_and_or_b32"],
-      "bfe": ["v_bfe_u32"], "pk_add": ["v_pk_add_u16"],
-      "lshl": ["v_lshlrev_b32_e32", "v_lshlrev_b32_e64"],
-      "lshr": ["v_lshrrev_b32_e32", "v_lshrrev_b32_e64"],
-      "or": ["v_or_b32_e32", "v_or_b32_e64"],
-      "and": ["v_and_b32_e32", "v_and_b32_e64"],
-      "dpp_mov": ["v_mov_b32_dpp"], "lshl_add": ["v_lshl_add_u32"]}
+FAST_FORMS = ("xor_vv", "xor_kv", "and_kv", "add_kv", "mov_v", "not_v",
+              "lshr_vv", "ashr_8", "lshl_b16", "lshr_b16", "add_vv_e64",
+              "xor_vv_e64", "bitop3_vvv96", "bitop3_vvvec")
 
 
-def rates(path):
-    """opcode -> wave-instructions / s per SIMD at 4 waves/SIMD"""
-    r = {}
-    for ln in open(path):
+def class_rates(ops_txt, sdwa_txt):
+    """chip-wide lane-ops/s of full-rate VALU, half-rate VALU, LDS b32"""
+    fast, slow, lds = [], [], []
+    for ln in open(ops_txt):
         f = ln.split()
-        if len(f) < 2 or f[1] != "waves/SIMD=4" or "[LDS]" in ln:
+        if len(f) < 2 or f[1] != "waves/SIMD=8" or f[0] in ("warm",
+                                                         "cndmask"):
             continue
         t = float(re.search(r"([\d.]+) T lane-ops/s", ln).group(1))
-        for op in UB.get(f[0], []):
-            r[op] = t * 1e12 / (SIMDS * 64)
-    return r
+        (fast if f[0] in FAST_FORMS else slow).append(t * 1e12)
+    for ln in open(sdwa_txt):
+        f = ln.split()
+        if len(f) > 1 and f[0] == "lds_fast" and f[1] == "waves/SIMD=8":
+            lds.append(float(re.search(r"([\d.]+) T lane-ops/s",
+                                       ln).group(1)) * 1e12)
+    med = lambda v: sorted(v)[len(v) // 2]
+    return med(fast), med(slow), med(lds)
 
 
 def short(k):
@@ -96,8 +98,9 @@ def counters(d):
 def main():
     out, wl, fdir, wdir, sdir = sys.argv[1:6]
     mix = json.load(open(os.path.join(ROOT, "profiles", "r03_isa_mix.json")))
-    rt = rates(os.path.join(ROOT, "profiles", "r03_ubench_valu.txt"))
-    xor = rt["v_xor_b32_e32"]
+    r_fast, r_slow, r_lds = class_rates(
+        os.path.join(ROOT, "profiles", "r03_ubench_ops.txt"),
+        os.path.join(ROOT, "profiles", "r03_ubench_sdwa.txt"))
     fa, _, grid = counters(fdir)
     wa, _, _ = counters(wdir)
     sa, sdur, _ = counters(sdir)
@@ -122,13 +125,22 @@ def main():
         s = {c: sum(v) / len(v) for c, v in sa.get(k, {}).items()}
         t = sorted(sdur[k])[len(sdur[k]) // 2] * 1e-9 if sdur.get(k) else 0
         if t and "SQ_INSTS_VALU" in s and name in mix:
-            ops = {o: c for o, c in mix[name]["ops"].items()
-                   if o.startswith("v_") and not o.startswith("v_accvgpr")}
-            tot = sum(ops.values())
-            per = sum(c / tot / rt.get(o, xor) for o, c in ops.items())
-            floor = s["SQ_INSTS_VALU"] / SIMDS * per
+            cl = mix[name]["classes"]
+            nv = cl.get("fast", 0) + cl.get("slow", 0)
+            floor = s["SQ_INSTS_VALU"] * 64 * (
+                cl.get("fast", 0) / nv / r_fast +
+                cl.get("slow", 0) / nv / r_slow)
             e.update(valu_floor_s=floor, kernel_s=t, int_frac=floor / t,
-                     valu_insts=s["SQ_INSTS_VALU"])
+                     valu_insts=s["SQ_INSTS_VALU"],
+                     rates_T={"fast": r_fast / 1e12, "slow": r_slow / 1e12,
+                              "lds_b32": r_lds / 1e12})
+            if "SQ_INSTS_LDS" in s:
+                nl = cl.get("lds", 0) + cl.get("lds_b128", 0)
+                w = (cl.get("lds", 0) + 4 * cl.get("lds_b128", 0)) / nl \
+                    if nl else 1.0
+                lf = s["SQ_INSTS_LDS"] * 64 * w / r_lds
+                e.update(lds_floor_s=lf, lds_floor_frac=lf / t,
+                         issue_frac=(floor + lf) / t)
         if "SQ_LDS_IDX_ACTIVE" in s and s.get("GRBM_GUI_ACTIVE"):
             e["lds_frac"] = s["SQ_LDS_IDX_ACTIVE"] / (
                 s["GRBM_GUI_ACTIVE"] / 8 * 256)

@@ -5,9 +5,13 @@
  * 279-280; srtp_decrypt srtp.c:310-321, 426-427; srtp_get_index
  * misc.c:22-41; srtp_replay_check replay.c:32-62) runs per stream, and
  * streams of different sessions are independent.  Here:
- *   1. packets are stably sorted by session (hipCUB LSD radix sort of the
- *      session index, values = packet index), so each session's packets
- *      form one segment in array order;
+ *   1. packets are stably grouped by session, so each session's packets
+ *      form one segment in array order: up to 65536 sessions by a counting
+ *      pass (per-session counts, one scan, an unstable scatter, then each
+ *      packet's rank among its session's packets by index -- a session
+ *      with more than SGPU_MP_SEGMAX packets fails the plan with SPF_SEG
+ *      and the host re-plans with the radix sort), else (or in.radix) by a
+ *      hipCUB LSD radix sort of the session index (values = packet index);
  *   2. inside a segment packet k is assumed to see s_l = seq of packet
  *      k-1 (the session's stored s_l for the first), ROC rollovers are
  *      prefix-summed, and every assumption is verified exactly as in the
@@ -96,6 +100,132 @@ __global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, K *kin,
 		v[i] = i;
 		kin[i] = (K)(s < nsess ? s : nsess - 1u);
 	}
+}
+
+/* ---- counting grouping (sessions <= 65536) ---------------------------- */
+
+/* per packet: its (clamped) session's count, the unstable slot in it;
+ * MP_HPER packets per thread, their atomics in flight together */
+#define MP_HPER 4
+__global__ void k_mp_hist(const uint32_t *sess, uint32_t *cnt,
+			  uint32_t *slot, uint32_t n, uint32_t nsess,
+			  struct sgpu_plan_out *out)
+{
+	const uint32_t i0 = blockIdx.x * (MP_BLOCK * MP_HPER) + threadIdx.x;
+	uint32_t s[MP_HPER], r[MP_HPER];
+	bool bad = false;
+#pragma unroll
+	for (int j = 0; j < MP_HPER; j++) {
+		const uint32_t i = i0 + j * MP_BLOCK;
+		s[j] = i < n ? sess[i] : 0u;
+		if (s[j] >= nsess) {
+			bad = true;
+			s[j] = nsess - 1u;
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < MP_HPER; j++)
+		r[j] = i0 + j * MP_BLOCK < n ? atomicAdd(&cnt[s[j]], 1u) : 0u;
+#pragma unroll
+	for (int j = 0; j < MP_HPER; j++)
+		if (i0 + j * MP_BLOCK < n)
+			slot[i0 + j * MP_BLOCK] = r[j];
+	if (bad)
+		atomicOr(&out->fail, (uint32_t)SPF_BAD);
+}
+
+/* segment bounds from the counts, two launches over 1024-session tiles:
+ * k_mp_tscan leaves each tile's exclusive prefix in segf and its total
+ * in tsum (SPF_SEG above SGPU_MP_SEGMAX); k_mp_toff adds the tiles
+ * before it and turns the counts in segl into last positions ("none" for
+ * an empty segment) */
+__global__ void __launch_bounds__(1024)
+k_mp_tscan(uint32_t *segf, const uint32_t *segl, uint32_t *tsum,
+	   uint32_t nsess, struct sgpu_plan_out *out)
+{
+	__shared__ uint32_t wsum[16];
+	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	const uint32_t c = k < nsess ? segl[k] : 0u;
+	if (c > SGPU_MP_SEGMAX)
+		atomicOr(&out->fail, (uint32_t)SPF_SEG);
+	uint32_t v = c;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t u = (uint32_t)__shfl_up((int)v, d);
+		if (lane >= (uint32_t)d)
+			v += u;
+	}
+	if (lane == 63)
+		wsum[wv] = v;
+	__syncthreads();
+	uint32_t pre = 0;
+	for (uint32_t q = 0; q < wv; q++)
+		pre += wsum[q];
+	if (k < nsess)
+		segf[k] = pre + v - c;
+	if (threadIdx.x == 1023)
+		tsum[blockIdx.x] = pre + v;
+}
+
+__global__ void __launch_bounds__(1024)
+k_mp_toff(uint32_t *segf, uint32_t *segl, const uint32_t *tsum,
+	  uint32_t nsess)
+{
+	__shared__ uint32_t base;
+	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+	if (threadIdx.x < 64) {
+		uint32_t v = threadIdx.x < blockIdx.x ? tsum[threadIdx.x] : 0u;
+		for (int d = 32; d > 0; d >>= 1)
+			v += (uint32_t)__shfl_xor((int)v, d);
+		if (threadIdx.x == 0)
+			base = v;
+	}
+	__syncthreads();
+	if (k >= nsess)
+		return;
+	const uint32_t c = segl[k], f = segf[k] + base;
+	segf[k] = f;
+	segl[k] = c ? f + c - 1u : 0xffffffffu;
+}
+
+__global__ void k_mp_cscatter(const uint32_t *sess, const uint32_t *slot,
+			      const uint32_t *segf, uint32_t *tmp, uint32_t n,
+			      uint32_t nsess)
+{
+	const uint32_t i = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint32_t s = sess[i] < nsess ? sess[i] : nsess - 1u;
+	tmp[segf[s] + slot[i]] = i;
+}
+
+/* stable order: the packet at unstable position q goes to its segment
+ * start + the number of its session's packets with a smaller index (a
+ * segment is read by the lanes that hold it: broadcast loads) */
+__global__ void k_mp_crank(const uint32_t *sess, const uint32_t *tmp,
+			   const uint32_t *segf, const uint32_t *segl,
+			   uint32_t *key, uint32_t *val, uint32_t n,
+			   uint32_t nsess)
+{
+	const uint32_t q = blockIdx.x * MP_BLOCK + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t i = tmp[q];
+	const uint32_t s = sess[i] < nsess ? sess[i] : nsess - 1u;
+	const uint32_t f = segf[s], l = segl[s];
+	if (l - f >= SGPU_MP_SEGMAX) {
+		/* SPF_SEG: the plan is not used, but the planner passes
+		 * still read a permutation */
+		key[q] = s;
+		val[q] = i;
+		return;
+	}
+	uint32_t r = 0;
+	for (uint32_t k = f; k <= l; k++)
+		r += tmp[k] < i ? 1u : 0u;
+	key[f + r] = s;
+	val[f + r] = i;
 }
 
 /* sorted 16-bit keys -> the 32-bit key array the planner passes read */
@@ -716,11 +846,33 @@ static size_t mp_cub_bytes(uint32_t n, uint32_t bits)
 	return tb > t16 ? tb : t16;
 }
 
+/* the counting grouping's counters: segl (see sgpu_mplan_rtp_phase),
+ * followed by the launch-order bins: sgpu_mplan_counter_words(nsess)
+ * words to zero */
+extern "C" uint32_t sgpu_mplan_counter_words(uint32_t nsess)
+{
+	return (uint32_t)(mp_align((size_t)nsess * 4) / 4) + 2 * MP_OBINS;
+}
+
+extern "C" uint32_t *sgpu_mplan_counters(void *scratch, uint32_t n,
+					 uint32_t nsess)
+{
+	const uint32_t nb = (n + MP_BLOCK - 1) / MP_BLOCK;
+	return (uint32_t *)((uint8_t *)scratch + 6 * mp_align((size_t)n * 4) +
+			    mp_align((size_t)nb * 4 + 64) +
+			    mp_align((size_t)nsess * 4));
+}
+
 extern "C" size_t sgpu_mplan_scratch(uint32_t n, uint32_t nsess)
 {
 	const uint32_t nb = (n + MP_BLOCK - 1) / MP_BLOCK;
+	/* the radix sort's temporary storage doubles as the counting
+	 * grouping's launch-order bins (>= 512 B) */
+	size_t tb = mp_align(mp_cub_bytes(n, 32));
+	if (tb < 512)
+		tb = 512;
 	return 6 * mp_align((size_t)n * 4) + mp_align((size_t)nb * 4 + 64) +
-	       2 * mp_align((size_t)nsess * 4) + mp_align(mp_cub_bytes(n, 32));
+	       2 * mp_align((size_t)nsess * 4) + tb;
 }
 
 extern "C" int sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
@@ -775,9 +927,36 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 	if (!in->out_zeroed &&
 	    hipMemsetAsync(out, 0, sizeof(*out), st) != hipSuccess)
 		return EIO;
+	if (in->nsess <= 65536 && !in->radix) {
+		/* counting grouping: the counts in segl (zeroed by the parse
+		 * prologue or here), unstable slots in vin, the unstable
+		 * order in pex (free until k_mp_mark) */
+		if (!in->cnt_zeroed &&
+		    hipMemsetAsync(segl, 0, (size_t)in->nsess * 4, st) !=
+		    hipSuccess)
+			return EIO;
+		const uint32_t nt = (in->nsess + 1023u) / 1024u;  /* <= 64 */
+		hipLaunchKernelGGL(k_mp_hist,
+				   dim3((n + MP_BLOCK * MP_HPER - 1) /
+					(MP_BLOCK * MP_HPER)),
+				   dim3(MP_BLOCK), 0, st, sess, segl, vin, n,
+				   in->nsess, out);
+		/* the tile totals in bcnt (free until k_mp_count) */
+		hipLaunchKernelGGL(k_mp_tscan, dim3(nt), dim3(1024), 0, st, segf,
+				   (const uint32_t *)segl, bcnt, in->nsess, out);
+		hipLaunchKernelGGL(k_mp_toff, dim3(nt), dim3(1024), 0, st, segf,
+				   segl, (const uint32_t *)bcnt, in->nsess);
+		hipLaunchKernelGGL(k_mp_cscatter, dim3(nb), dim3(MP_BLOCK), 0,
+				   st, sess, (const uint32_t *)vin,
+				   (const uint32_t *)segf, pex, n, in->nsess);
+		hipLaunchKernelGGL(k_mp_crank, dim3(nb), dim3(MP_BLOCK), 0, st,
+				   sess, (const uint32_t *)pex,
+				   (const uint32_t *)segf, (const uint32_t *)segl,
+				   kout, vout, n, in->nsess);
+	}
 	/* pex is free until k_mp_mark (the clamped keys), sseq until
 	 * k_mp_count (sorted 16-bit keys) */
-	if (in->nsess <= 65536 && in->key_bits <= 16) {
+	else if (in->nsess <= 65536 && in->key_bits <= 16) {
 		uint16_t *k16 = (uint16_t *)pex, *o16 = (uint16_t *)sseq;
 		hipLaunchKernelGGL(k_mp_iota<uint16_t>, dim3(nb), dim3(MP_BLOCK),
 				   0, st, vin, sess, k16, n, in->nsess, out, segl);
@@ -817,17 +996,24 @@ extern "C" int sgpu_mplan_rtp_phase(int phase, const struct sgpu_mplan_in *in,
 			   (const uint32_t *)segf, (const uint32_t *)segl,
 			   st_out, out);
 	if (order) {
-		/* crypto launch order; pex and kout are free once k_mp_final
-		 * has run (each >= 256 B: bin counts and cursors) */
+		/* crypto launch order: bin counts and cursors right behind the
+		 * counters, zeroed with them by the parse prologue (counting
+		 * grouping: sgpu_mplan_counters, 64 + 64 words), else in pex
+		 * and kout (free once k_mp_final has run, each >= 256 B) */
 		const uint32_t ob = (n + MP_OBLOCK * MP_OPER - 1) /
 				    (MP_OBLOCK * MP_OPER);
-		if (hipMemsetAsync(pex, 0, MP_OBINS * 4, st) != hipSuccess ||
-		    hipMemsetAsync(kout, 0, MP_OBINS * 4, st) != hipSuccess)
+		uint32_t *ghist = pex, *gcur = kout;
+		if (!in->radix && in->cnt_zeroed && in->nsess <= 65536) {
+			ghist = (uint32_t *)p;
+			gcur = ghist + MP_OBINS;
+		}
+		else if (hipMemsetAsync(pex, 0, MP_OBINS * 4, st) != hipSuccess ||
+			 hipMemsetAsync(kout, 0, MP_OBINS * 4, st) != hipSuccess)
 			return EIO;
 		hipLaunchKernelGGL(k_mp_ocount, dim3(ob), dim3(MP_OBLOCK), 0,
-				   st, pos, end, pex, n);
+				   st, pos, end, ghist, n);
 		hipLaunchKernelGGL(k_mp_oscatter, dim3(ob), dim3(MP_OBLOCK), 0,
-				   st, pos, end, (const uint32_t *)pex, kout,
+				   st, pos, end, (const uint32_t *)ghist, gcur,
 				   order, n);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : EIO;

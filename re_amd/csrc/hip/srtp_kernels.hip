@@ -352,6 +352,8 @@ __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 		if (pro.cm_out && threadIdx.x == 0)
 			*pro.cm_out = pro.cm;
 	}
+	for (uint32_t k = i; k < pro.nz2; k += gridDim.x * blockDim.x)
+		pro.z2[k] = 0;
 	if (pro.wchk) {
 		k_parse_rtp_checked(arena, asz, pos, end, out, n, pro);
 		return;

@@ -144,6 +144,8 @@ static struct {
 				   the general per-lane-key kernel */
 	int splan;              /* srtp_gpu_tune splan: single-session RTP
 				   batches through the per-stream planner */
+	int mpradix;            /* srtp_gpu_tune mpradix: multi-session plans
+				   group by the radix sort (not counting) */
 	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
 				   device-planned batch fold on the host */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
@@ -239,6 +241,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.splan = value > 0;
 	else if (!strcmp(name, "nomk"))
 		g_env.nomk = value > 0;
+	else if (!strcmp(name, "mpradix"))
+		g_env.mpradix = value > 0;
 	else if (!strcmp(name, "nocombine"))
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "trace"))
@@ -3254,6 +3258,7 @@ struct dcall {
 	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
 	struct sgpu_splan_in sin; /* several streams: the plan input */
 	int devfold;            /* many sessions: fold queued on the device */
+	int radix;              /* ... grouped by the radix sort */
 };
 
 /* single-stream RTP batch planned and processed on the device: the
@@ -3313,7 +3318,7 @@ static int dev_planned_issue(struct dcall *k)
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
 			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm, NULL, NULL,
-			0, 0, 0, 0};
+			0, 0, 0, 0, NULL, 0};
 		k->in.zeroed = 1;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
@@ -3567,7 +3572,7 @@ static int dev_splanned_issue(struct dcall *k)
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
 			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d,
-			c0->dev, NULL, NULL, 0, 0, 0, 0};
+			c0->dev, NULL, NULL, 0, 0, 0, 0, NULL, 0};
 		k->sin.zeroed = 1;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
@@ -3739,7 +3744,7 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		struct sgpu_prologue pro = {
 			es_d, nfail_d, (uint32_t *)po_d, 1,
 			(uint32_t)(sizeof(*po) / 4), (uint32_t *)w->cm.d, cm, NULL, NULL,
-			0, 0, 0, 0};
+			0, 0, 0, 0, NULL, 0};
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, prot ? NULL : eix_d,
 					  (uint32_t)n, 1, &pro, stream);
@@ -3913,14 +3918,25 @@ static int dev_mplanned_issue(struct dcall *k)
 	memset(&in, 0, sizeof(in));
 	in.wchk = (const uint32_t *)(w->mscr.d + scr + n * 4);
 	{
-		/* zeroes the plan out too (k_mp_iota ORs into it) */
+		/* zeroes the plan out too (k_mp_iota ORs into it) and the
+		 * counting grouping's per-session counters */
+		const int radix = k->radix || g_env.mpradix || nsess > 65536;
 		struct sgpu_prologue pro = {es_d, nfail_d, (uint32_t *)po_d, 1,
 					    (uint32_t)(sizeof(*po) / 4), NULL, 0,
 					    (uint32_t *)in.wchk, d->cap,
 					    (uint32_t)prot, T,
 					    prot ? (gcm ? 16u : (T > 4 ? T : 4u))
 						 : 0u,
-					    SGPU_CACHED_MAX(c0->mode)};
+					    SGPU_CACHED_MAX(c0->mode),
+					    radix ? NULL :
+					    sgpu_mplan_counters(w->mscr.d,
+								(uint32_t)n,
+								(uint32_t)nsess),
+					    radix ? 0u :
+					    sgpu_mplan_counter_words(
+						    (uint32_t)nsess)};
+		in.radix = (uint32_t)radix;
+		in.cnt_zeroed = !radix;
 		err = sgpu_parse_prologue(d->arena, d->arena_size, d->pos,
 					  d->end, hd_d, NULL, (uint32_t)n, 0,
 					  &pro, stream);
@@ -4035,6 +4051,7 @@ static int dev_mplanned_finish(struct dcall *k)
 	uint32_t nfail = po->nfail;
 	int err;
 
+	k->pfail = po->fail;
 	if (g_env.times)
 		fprintf(stderr, "re_srtp mplan n=%zu nsess=%zu up=%u: gather "
 			"%.3f submit %.3f wait %.3f ms\n", n, k->nsess, k->nup,
@@ -4085,8 +4102,8 @@ static int dev_mplanned_finish(struct dcall *k)
 }
 
 /* synchronous: -1 not plannable (nothing modified), else 0 / errno */
-static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
-			struct srtp_batch_dev *d)
+static int dev_mplanned_(int op, struct srtp **sessv, size_t nsess,
+			 struct srtp_batch_dev *d, int radix, uint32_t *pfail)
 {
 	struct dcall k;
 	int err;
@@ -4095,6 +4112,7 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 	k.sessv = sessv;
 	k.nsess = nsess;
 	k.d = *d;
+	k.radix = radix;
 	k.w = ws_get();
 	if (!k.w)
 		return ENOMEM;
@@ -4103,7 +4121,21 @@ static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
 		err = sgpu_stream_sync(d->stream);
 	if (err)
 		return err;
-	return dev_mplanned_finish(&k);
+	err = dev_mplanned_finish(&k);
+	*pfail = k.pfail;
+	return err;
+}
+
+/* a session with more than SGPU_MP_SEGMAX packets (SPF_SEG): re-planned
+ * with the radix-sort grouping */
+static int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
+			struct srtp_batch_dev *d)
+{
+	uint32_t pf = 0;
+	int r = dev_mplanned_(op, sessv, nsess, d, g_env.mpradix, &pf);
+	if (r == -1 && (pf & SPF_SEG) && !g_env.mpradix)
+		r = dev_mplanned_(op, sessv, nsess, d, 1, &pf);
+	return r;
 }
 
 /* ---- asynchronous device batches (re_srtp_batch.h) -------------------- */
@@ -4169,6 +4201,14 @@ static void tk_finish_one(void)
 		/* a second SSRC in a single-stream plan: the per-stream one */
 		if (!r && t->kind == TK_PLANNED && (k->pfail & SPF_SSRC))
 			r = dev_splanned(k->op, k->sessv[0], &k->d);
+		/* a session over the counting grouping's bound: the radix
+		 * sort */
+		else if (!r && t->kind == TK_MPLANNED && (k->pfail & SPF_SEG) &&
+			 !k->radix) {
+			uint32_t pf = 0;
+			r = dev_mplanned_(k->op, k->sessv, k->nsess, &k->d, 1,
+					  &pf);
+		}
 		else if (!r)
 			r = -1;
 		if (r == -1)

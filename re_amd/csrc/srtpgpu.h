@@ -230,7 +230,11 @@ enum {
 	SPF_BAD     = 1u << 8,  /* invalid window (pos/end/cap/arena) */
 	SPF_PRED    = 1u << 9,  /* the chained call before did not complete
 				   on the device (async batches) */
+	SPF_SEG     = 1u << 10, /* multi-session counting grouping: a session
+				   with more than SGPU_MP_SEGMAX packets (the
+				   host re-plans with the radix sort) */
 };
+#define SGPU_MP_SEGMAX 1024
 
 /*
  * Chained asynchronous batches: a call queued behind a pending one on the
@@ -347,7 +351,18 @@ struct sgpu_mplan_in {
 				   SIZE, BAD, CAP) were made by the parse
 				   prologue, one word per 256-packet block
 				   (sgpu_prologue.wchk) */
+	uint32_t radix;         /* group by the radix sort (else, for up to
+				   65536 sessions, the counting grouping) */
+	uint32_t cnt_zeroed;    /* counting: its per-session counters
+				   (sgpu_mplan_counters) already zeroed */
 };
+
+/* the counting grouping's per-session counters inside the scratch (the
+ * parse prologue zeroes them: in.cnt_zeroed) */
+uint32_t *sgpu_mplan_counters(void *scratch, uint32_t n, uint32_t nsess);
+/* ... how many words from there the prologue zeroes (counters and the
+ * crypto launch order's bins) */
+uint32_t sgpu_mplan_counter_words(uint32_t nsess);
 
 /* the same in two launch groups: phase 1 sorts the packets by session
  * (needs neither st_in nor the session map), phase 2 plans; the host
@@ -533,6 +548,8 @@ struct sgpu_prologue {
 	uint32_t *wchk;
 	const uint32_t *cap;
 	uint32_t prot, tag, need, maxlen;
+	uint32_t *z2;           /* nz2 words zeroed by the whole grid */
+	uint32_t nz2;
 };
 int   sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
 			  const uint32_t *pos, const uint32_t *end,

@@ -797,3 +797,80 @@ def test_resident_state_across_paths(suite, torch_cuda):
         for u, v in zip(x[0] + x[1], y[0] + y[1]):
             assert (u == v).all()
     assert A[1] == B[1] and A[2] == B[2]
+
+
+def hot_session_traffic(rng, n, nsess, hot, s0=65000):
+    """multi-session traffic where session 0 carries `hot` of the n
+    packets (in order per session, interleaved at random)"""
+    owner = np.concatenate([np.zeros(hot, dtype=np.int64),
+                            rng.integers(1, nsess, n - hot)])
+    rng.shuffle(owner)
+    nxt, out = {}, []
+    for s in owner.tolist():
+        seq = nxt.get(s, s0)
+        nxt[s] = (seq + 1) & 0xffff
+        out.append((s, rtp_packet(rng, seq, 0x7000 + s,
+                                  plen=int(rng.integers(0, 300)))))
+    return out
+
+
+@pytest.mark.parametrize("suite", [1, 5])
+def test_multi_session_counting_grouping(suite, torch_cuda):
+    """the multi-session planner groups packets by session with a counting
+    pass (stable rank among a session's packets); a session with more than
+    SGPU_MP_SEGMAX (1024) packets rejects that grouping (SPF_SEG) and the
+    call is re-planned with the radix sort.  Both must equal the radix-sort
+    grouping (srtp_gpu_tune mpradix) and the general engine, protect and
+    unprotect, with a forged packet in the hot session"""
+    torch = torch_cuda
+    rng = np.random.default_rng(404 + suite)
+    nsess = 12
+    keys = keys_for(suite, nsess)
+    ssrcs = [0x7000 + s for s in range(nsess)]
+    batches = [hot_session_traffic(rng, 3000, nsess, 1500),   # SPF_SEG
+               hot_session_traffic(rng, 3000, nsess, 900, s0=2000)]
+    res = {}
+    for mode in ("count", "radix", "general"):
+        if mode == "radix":
+            P.lib().srtp_gpu_tune(b"mpradix", 1)
+        tx = [P.Srtp(suite, k) for k in keys]
+        rx = [P.Srtp(suite, k) for k in keys]
+        outs, rej = [], []
+        for bi, pk in enumerate(batches):
+            r0 = P.counter("rejects")
+            arena, pos, end, cap, sess = to_arena(pk)
+            if mode == "general":
+                enc = run(torch, "srtp_encrypt", tx, arena, pos, end, cap,
+                          sess, True)
+            else:
+                enc = run_dev(torch, "srtp_encrypt", tx, arena, pos, end,
+                              cap, sess)
+            prot = [(s, enc[0][pos[i]:enc[2][i]].tobytes())
+                    for i, (s, _) in enumerate(pk)]
+            hot = next(i for i, (s, _) in enumerate(pk) if s == 0 and i > 700)
+            q = bytearray(prot[hot][1])
+            q[-1] ^= 0x04
+            prot[hot] = (prot[hot][0], bytes(q))
+            a2, p2, e2, c2, s2 = to_arena(prot)
+            if mode == "general":
+                dec = run(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2,
+                          True)
+            else:
+                dec = run_dev(torch, "srtp_decrypt", rx, a2, p2, e2, c2, s2)
+            assert int(dec[3][hot]) == P.EAUTH
+            outs.append((enc, dec))
+            rej.append(P.counter("rejects") - r0)
+        P.lib().srtp_gpu_tune(b"mpradix", 0)
+        res[mode] = (outs, states(tx, ssrcs), states(rx, ssrcs), rej)
+        for c in tx + rx:
+            c.close()
+    # the hot batch re-planned (one reject per direction), the other not
+    assert res["count"][3][0] == 2 and res["count"][3][1] == 0
+    assert res["radix"][3] == [0, 0]
+    A = res["count"]
+    for mode in ("radix", "general"):
+        B = res[mode]
+        for (ea, da), (eb, db) in zip(A[0], B[0]):
+            for x, y in zip(ea + da, eb + db):
+                assert (x == y).all(), mode
+        assert A[1] == B[1] and A[2] == B[2], mode

@@ -26,6 +26,12 @@ kfn_t sgpu_pick_ctr14_fast(int prot, int refix)
 	return prot ? k_ctr_fast_any<14, true> : k_ctr_fast_any<14, false>;
 }
 
+/* ... their single-key SRTCP form */
+kfn_t sgpu_pick_ctr14_fast_rtcp(int prot)
+{
+	return prot ? k_ctr_fast_rtcp<14, true> : k_ctr_fast_rtcp<14, false>;
+}
+
 /* ... and their multi-session (per-lane key) form */
 kfn_t sgpu_pick_ctr14_fast_mk(int prot)
 {

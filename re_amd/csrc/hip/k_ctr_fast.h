@@ -91,6 +91,7 @@ struct FastPkt {
 	uint32_t p, off, L, hl, ssrc, ixhi, ixlo, roc;
 };
 
+template <bool RTCP = false>
 __device__ __forceinline__ bool fast_pkt(const struct sgpu_compact &c,
 					 uint32_t t, FastPkt &f)
 {
@@ -106,6 +107,15 @@ __device__ __forceinline__ bool fast_pkt(const struct sgpu_compact &c,
 	const uint32_t *hw = (const uint32_t *)(c.hdr + f.p);
 	f.ssrc = hw[0];
 	f.hl = hw[2];
+	if (RTCP) {
+		/* SRTCP (sgpu_rdesc): E || index is both the IV's index
+		 * (srtcp.c srtp_iv_calc) and the MAC trailer word */
+		const uint32_t w = (uint32_t)d;
+		f.ixhi = (w & 0x7fffffffu) >> 16;
+		f.ixlo = w & 0xffffu;
+		f.roc = w;
+		return true;
+	}
 	f.ixhi = (uint32_t)(d >> 16);
 	f.ixlo = (uint32_t)(d & 0xffffu);
 	f.roc = f.ixhi + ((fl & SD_ROC_P1) ? 1u : 0u) -
@@ -196,13 +206,20 @@ __device__ __forceinline__ void tail_xor_store(const uint8_t *smem,
 	}
 }
 
-template <int NR, int SHIFT, bool PROT, bool MK = false>
+/*
+ * RTCP: single-key SRTCP batches planned by k_plan_rtcp (srtcp_encrypt
+ * srtcp.c:31-140, srtcp_decrypt srtcp.c:143-287): header class 2 (hl =
+ * 8), the MAC trailer word is E || index (protect: stored at L in front
+ * of the tag; unprotect: the 4 bytes in front of the tag, so A = L - T -
+ * 4), no ROC written over the tag, E = 0: no cipher region.
+ */
+template <int NR, int SHIFT, bool PROT, bool MK = false, bool RTCP = false>
 __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 {
 	tt4_fill(smem, a.t0);
 	__syncthreads();
 	FastPkt f;
-	if (!fast_pkt(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
+	if (!fast_pkt<RTCP>(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
 		return;
 	uint32_t rk[4 * (NR + 1)];
 	/* MK: every lane its own session context (keys in VGPRs); all of
@@ -215,8 +232,10 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 	uint8_t *const pkt = arena + f.off;
 	const uint64_t pasz = a.asz - f.off;
 	const uint32_t T = PROT ? 0u : __builtin_amdgcn_readfirstlane(cp->tag_len);
-	const uint32_t A = f.L - T;             /* MAC data / cipher end */
-	const uint32_t hl = f.hl;
+	/* MAC data / cipher end */
+	const uint32_t A = f.L - T - (RTCP && !PROT ? 4u : 0u);
+	/* unencrypted SRTCP (E = 0): an empty cipher region */
+	const uint32_t hl = RTCP && !(f.roc >> 31) ? A : f.hl;
 
 	uint32_t iv[4];
 	fast_iv(cp, f, iv);
@@ -390,8 +409,25 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 	const uint32_t tag_len = __builtin_amdgcn_readfirstlane(cp->tag_len);
 	uint8_t *tp = pkt + A;
 	if (PROT) {
+		if (RTCP) {
+			st_be32(tp, f.roc);     /* E || index (srtcp.c:115) */
+			tp += 4;
+		}
 		for (uint32_t q = 0; q < tag_len; q++)
 			tp[q] = (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
+		return;
+	}
+	if (RTCP) {
+		/* tp = the tag: no ROC written over it */
+		tp += 4;
+		uint32_t diff = 0;
+		for (uint32_t q = 0; q < tag_len; q++)
+			diff |= tp[q] ^ (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
+		const uint8_t vd = (diff == 0 ? SV_TAG_OK : 0) | SV_CIPHERED;
+		if (!(vd & SV_TAG_OK))
+			atomicAdd(a.c.nfail, 1u);
+		if (a.verdict)
+			a.verdict[f.p] = vd;
 		return;
 	}
 	uint32_t diff = 0;
@@ -609,6 +645,20 @@ k_ctr_fast_mk(const KArgs a)
 	case 3: ctr_fast_body<NR, 3, PROT, true>(a, smem); break;
 	default: break;                 /* rejected plan */
 	}
+}
+
+/* single-key SRTCP batches (header class 2); a.c.guard: the plan's skip
+ * word of class 2 */
+template <int NR, bool PROT>
+__global__ void
+__attribute__((amdgpu_flat_work_group_size(1, CTRF_BLK(PROT))))
+__attribute__((amdgpu_waves_per_eu(CTRF_BLK(PROT) / 256, 8)))
+k_ctr_fast_rtcp(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	if (*a.c.guard)
+		return;                 /* rejected plan */
+	ctr_fast_body<NR, 2, PROT, false, true>(a, smem);
 }
 
 template <int NR>

@@ -731,5 +731,7 @@ kfn_t sgpu_pick_ctr14_fast(int prot, int refix);
 unsigned sgpu_ctr_fast_block(int prot);
 kfn_t sgpu_pick_ctr10_fast_mk(int prot);
 kfn_t sgpu_pick_ctr14_fast_mk(int prot);
+kfn_t sgpu_pick_ctr10_fast_rtcp(int prot);
+kfn_t sgpu_pick_ctr14_fast_rtcp(int prot);
 unsigned sgpu_ctr_fast_mk_block(void);
 unsigned sgpu_gcm_block(bool uni);

@@ -1214,6 +1214,26 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				   0);
 		return e;
 	}
+	if (mode == SGPU_MODE_CTR && shift == 2 && c->rtcp &&
+	    c->uniform == 4 && !c->undo && !c->idx && !c->sess) {
+		/* device-planned single-key SRTCP batch: the lean kernel's
+		 * SRTCP form (a forged packet is undone with the whole batch
+		 * by the caller, as for the general kernel) */
+		KArgs a;
+		memset(&a, 0, sizeof(a));
+		a.arena = arena;
+		a.asz = arena_size;
+		a.comps = (const struct sgpu_comp *)g_table;
+		a.t0 = g_T0_dev;
+		a.verdict = c->verdict;
+		a.save = c->save;
+		a.c = *c;
+		return launch(nr == 10 ? sgpu_pick_ctr10_fast_rtcp(prot)
+				       : sgpu_pick_ctr14_fast_rtcp(prot),
+			      a, c->n, prof_slot(mode, nr, 2, prot),
+			      (hipStream_t)stream, sgpu_ctr_fast_block(prot),
+			      "k_ctr_fast_rtcp", nr, prot);
+	}
 	if (mode == SGPU_MODE_CTR && shift < 0 && c->uniform == 3 &&
 	    !c->undo && c->sess) {
 		/* multi-session device plan: the lean kernel with per-lane

@@ -3753,10 +3753,12 @@ static int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_plan_rtcp(&in, hd_d, eix_d, d->pos, es_d, d->cap,
 				     d->arena_size, desc_d, po_d, stream);
 	if (!err) {
+		/* CTR: the lean kernel's SRTCP form (srtp_gpu_tune nolean:
+		 * the general compact kernel) */
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1,
+			save_d, nfail_d, 0, gcm || g_env.nolean ? 1 : 4,
 			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, prot, stream);

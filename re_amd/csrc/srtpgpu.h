@@ -157,7 +157,8 @@ struct sgpu_compact {
 	int uniform;                    /* every packet: one session context;
 					   2: and the device planner's shape
 					   (SD_RUN | SD_CIPHER, [hl, A) --
-					   the lean CTR kernels) */
+					   the lean CTR kernels); 4: the same
+					   for SRTCP (k_plan_rtcp, rtcp = 1) */
 	const uint32_t *guard;          /* device word; nonzero: do nothing
 					   (a rejected device plan) or NULL */
 	int rtcp;                       /* SRTCP packets: descriptor = SRTCP

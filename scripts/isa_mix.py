@@ -24,7 +24,8 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TUS = {"ctr10a.hip": ["k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_hmac_any"],
+TUS = {"ctr10a.hip": ["k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_fast_rtcp",
+                      "k_ctr_hmac_any"],
        "ctr14a.hip": ["k_ctr_fast_any"],
        "gcm.hip": ["k_gcmu", "k_gcm"]}
 

@@ -32,7 +32,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIMDS = 1024
-CRYPTO = ("k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_hmac", "k_gcm")
+CRYPTO = ("k_ctr_fast_any", "k_ctr_fast_mk", "k_ctr_fast_rtcp", "k_ctr_hmac",
+          "k_gcm")
 FAST_FORMS = ("xor_vv", "xor_kv", "and_kv", "add_kv", "mov_v", "not_v",
               "lshr_vv", "ashr_8", "lshl_b16", "lshr_b16", "add_vv_e64",
               "xor_vv_e64", "bitop3_vvv96", "bitop3_vvvec")

@@ -287,7 +287,9 @@ class SrtpUdp:
 
     def __init__(self, fd, rx=None, tx=None, batch=256, slot=1536,
                  handler=None, pipeline=False):
-        self._cb = UDP_RECV_H(self._recv)
+        # no Python handler: no per-datagram callback at all (the helper
+        # still counts received / authentic datagrams, srtp_udp_stats)
+        self._cb = UDP_RECV_H(self._recv) if handler else UDP_RECV_H()
         self.handler = handler
         self.ptr = ctypes.c_void_p()
         self.err = lib().srtp_udp_alloc(

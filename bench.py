@@ -905,9 +905,15 @@ def percall_bench(args):
     job's cores for the same packet size"""
     exe = os.path.join(ROOT, "re_amd", "lib", "percall")
     threads = sorted({4, 16, 64})
+    # --tune knobs reach the driver's library through its environment
+    env = dict(os.environ)
+    for kv in args.tune:
+        k, v = kv.split("=")
+        if int(v):
+            env["RE_SRTP_" + k.upper()] = v
     out = subprocess.run([exe, str(args.percall_calls)] +
                          [str(t) for t in threads], capture_output=True,
-                         text=True, timeout=900, check=True).stdout
+                         text=True, timeout=900, check=True, env=env).stdout
     r = json.loads(out.strip().splitlines()[-1])
     line = {"metric": "per-call srtp_encrypt + srtp_decrypt of one 1200-B "
                       "RTP packet (unchanged re_srtp.h API)",

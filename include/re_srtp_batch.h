@@ -156,11 +156,14 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 /**
  * Diagnostics / tuning knobs (defaults from the environment, read once:
  * RE_SRTP_NOPLAN, RE_SRTP_GENERAL, RE_SRTP_PERCLASS, RE_SRTP_NOLEAN,
- * RE_SRTP_NODEVFOLD, RE_SRTP_TRACE,
+ * RE_SRTP_NODEVFOLD, RE_SRTP_NOCOOP, RE_SRTP_TRACE,
  * RE_SRTP_TIMES, RE_SRTP_CHUNK, RE_SRTP_PAR_MIN).  name is one of
  * "noplan" (no device planners), "general" (general engine only),
  * "perclass" (one CTR launch per header class), "nolean" (the general
- * CTR kernels for device-planned batches), "nodevfold" (forged packets
+ * CTR kernels for device-planned batches), "nocoop" (small host-planned
+ * CTR launches keep the cipher in the one-packet-per-lane kernel),
+ * "mpradix" (multi-session plans group packets by the radix sort),
+ * "nodevfold" (forged packets
  * of a device-planned batch fold on the host), "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores

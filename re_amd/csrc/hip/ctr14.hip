@@ -3,6 +3,12 @@
  */
 #include "k_ctr.h"
 
+/* small general launches: the cipher regions one packet per workgroup */
+kfn_t sgpu_pick_ctr14_coop(int prot)
+{
+	return prot ? k_ctr_coop<14, true> : k_ctr_coop<14, false>;
+}
+
 kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot)
 {
 	if (shift < 0)

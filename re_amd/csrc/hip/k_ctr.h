@@ -74,7 +74,8 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 {
 	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
 		return;
-	tt4_fill(smem, a.t0);
+	if (COMPACT || !a.nocipher)     /* MAC only: no AES */
+		tt4_fill(smem, a.t0);
 	__syncthreads();
 
 	uint8_t *const arena = a.arena;
@@ -115,7 +116,8 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 			rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
 	}
 
-	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
+	const bool do_cipher = (j.flags & SJ_CIPHER) != 0 &&
+			       (COMPACT || !a.nocipher);
 	const bool do_hmac = (j.flags & SJ_HMAC) != 0;
 	const bool trail = (j.flags & SJ_TRAILER) != 0;
 	const bool cipher_if_ok = !PROT && (j.flags & SJ_CIPHER_IF_OK);
@@ -439,6 +441,81 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 		atomicAdd(a.c.nfail, 1u);
 	if (verdict)
 		verdict[i] = vd;
+}
+
+/*
+ * Small general launches (the per-packet API's one mbuf per call, a few
+ * concurrent callers): one packet per lane leaves a 1200-B packet's 75
+ * AES blocks and 21 SHA-1 compressions as one serial chain (~110 us).
+ * k_ctr_coop takes the cipher regions instead, one packet per workgroup
+ * and one 16-byte keystream block per lane, and k_ctr_hmac runs with
+ * KArgs.nocipher (MAC only): protect encrypts first (the MAC covers the
+ * ciphertext), unprotect runs after the MAC and applies the keystream
+ * where the general kernel would have stored plaintext (store_ct: no MAC,
+ * or decrypt-if-authentic with the tag ok) -- the same bytes and verdicts
+ * (SV_CIPHERED) as the fused kernel.  Byte-exact stores at the region
+ * end: the ROC may already sit right behind it (srtp.c:342-344).
+ */
+template <int NR, bool PROT>
+__global__ void __launch_bounds__(256)
+k_ctr_coop(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
+	const uint32_t i = blockIdx.x;
+	if (i >= a.njobs)
+		return;
+	const struct sgpu_job j = a.jobs[i];
+	if ((j.flags & SJ_SKIP) || !(j.flags & SJ_CIPHER))
+		return;
+	if (!PROT) {
+		const bool do_hmac = (j.flags & SJ_HMAC) != 0;
+		const bool if_ok = (j.flags & SJ_CIPHER_IF_OK) != 0;
+		if (!(if_ok || !do_hmac))
+			return;                 /* no plaintext stored */
+		if (if_ok && !(a.verdict[i] & SV_TAG_OK))
+			return;                 /* forged: ciphertext stays */
+	}
+	tt_fill(smem, a.t0);
+	__syncthreads();
+	const struct sgpu_comp *cp = a.comps +
+				     __builtin_amdgcn_readfirstlane(j.comp);
+	uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+	for (int k = 0; k < 4 * (NR + 1); k++)
+		rk[k] = __builtin_amdgcn_readfirstlane(cp->rk[k]);
+	uint32_t iv[4];
+	{
+		const uint4 ks = *(const uint4 *)cp->k_s;
+		iv[0] = ks.x;
+		iv[1] = ks.y ^ bswap32(j.ssrc);
+		iv[2] = ks.z ^ bswap32(j.ixhi);
+		iv[3] = (ks.w ^ (bswap32(j.ixlo) >> 16)) & 0xffffu;
+	}
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	uint8_t *pkt = a.arena + j.off;
+	const uint32_t c_end = j.c_off + j.c_len;
+	for (uint32_t b = threadIdx.x; j.c_off + 16u * b < c_end;
+	     b += blockDim.x) {
+		uint32_t ks[4];
+		ctr_block<NR, false>(smem, lo, rk, iv, (int32_t)b, ks);
+		const uint32_t p0 = j.c_off + 16u * b;
+#pragma unroll
+		for (int w = 0; w < 4; w++) {
+			const uint32_t bp = p0 + 4u * w;
+			if (bp >= c_end)
+				break;
+			if (c_end - bp >= 4u) {
+				uint32_t *wp = (uint32_t *)(pkt + bp);
+				*wp = *wp ^ ks[w];
+			}
+			else {
+				for (uint32_t k = 0; k < c_end - bp; k++)
+					pkt[bp + k] ^= (uint8_t)(ks[w] >> (8 * k));
+			}
+		}
+	}
+	if (!PROT && threadIdx.x == 0 && a.verdict)
+		a.verdict[i] |= SV_CIPHERED;
 }
 
 template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>

@@ -296,6 +296,8 @@ struct KArgs {
 	uint8_t *verdict;
 	uint32_t *save;
 	struct sgpu_compact c;          /* compact path */
+	int nocipher;                   /* general path: the cipher regions are
+					   done by k_ctr_coop (small launches) */
 };
 
 /*
@@ -721,6 +723,8 @@ typedef void (*kfn_t)(const KArgs);
 /* kernel pickers, one per translation unit */
 unsigned sgpu_ctr_block(bool uni, int prot);
 kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);
+kfn_t sgpu_pick_ctr10_coop(int prot);
+kfn_t sgpu_pick_ctr14_coop(int prot);
 kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr10_any(bool uni, int prot);
 kfn_t sgpu_pick_ctr14_any(bool uni, int prot);

@@ -1137,6 +1137,8 @@ static int prof_slot(int mode, int nr, int shift, int prot)
 	       (mode ? 0 : shift);
 }
 
+static int g_coop = 1;
+
 /*
  * Launch one kernel over jobs[0..njobs).  The caller (host C) groups jobs
  * so that one launch shares (mode, key size, shift class, direction).
@@ -1151,6 +1153,9 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	kfn_t f = mode == SGPU_MODE_GCM ? sgpu_pick_gcm(false, false, nr, prot)
 		  : nr == 10 ? sgpu_pick_ctr10(false, false, shift, prot)
 			     : sgpu_pick_ctr14(false, false, shift, prot);
+	/* small CTR launches: cipher regions by k_ctr_coop (k_ctr.h) */
+	const bool coop = mode == SGPU_MODE_CTR && njobs <= SGPU_COOP_MAX &&
+			  g_coop;
 	if (!f) {
 		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
 			 mode, nr);
@@ -1166,10 +1171,36 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	a.t0 = g_T0_dev;
 	a.verdict = verdict;
 	a.save = save;
-	return launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
-		      (hipStream_t)stream,
-		      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK,
-		      mode == SGPU_MODE_GCM ? "k_gcm" : "k_ctr_hmac", nr, prot);
+	if (!coop)
+		return launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
+			      (hipStream_t)stream,
+			      mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK,
+			      mode == SGPU_MODE_GCM ? "k_gcm" : "k_ctr_hmac", nr,
+			      prot);
+	a.nocipher = 1;
+	kfn_t fc = nr == 10 ? sgpu_pick_ctr10_coop(prot)
+			    : sgpu_pick_ctr14_coop(prot);
+	int e = 0;
+	if (prot) {
+		hipLaunchKernelGGL(fc, dim3(njobs), dim3(256), 0,
+				   (hipStream_t)stream, a);
+		e = herr(hipGetLastError(), "coop launch");
+	}
+	if (!e)
+		e = launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
+			   (hipStream_t)stream, CTR_BLOCK, "k_ctr_hmac", nr, prot);
+	if (!e && !prot) {
+		hipLaunchKernelGGL(fc, dim3(njobs), dim3(256), 0,
+				   (hipStream_t)stream, a);
+		e = herr(hipGetLastError(), "coop launch");
+	}
+	return e;
+}
+
+/* srtp_gpu_tune nocoop (A/B): small general launches fused as usual */
+extern "C" void sgpu_set_coop(int on)
+{
+	g_coop = on;
 }
 
 extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,

@@ -166,6 +166,8 @@ static void env_read(void)
 	g_env.nodevfold = getenv("RE_SRTP_NODEVFOLD") != NULL;
 	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
 	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
+	if (getenv("RE_SRTP_NOCOOP"))
+		sgpu_set_coop(0);
 	e = getenv("RE_SRTP_CHUNK");
 	v = e ? atol(e) : 0;
 	g_env.chunk = v >= 64 ? (size_t)v : (size_t)1 << 18;
@@ -243,6 +245,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nomk = value > 0;
 	else if (!strcmp(name, "mpradix"))
 		g_env.mpradix = value > 0;
+	else if (!strcmp(name, "nocoop"))
+		sgpu_set_coop(value <= 0);
 	else if (!strcmp(name, "nocombine"))
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "trace"))

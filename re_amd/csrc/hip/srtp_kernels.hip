@@ -1155,7 +1155,8 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 			     : sgpu_pick_ctr14(false, false, shift, prot);
 	/* small CTR launches: cipher regions by k_ctr_coop (k_ctr.h) */
 	const bool coop = mode == SGPU_MODE_CTR && njobs <= SGPU_COOP_MAX &&
-			  g_coop;
+			  g_coop && (prot || verdict);   /* unprotect: the MAC's
+							    verdict gates it */
 	if (!f) {
 		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
 			 mode, nr);

@@ -314,6 +314,9 @@ def main():
                          "(re_amd/bench/percall.c), latency percentiles "
                          "and rates, beside the reference on 1 core")
     ap.add_argument("--percall-calls", type=int, default=20000)
+    ap.add_argument("--percall-suite", type=int, default=1,
+                    help="--percall: enum srtp_suite (1 AES_CM_128_HMAC_"
+                         "SHA1_80, 4 AES_128_GCM, 5 AES_256_GCM)")
     ap.add_argument("--dry-run", action="store_true",
                     help="testing only (CPU): rank plumbing, no GPU work")
     args = ap.parse_args()
@@ -907,6 +910,7 @@ def percall_bench(args):
     threads = sorted({4, 16, 64})
     # --tune knobs reach the driver's library through its environment
     env = dict(os.environ)
+    env["PERCALL_SUITE"] = str(args.percall_suite)
     for kv in args.tune:
         k, v = kv.split("=")
         if int(v):
@@ -920,8 +924,7 @@ def percall_bench(args):
             "value": r["pairs_per_s_1thread"], "unit": "pairs/s",
             "higher_is_better": True, "n_gpus": 1, "data": "synthetic",
             "dtype": "u8", "percall": r,
-            "config": {"workload": "per-call, AES_CM_128_HMAC_SHA1_80, "
-                                   "1200 B"}}
+            "config": {"workload": "per-call, %s, 1200 B" % r["suite"]}}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(CONFIGS[2])
     print(json.dumps(line))

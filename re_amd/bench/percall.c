@@ -44,19 +44,34 @@ struct job {
 	double t0, t1;
 };
 
+/* the suite under test: PERCALL_SUITE = enum srtp_suite value (default
+ * AES_CM_128_HMAC_SHA1_80); master key + salt lengths per suite */
+static enum srtp_suite g_suite = SRTP_AES_CM_128_HMAC_SHA1_80;
+
+static size_t key_len(enum srtp_suite s)
+{
+	switch (s) {
+	case SRTP_AES_128_GCM:          return 16 + 12;
+	case SRTP_AES_256_GCM:          return 32 + 12;
+	case SRTP_AES_256_CM_HMAC_SHA1_32:
+	case SRTP_AES_256_CM_HMAC_SHA1_80: return 32 + 14;
+	default:                        return 16 + 14;
+	}
+}
+
 static void *run(void *arg)
 {
 	struct job *j = arg;
-	uint8_t key[30], pkt[1200];
+	uint8_t key[46], pkt[1200];
 	struct srtp *tx = NULL, *rx = NULL;
 	struct mbuf *mb = mbuf_alloc(1400);
 	long i;
 	int k;
 
-	for (k = 0; k < 30; k++)
+	for (k = 0; k < 46; k++)
 		key[k] = (uint8_t)(17 * k + j->id);
-	if (!mb || srtp_alloc(&tx, SRTP_AES_CM_128_HMAC_SHA1_80, key, 30, 0) ||
-	    srtp_alloc(&rx, SRTP_AES_CM_128_HMAC_SHA1_80, key, 30, 0)) {
+	if (!mb || srtp_alloc(&tx, g_suite, key, key_len(g_suite), 0) ||
+	    srtp_alloc(&rx, g_suite, key, key_len(g_suite), 0)) {
 		j->errors = -1;
 		return NULL;
 	}
@@ -107,6 +122,8 @@ static double pct(double *v, long n, double p)
 int main(int argc, char **argv)
 {
 	const long calls = argc > 1 ? atol(argv[1]) : 20000;
+	if (getenv("PERCALL_SUITE"))
+		g_suite = (enum srtp_suite)atoi(getenv("PERCALL_SUITE"));
 	struct job j0;
 	int a;
 
@@ -128,11 +145,12 @@ int main(int argc, char **argv)
 	qsort(j0.lat_e, calls, sizeof(double), cmpd);
 	qsort(j0.lat_d, calls, sizeof(double), cmpd);
 	printf("{\"calls\":%ld,\"pkt_len\":1200,"
-	       "\"suite\":\"AES_CM_128_HMAC_SHA1_80\","
+	       "\"suite\":\"%s\","
 	       "\"encrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
 	       "\"decrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
 	       "\"pairs_per_s_1thread\":%.0f,\"threads\":[",
-	       calls, pct(j0.lat_e, calls, 0.5), pct(j0.lat_e, calls, 0.99),
+	       calls, srtp_suite_name(g_suite),
+	       pct(j0.lat_e, calls, 0.5), pct(j0.lat_e, calls, 0.99),
 	       j0.lat_e[0], pct(j0.lat_d, calls, 0.5),
 	       pct(j0.lat_d, calls, 0.99), j0.lat_d[0],
 	       calls / ((j0.t1 - j0.t0) * 1e-6));

@@ -197,6 +197,10 @@ k_gcm(const KArgs a)
 	const uint32_t aad_total = A + (trail ? 4u : 0u);
 	const uint32_t c_off = j.c_off, c_len = do_cipher ? j.c_len : 0u;
 	const uint32_t c_end = c_off + c_len;
+	/* small general launches: k_gcm_coop applies the keystream (before
+	 * this kernel on protect, after it on unprotect); here GHASH reads
+	 * the ciphertext as it lies */
+	const bool ks_here = COMPACT || !a.nocipher;
 
 	uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
 	/* GHASH over AAD */
@@ -214,6 +218,12 @@ k_gcm(const KArgs a)
 	for (uint32_t b = 0; b < nfull; b++) {
 		const uint32_t p = c_off + 16u * b;
 		uint4 v = ld16(pkt, pasz, p);
+		if (!ks_here) {
+			x0 ^= bswap32(v.x); x1 ^= bswap32(v.y);
+			x2 ^= bswap32(v.z); x3 ^= bswap32(v.w);
+			ghash_mul(x0, x1, x2, x3, tab, stride, laneoff, rem4);
+			continue;
+		}
 		uint32_t ks[4];
 		C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
 		const uint32_t o0 = v.x ^ ks[0], o1 = v.y ^ ks[1];
@@ -227,8 +237,9 @@ k_gcm(const KArgs a)
 		const uint32_t b = nfull, p = c_off + 16u * b;
 		uint4 v = ld16(pkt, pasz, p);
 		uint32_t d[4] = {v.x, v.y, v.z, v.w};
-		uint32_t ks[4], ct[4];
-		C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
+		uint32_t ks[4] = {0, 0, 0, 0}, ct[4];
+		if (ks_here)
+			C.block(smem, lo, rk, (int32_t)(b + 2u), ks);
 		const uint32_t rem = c_end - p;
 #pragma unroll
 		for (int q = 0; q < 4; q++) {
@@ -236,7 +247,9 @@ k_gcm(const KArgs a)
 			uint32_t nbytes = bp < rem ? min(rem - bp, 4u) : 0u;
 			uint32_t m = (uint32_t)((1ull << (8 * nbytes)) - 1ull);
 			const uint32_t o = (d[q] ^ ks[q]) & m;
-			ct[q] = PROT ? o : (d[q] & m);
+			ct[q] = PROT && ks_here ? o : (d[q] & m);
+			if (!ks_here)
+				continue;
 			if (nbytes == 4)
 				*(uint32_t *)(pkt + p + bp) = o;
 			else if (nbytes)
@@ -279,6 +292,76 @@ k_gcm(const KArgs a)
 	}
 	if (verdict)
 		verdict[i] = vd;
+}
+
+/*
+ * Small general launches (k_ctr_coop's GCM form): the keystream of one
+ * packet's cipher region across a workgroup, one 16-byte block (counter
+ * b + 2) per lane; k_gcm runs with KArgs.nocipher and only GHASHes.
+ * Protect: this kernel first (GHASH covers the ciphertext); unprotect:
+ * after k_gcm (which read the received ciphertext), decrypting in place
+ * whatever the tag (aes.c:136-249: the EVP decrypt writes before the
+ * final tag check), like the fused kernel.  Undo jobs stay in k_gcm.
+ */
+template <int NR>
+__global__ void __launch_bounds__(256)
+k_gcm_coop(const KArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES];
+	const uint32_t i = blockIdx.x;
+	if (i >= a.njobs)
+		return;
+	const struct sgpu_job j = a.jobs[i];
+	if ((j.flags & (SJ_SKIP | SJ_UNDO)) || !(j.flags & SJ_CIPHER))
+		return;
+	tt_fill(smem, a.t0);
+	__syncthreads();
+	const struct sgpu_comp *cp = a.comps +
+				     __builtin_amdgcn_readfirstlane(j.comp);
+	uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+	for (int k = 0; k < 4 * (NR + 1); k++)
+		rk[k] = __builtin_amdgcn_readfirstlane(cp->rk[k]);
+	/* srtp_iv_calc_gcm (misc.c:93-105), as k_gcm */
+	uint32_t iv[3];
+	{
+		const uint4 ks = *(const uint4 *)cp->k_s;
+		const uint32_t be0 = (j.ssrc >> 16) & 0xffffu;
+		const uint32_t be1 = ((j.ssrc & 0xffffu) << 16) | (j.ixhi >> 16);
+		const uint32_t be2 = ((j.ixhi & 0xffffu) << 16) | (j.ixlo & 0xffffu);
+		iv[0] = ks.x ^ bswap32(be0);
+		iv[1] = ks.y ^ bswap32(be1);
+		iv[2] = ks.z ^ bswap32(be2);
+	}
+	const uint32_t lo = (threadIdx.x & 31u) * 4u;
+	uint8_t *pkt = a.arena + j.off;
+	const uint32_t c_end = j.c_off + j.c_len;
+	for (uint32_t b = threadIdx.x; j.c_off + 16u * b < c_end;
+	     b += blockDim.x) {
+		uint32_t s0 = iv[0], s1 = iv[1], s2 = iv[2], s3 = bswap32(b + 2u);
+		aes_block<NR>(smem, lo, rk, s0, s1, s2, s3);
+		const uint32_t ks[4] = {s0, s1, s2, s3};
+		const uint32_t p0 = j.c_off + 16u * b;
+#pragma unroll
+		for (int w = 0; w < 4; w++) {
+			const uint32_t bp = p0 + 4u * w;
+			if (bp >= c_end)
+				break;
+			if (c_end - bp >= 4u) {
+				uint32_t *wp = (uint32_t *)(pkt + bp);
+				*wp = *wp ^ ks[w];
+			}
+			else {
+				for (uint32_t k = 0; k < c_end - bp; k++)
+					pkt[bp + k] ^= (uint8_t)(ks[w] >> (8 * k));
+			}
+		}
+	}
+}
+
+kfn_t sgpu_pick_gcm_coop(int nr)
+{
+	return nr == 10 ? k_gcm_coop<10> : k_gcm_coop<14>;
 }
 
 /* ------------------------------------------------------------------ */

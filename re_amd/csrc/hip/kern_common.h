@@ -724,6 +724,7 @@ typedef void (*kfn_t)(const KArgs);
 unsigned sgpu_ctr_block(bool uni, int prot);
 kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr10_coop(int prot);
+kfn_t sgpu_pick_gcm_coop(int nr);
 kfn_t sgpu_pick_ctr14_coop(int prot);
 kfn_t sgpu_pick_ctr14(bool compact, bool uni, int shift, int prot);
 kfn_t sgpu_pick_ctr10_any(bool uni, int prot);

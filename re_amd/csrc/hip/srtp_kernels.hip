@@ -1154,9 +1154,9 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		  : nr == 10 ? sgpu_pick_ctr10(false, false, shift, prot)
 			     : sgpu_pick_ctr14(false, false, shift, prot);
 	/* small CTR launches: cipher regions by k_ctr_coop (k_ctr.h) */
-	const bool coop = mode == SGPU_MODE_CTR && njobs <= SGPU_COOP_MAX &&
-			  g_coop && (prot || verdict);   /* unprotect: the MAC's
-							    verdict gates it */
+	const bool coop = njobs <= SGPU_COOP_MAX && g_coop &&
+			  (mode == SGPU_MODE_GCM || prot || verdict);
+			  /* CTR unprotect: the MAC's verdict gates it */
 	if (!f) {
 		snprintf(g_err, sizeof(g_err), "no kernel for mode %d nr %d",
 			 mode, nr);
@@ -1179,8 +1179,9 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 			      mode == SGPU_MODE_GCM ? "k_gcm" : "k_ctr_hmac", nr,
 			      prot);
 	a.nocipher = 1;
-	kfn_t fc = nr == 10 ? sgpu_pick_ctr10_coop(prot)
-			    : sgpu_pick_ctr14_coop(prot);
+	kfn_t fc = mode == SGPU_MODE_GCM ? sgpu_pick_gcm_coop(nr)
+		   : nr == 10 ? sgpu_pick_ctr10_coop(prot)
+			      : sgpu_pick_ctr14_coop(prot);
 	int e = 0;
 	if (prot) {
 		hipLaunchKernelGGL(fc, dim3(njobs), dim3(256), 0,
@@ -1189,7 +1190,9 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	}
 	if (!e)
 		e = launch(f, a, njobs, prof_slot(mode, nr, shift, prot),
-			   (hipStream_t)stream, CTR_BLOCK, "k_ctr_hmac", nr, prot);
+			   (hipStream_t)stream,
+			   mode == SGPU_MODE_GCM ? KBLOCK : CTR_BLOCK,
+			   mode == SGPU_MODE_GCM ? "k_gcm" : "k_ctr_hmac", nr, prot);
 	if (!e && !prot) {
 		hipLaunchKernelGGL(fc, dim3(njobs), dim3(256), 0,
 				   (hipStream_t)stream, a);

@@ -110,9 +110,9 @@ uint64_t sgpu_table_device_ptr(void);
 /* run one kernel class over jobs[0..njobs) of a device arena.  Every job
  * of a launch shares (mode, nr, shift = (c_off/4)&3, direction); verdict is
  * a device array (or NULL).  `stream` is a hipStream_t or NULL. */
-#define SGPU_COOP_MAX 2048     /* CTR launches of at most this many jobs run
-				   their cipher regions one packet per
-				   workgroup (k_ctr_coop) */
+#define SGPU_COOP_MAX 2048     /* general launches of at most this many jobs
+				   run their cipher regions one packet per
+				   workgroup (k_ctr_coop, k_gcm_coop) */
 void  sgpu_set_coop(int on);
 int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,

@@ -26,11 +26,16 @@ def torch_cuda():
     return torch
 
 
-def test_per_call_golden(golden, torch_cuda):
-    """Every recorded reference call, replayed one srtp_* call at a time."""
+@pytest.mark.parametrize("coop", [1, 0])
+def test_per_call_golden(golden, coop, torch_cuda):
+    """Every recorded reference call, replayed one srtp_* call at a time --
+    with the small-launch split (the cipher regions by k_ctr_coop /
+    k_gcm_coop, the general kernel MAC-only: the default) and with the
+    cipher fused into the one-packet-per-lane kernel (nocoop)."""
     be = ProductBackend()
-    bad = [m for m in (replay_scenario(be, s) for s in golden["scenarios"])
-           if m]
+    with P.tune(nocoop=1 - coop):
+        bad = [m for m in (replay_scenario(be, s)
+                           for s in golden["scenarios"]) if m]
     assert not bad, bad[:5]
 
 

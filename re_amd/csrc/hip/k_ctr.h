@@ -228,6 +228,24 @@ __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 	};
 
 	uint32_t k = 0;
+	if (!COMPACT && !do_cipher && do_hmac) {
+		/* MAC only (KArgs.nocipher: the small-launch split, or a job
+		 * without a cipher region): whole 64-byte chunks of [0, A)
+		 * straight into SHA-1, the rest by the general chunk */
+		const uint32_t kA = A / 64u;
+		for (; k < kA; k++) {
+			uint32_t w[16];
+#pragma unroll
+			for (int g = 0; g < 4; g++) {
+				const uint4 v = ld16(pkt, pasz, 64u * k + 16u * g);
+				w[4 * g] = bswap32(v.x);
+				w[4 * g + 1] = bswap32(v.y);
+				w[4 * g + 2] = bswap32(v.z);
+				w[4 * g + 3] = bswap32(v.w);
+			}
+			sha1_compress(h, w);
+		}
+	}
 	for (; k < kf0; k++)
 		chunk_general(k, false);
 	/*

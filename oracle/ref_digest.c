@@ -199,7 +199,9 @@ int main(int argc, char **argv)
 	n = argc > 2 ? (size_t)atol(argv[2]) : cf.n;
 	klen = keylen[cf.suite] + saltlen[cf.suite];
 	maxlen = cf.length ? cf.length : 1400;
-	slot = (maxlen + (cf.rtcp ? 20 : 16) + 15) & ~(size_t)15;
+	/* workload.slot_size: SRTCP slots 64-B aligned (make_rtcp_arena) */
+	slot = cf.rtcp ? (maxlen + 20 + 63) & ~(size_t)63
+		       : (maxlen + 16 + 15) & ~(size_t)15;
 	nrows = cf.nssrc > 1 ? cf.nssrc : cf.nsess;
 
 	arena = calloc(n, slot);

@@ -34,10 +34,13 @@ XS_MUL = 0x2545F4914F6CDD1D
 CONFIG1_KEY = b"\x22" * 16 + b"\x44" * 14
 
 
-def slot_size(max_len, room=16):
+def slot_size(max_len, room=16, align=16):
     """packet slot: the packet, `room` bytes for what protect appends (the
-    SRTP tag: <= 16 B; SRTCP: E||index + tag, <= 20 B), 16-B aligned"""
-    return (max_len + room + 15) & ~15
+    SRTP tag: <= 16 B; SRTCP: E||index + tag, <= 20 B), `align`-B aligned
+    (SRTCP arenas: 64, so every packet starts on a 64-B line boundary like
+    the RTP configs' 1216-B slots -- the kernels walk packet-aligned 64-B
+    chunks)"""
+    return (max_len + room + align - 1) & ~(align - 1)
 
 
 def xs_state(seed, idx):
@@ -75,7 +78,7 @@ def make_keys(nsess, klen, seed=SEED_KEYS, ids=None):
 
 
 def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
-               payload=True, first=0, room=16, idx=None):
+               payload=True, first=0, room=16, idx=None, align=16):
     """Returns (arena uint8[n*slot], pos, end, cap) numpy arrays.
 
     lengths: int or uint32 array (RTP packet length incl. 12-B header).
@@ -88,7 +91,7 @@ def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
     lengths = np.broadcast_to(np.asarray(lengths, dtype=np.uint32),
                               (npkts,)).copy()
     maxlen = int(lengths.max())
-    slot = slot_size(maxlen, room)
+    slot = slot_size(maxlen, room, align)
     arena = np.zeros((npkts, slot), dtype=np.uint8)
     gidx = np.arange(first, first + npkts, dtype=np.uint64) if idx is None \
         else np.asarray(idx, dtype=np.uint64)
@@ -140,7 +143,7 @@ def make_rtcp_arena(npkts, length, seed=SEED_PAYLOAD, first=0):
     from the same generators as make_arena.  Returns (arena, pos, end, cap).
     """
     arena, pos, end, cap = make_arena(npkts, length, seed=seed, first=first,
-                                      room=20)
+                                      room=20, align=64)
     a = arena.reshape(npkts, -1)
     words = (int(length) // 4 - 1) & 0xffff
     a[:, 0] = 0x80

@@ -199,9 +199,11 @@ int main(int argc, char **argv)
 	n = argc > 2 ? (size_t)atol(argv[2]) : cf.n;
 	klen = keylen[cf.suite] + saltlen[cf.suite];
 	maxlen = cf.length ? cf.length : 1400;
-	/* workload.slot_size: SRTCP slots 64-B aligned (make_rtcp_arena) */
+	/* workload.make_arena / slot_size: SRTCP and mixed-length slots
+	 * 64-B aligned, the rest 16-B aligned */
 	slot = cf.rtcp ? (maxlen + 20 + 63) & ~(size_t)63
-		       : (maxlen + 16 + 15) & ~(size_t)15;
+	       : !cf.length ? (maxlen + 16 + 63) & ~(size_t)63
+			    : (maxlen + 16 + 15) & ~(size_t)15;
 	nrows = cf.nssrc > 1 ? cf.nssrc : cf.nsess;
 
 	arena = calloc(n, slot);

@@ -78,7 +78,7 @@ def make_keys(nsess, klen, seed=SEED_KEYS, ids=None):
 
 
 def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
-               payload=True, first=0, room=16, idx=None, align=16):
+               payload=True, first=0, room=16, idx=None, align=None):
     """Returns (arena uint8[n*slot], pos, end, cap) numpy arrays.
 
     lengths: int or uint32 array (RTP packet length incl. 12-B header).
@@ -88,6 +88,10 @@ def make_arena(npkts, lengths, s0=65000, sess=None, seed=SEED_PAYLOAD,
     idx: or the global index of every packet (a session-hashed shard of a
     longer workload, re_amd/shard.py shard_sessions).
     """
+    # mixed lengths (config 4): 64-B aligned slots, so every packet starts
+    # on a line boundary (oracle/ref_digest.c applies the same rule)
+    if align is None:
+        align = 16 if np.ndim(lengths) == 0 else 64
     lengths = np.broadcast_to(np.asarray(lengths, dtype=np.uint32),
                               (npkts,)).copy()
     maxlen = int(lengths.max())

@@ -149,6 +149,58 @@ int srtp_stream_export(const struct srtp *srtp, uint32_t ssrc,
 		       struct srtp_stream_state *st);
 int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st);
 
+/**
+ * Cross-rank replay fold of ONE SRTP stream whose unprotect was split
+ * across ranks (no reference counterpart: the reference is
+ * single-process).  Each rank unprotects its contiguous shard from an
+ * assumed boundary state (srtp_stream_import), then records per packet
+ * what its own receiver did (srtp_rx_index: 16 B per packet); the ranks
+ * all-gather the records and srtp_rx_fold replays the reference receiver
+ * over the whole stream in arrival order -- stream_get_seq's first-seq
+ * rule (src/srtp/stream.c:87-109), ETIMEDOUT and the ROC bump before
+ * authentication (src/srtp/srtp.c:313-321), the tag verdict, the replay
+ * window after the tag (src/srtp/replay.c:32-62; srtp.c:362-368, 414-421) and
+ * s_l on success only (srtp.c:426-427) -- so a packet replayed across a
+ * shard boundary gets EALREADY exactly as one receiver would give it.
+ */
+enum srtp_rx_stage {
+	SRTP_RX_NOHDR = 0,      /* failed before the stream step: res is final */
+	SRTP_RX_NOIX = 1,       /* the rank gave ETIMEDOUT: no index computed */
+	SRTP_RX_IX = 2,         /* the rank authenticated at index ix */
+};
+
+struct srtp_rx_rec {
+	uint64_t ix;            /* 48-bit index the rank used (SRTP_RX_IX) */
+	int32_t res;            /* the rank's result for the packet */
+	uint16_t seq;
+	uint8_t stage;          /* enum srtp_rx_stage */
+	uint8_t pad;
+};
+
+/**
+ * A rank's records: its packets arena[pos[i], end[i]) in arrival order (all
+ * of SSRC st0->ssrc, else EINVAL), res[i] the results its
+ * srtp_decrypt_batch* call returned, st0 the state the rank imported
+ * before that call.  0 or EINVAL.
+ */
+int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
+		  const uint32_t *pos, const uint32_t *end,
+		  const int32_t *res, size_t n, struct srtp_rx_rec *rec);
+
+/**
+ * Fold the gathered records of the whole stream from *st (the true state
+ * before packet 0): err[i] = the reference receiver's result.  Stops at
+ * the first packet whose true index differs from the one its rank
+ * authenticated at (the rank's boundary state was wrong, so its verdict
+ * is void): *ndone = that packet's position and *st = the exact state
+ * before it -- re-run packets ndone.. from *st (srtp_stream_import).
+ * *ndone == n when every verdict stands; *st is then the final state.
+ * 0 or EINVAL.
+ */
+int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
+		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
+		 size_t *ndone);
+
 /** Batched session setup: n contexts in one GPU launch (key agility). */
 int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 		    const uint8_t *keys, size_t key_bytes, int flags);

@@ -1163,3 +1163,21 @@ int oracle_stream_state(const struct osrtp *s, uint32_t ssrc, uint32_t *roc,
 	}
 	return -1;
 }
+
+/* test hook: set (or create) ssrc's receiver state -- a rank that starts
+ * its shard from an assumed boundary state (tests/test_rxfold_cpu.py) */
+int oracle_stream_set(struct osrtp *s, uint32_t ssrc, uint32_t roc,
+		      uint32_t s_l, uint32_t s_l_set, uint64_t lix,
+		      uint64_t bitmap)
+{
+	struct ostream *st;
+	int err = stream_get(&st, s, ssrc);
+	if (err)
+		return err;
+	st->roc = roc;
+	st->s_l = (uint16_t)s_l;
+	st->s_l_set = (uint8_t)s_l_set;
+	st->replay_rtp.lix = lix;
+	st->replay_rtp.bitmap = bitmap;
+	return 0;
+}

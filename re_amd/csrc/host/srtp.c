@@ -4645,6 +4645,139 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 	return 0;
 }
 
+/* ---- cross-rank replay fold (include/re_srtp_batch.h) ----------------- */
+
+int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
+		  const uint32_t *pos, const uint32_t *end,
+		  const int32_t *res, size_t n, struct srtp_rx_rec *rec)
+{
+	uint32_t roc;
+	uint16_t s_l;
+	uint8_t set;
+	size_t i;
+
+	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)))
+		return EINVAL;
+	roc = st0->roc;
+	s_l = st0->s_l;
+	set = st0->s_l_set;
+	for (i = 0; i < n; i++) {
+		struct srtp_rx_rec *r = &rec[i];
+		struct pinfo pi;
+		int diff;
+
+		memset(r, 0, sizeof(*r));
+		memset(&pi, 0, sizeof(pi));
+		r->res = res[i];
+		pi.start = pos[i];
+		pi.end = end[i];
+		parse_rtp(&pi, arena);
+		if (pi.hdr_len == UINT32_MAX) {
+			r->stage = SRTP_RX_NOHDR;
+			continue;
+		}
+		if (pi.ssrc != st0->ssrc)
+			return EINVAL;
+		r->seq = pi.seq;
+		/* the rank's own receiver, step by step (srtp.c:310-321) */
+		if (!set) {
+			s_l = pi.seq;
+			set = 1;
+		}
+		diff = (int)pi.seq - (int)s_l;
+		if (diff > 32768) {
+			r->stage = SRTP_RX_NOIX;
+			continue;
+		}
+		if (diff <= -32768) {
+			roc++;
+			s_l = 0;
+		}
+		r->stage = SRTP_RX_IX;
+		r->ix = get_index(roc, s_l, pi.seq);
+		if (res[i] == 0 && pi.seq > s_l)
+			s_l = pi.seq;
+	}
+	return 0;
+}
+
+int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
+		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
+		 size_t *ndone)
+{
+	struct replay rp;
+	uint32_t roc;
+	uint16_t s_l;
+	uint8_t set;
+	size_t i;
+
+	/* every suite checks the replay window after its tag (srtp.c:362-368
+	 * HMAC, 414-421 GCM), so suite is only validated */
+	if (!st || !ndone || (n && (!rec || !err)) ||
+	    (unsigned)suite > SRTP_AES_256_GCM)
+		return EINVAL;
+	rp.bitmap = st->replay_rtp_bitmap;
+	rp.lix = st->replay_rtp_lix;
+	roc = st->roc;
+	s_l = st->s_l;
+	set = st->s_l_set;
+	for (i = 0; i < n; i++) {
+		const struct srtp_rx_rec *r = &rec[i];
+		const uint32_t roc0 = roc;
+		const uint16_t s_l0 = s_l;
+		const uint8_t set0 = set;
+		uint64_t ix;
+		int diff;
+
+		if (r->stage == SRTP_RX_NOHDR) {
+			err[i] = r->res;
+			continue;
+		}
+		if (!set) {
+			s_l = r->seq;
+			set = 1;
+		}
+		diff = (int)r->seq - (int)s_l;
+		if (diff > 32768) {
+			err[i] = ETIMEDOUT;
+			continue;
+		}
+		if (r->stage != SRTP_RX_IX)
+			goto void_verdict;
+		if (diff <= -32768) {
+			roc++;
+			s_l = 0;
+		}
+		ix = get_index(roc, s_l, r->seq);
+		if (ix != r->ix)
+			goto void_verdict;
+		if (r->res != 0 && r->res != EALREADY) {
+			err[i] = r->res;        /* tag verdict: ROC bump stays */
+			continue;
+		}
+		if (!replay_check(&rp, ix)) {
+			err[i] = EALREADY;
+			continue;
+		}
+		err[i] = 0;
+		if (r->seq > s_l)
+			s_l = r->seq;
+		continue;
+	void_verdict:
+		roc = roc0;
+		s_l = s_l0;
+		set = set0;
+		break;
+	}
+	st->replay_rtp_bitmap = rp.bitmap;
+	st->replay_rtp_lix = rp.lix;
+	st->roc = roc;
+	st->s_l = s_l;
+	st->s_l_set = set;
+	*ndone = i;
+	return 0;
+}
+
 /* ---- RTCP compound decode (include/re_rtcp_batch.h) ------------------- */
 
 int rtcp_decode_batch_dev(const uint8_t *arena, size_t arena_size,

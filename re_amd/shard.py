@@ -91,3 +91,91 @@ def reduce_results(dist, counters, elapsed):
             counters.copy_(c)
             elapsed.copy_(e)
     return counters, elapsed
+
+
+# ---- cross-rank replay fold --------------------------------
+#
+# When one stream's unprotect is split across ranks and its shape has no
+# closed form (loss, reordering, replays or forged packets across a shard
+# boundary), each rank unprotects its shard from an assumed boundary state,
+# records per packet what its receiver did (16 B: index, result, seq,
+# stage), the ranks all-gather the records, and every rank replays the
+# reference receiver over the whole stream (srtp_rx_fold): one all-gather
+# of 16 B per packet (16 MB per 1M) is the only data collective.
+
+def _rx_rec_dtype():
+    import numpy as np
+    # struct srtp_rx_rec (include/re_srtp_batch.h)
+    return np.dtype([("ix", "<u8"), ("res", "<i4"), ("seq", "<u2"),
+                     ("stage", "u1"), ("pad", "u1")])
+
+
+def rx_records(st0, arena, pos, end, res):
+    """the rank's records (srtp_rx_index): arena a host uint8 array,
+    pos/end uint32 arrays, res the int32 results of the rank's decrypt call,
+    st0 the StreamState it imported before the call."""
+    import ctypes
+    import numpy as np
+    from . import srtp as S
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    pos = np.ascontiguousarray(pos, dtype=np.uint32)
+    end = np.ascontiguousarray(end, dtype=np.uint32)
+    res = np.ascontiguousarray(res, dtype=np.int32)
+    n = len(pos)
+    if len(end) != n or len(res) != n:
+        raise ValueError("rx_records: pos, end and res differ in length")
+    if n and int(end.max()) > arena.size:
+        raise ValueError("rx_records: end beyond the arena")
+    rec = np.zeros(n, dtype=_rx_rec_dtype())
+    e = S.lib().srtp_rx_index(ctypes.byref(st0), arena.ctypes.data,
+                              pos.ctypes.data, end.ctypes.data,
+                              res.ctypes.data, n, rec.ctypes.data)
+    if e:
+        raise OSError(e, "srtp_rx_index")
+    return rec
+
+
+def rx_fold(st, suite, rec):
+    """fold the whole stream's records from StreamState st (the true state
+    before its first packet; updated in place).  Returns (err int32 array
+    of the packets folded, ndone): ndone < len(rec) when packet ndone was
+    authenticated at an index its rank's boundary state got wrong -- re-run
+    packets ndone.. from st."""
+    import ctypes
+    import numpy as np
+    from . import srtp as S
+    rec = np.ascontiguousarray(rec, dtype=_rx_rec_dtype())
+    err = np.zeros(len(rec), dtype=np.int32)
+    nd = ctypes.c_size_t(0)
+    e = S.lib().srtp_rx_fold(ctypes.byref(st), suite, rec.ctypes.data,
+                             len(rec), err.ctypes.data, ctypes.byref(nd))
+    if e:
+        raise OSError(e, "srtp_rx_fold")
+    return err[:nd.value], nd.value
+
+
+def gather_records(dist, rec):
+    """all-gather every rank's records in rank order (shards are
+    contiguous, so rank order is arrival order); ranks may hold different
+    counts.  One all_gather of the counts, one of the padded records."""
+    import numpy as np
+    import torch
+    if dist is None or not dist.is_initialized() or \
+            dist.get_world_size() == 1:
+        return rec
+    world = dist.get_world_size()
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend() == "nccl" else torch.device("cpu")
+    cnt = torch.tensor([len(rec)], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt)
+    cnts = [int(c.item()) for c in cnts]
+    m = max(cnts)
+    raw = np.zeros(m * rec.dtype.itemsize, dtype=np.uint8)
+    raw[:rec.nbytes] = rec.view(np.uint8)
+    t = torch.from_numpy(raw).to(dev)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    parts = [o.cpu().numpy()[:c * rec.dtype.itemsize].view(rec.dtype)
+             for o, c in zip(outs, cnts)]
+    return np.concatenate(parts)

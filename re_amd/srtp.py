@@ -101,6 +101,10 @@ class StreamState(ctypes.Structure):
                 ("rtcp_index", ctypes.c_uint32)]
 
 
+# enum srtp_rx_stage (include/re_srtp_batch.h)
+RX_NOHDR, RX_NOIX, RX_IX = 0, 1, 2
+
+
 EXPORTS = (
     "srtp_alloc", "srtp_encrypt", "srtp_decrypt", "srtcp_encrypt",
     "srtcp_decrypt", "srtp_suite_name",
@@ -110,7 +114,7 @@ EXPORTS = (
     "srtp_decrypt_batch_dev", "srtcp_encrypt_batch_dev",
     "srtcp_decrypt_batch_dev", "srtp_encrypt_batch_dev_async",
     "srtp_decrypt_batch_dev_async", "srtp_batch_wait", "srtp_stream_export",
-    "srtp_stream_import", "srtp_alloc_many", "srtp_gpu_error",
+    "srtp_stream_import", "srtp_rx_index", "srtp_rx_fold", "srtp_alloc_many", "srtp_gpu_error",
     "srtp_gpu_prof", "srtp_gpu_prof_read", "srtp_gpu_prof_read_named",
     "srtp_gpu_tune", "srtp_gpu_counter",
     "rtcp_decode_batch_dev",
@@ -165,6 +169,10 @@ def load():
     L.srtp_stream_import.argtypes = [vp, ctypes.POINTER(StreamState)]
     L.srtp_alloc_many.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_int,
                                   ctypes.c_char_p, sz, ctypes.c_int]
+    L.srtp_rx_index.argtypes = [ctypes.POINTER(StreamState), vp, vp, vp, vp,
+                                sz, vp]
+    L.srtp_rx_fold.argtypes = [ctypes.POINTER(StreamState), ctypes.c_int, vp,
+                               sz, vp, ctypes.POINTER(sz)]
     L.srtp_gpu_prof.argtypes = [ctypes.c_int]
     L.srtp_gpu_tune.argtypes = [ctypes.c_char_p, ctypes.c_long]
     L.srtp_gpu_counter.argtypes = [ctypes.c_char_p]

@@ -57,6 +57,9 @@ def _load():
     u64p = ctypes.POINTER(ctypes.c_uint64)
     lib.oracle_stream_state.argtypes = [vp, ctypes.c_uint32, u32p, u32p,
                                         u64p, u64p]
+    lib.oracle_stream_set.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint64, ctypes.c_uint64]
     return lib
 
 

@@ -158,3 +158,89 @@ def test_bench_spawns_two_gpu_ranks():
     assert ln["n_gpus"] == 2 and ln["dist_world"] == 2
     assert ln["verified_roundtrip"] is True and ln["errors"] == 0
     assert ln["config"]["workload"].startswith("config5")
+
+
+def test_split_stream_fold_on_device_results(torch_cuda):
+    """one stream with loss, reordering across the shard boundary, replays
+    and forged packets, unprotected on the GPU as two shards (rank 1 from
+    the header-only boundary guess) and folded with srtp_rx_index /
+    srtp_rx_fold (re_amd/shard.py): equal to the same stream unprotected
+    in one call, and to the oracle receiver (tests/test_rxfold_cpu.py
+    covers the fold against the oracle on the CPU)"""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import test_rxfold_cpu as X
+    from oracle_lib import OracleBackend
+    torch = torch_cuda
+    O = OracleBackend()
+    suite = X.CM80
+    key = X.key_for(suite)
+    ixs = [65000 + i for i in range(3000) if i % 37 != 5]
+    # protect on the GPU, in index order, slot per packet
+    plain = [X.rtp(ix & 0xffff, ix) for ix in ixs]
+
+    def arena_dev(pkts, room):
+        slot = (max(len(p) for p in pkts) + room + 15) & ~15
+        buf = np.zeros(slot * len(pkts), dtype=np.uint8)
+        pos = np.arange(len(pkts), dtype=np.uint32) * slot
+        end = pos + np.array([len(p) for p in pkts], dtype=np.uint32)
+        for i, p in enumerate(pkts):
+            buf[pos[i]:end[i]] = np.frombuffer(p, dtype=np.uint8)
+        return buf, pos, end, pos + slot
+
+    buf, pos, end, cap = arena_dev(plain, 16)
+    dev = torch.from_numpy(buf).cuda()
+    tx = P.Srtp(suite, key)
+    assert not run(torch, "srtp_encrypt", tx, dev, pos, end, cap, 0,
+                   len(plain)).any()
+    host = dev.cpu().numpy()
+    prot = {ix: host[pos[i]:end[i]].tobytes() for i, ix in enumerate(ixs)}
+    tx.close()
+    order = list(ixs)
+    b = len(order) // 2
+    # the packet just before the boundary arrives 3 packets after it
+    late = order.pop(b - 1)
+    order.insert(b + 2, late)
+    pkts = [prot[ix] for ix in order]
+    pkts.insert(b + 5, prot[order[b - 10]])          # replay across it
+    pkts.insert(b - 20, pkts[b - 40])                # replay before it
+    f = bytearray(pkts[b + 30])
+    f[24] ^= 1
+    pkts.insert(b + 31, bytes(f))                    # forged
+    n = len(pkts)
+    truth, fin = X.receive(O, suite, pkts)
+
+    # unsharded on the GPU
+    buf, pos, end, cap = arena_dev(pkts, 0)
+    one = torch.from_numpy(buf).cuda()
+    rx = P.Srtp(suite, key)
+    e1 = run(torch, "srtp_decrypt", rx, one, pos, end.copy(), cap, 0, n)
+    assert (e1 == truth).all()
+    e, so = rx.export(X.SSRC)
+    assert e == 0
+    st_one = (so.roc, so.s_l, so.s_l_set, so.replay_rtp_lix,
+              so.replay_rtp_bitmap)
+    rx.close()
+
+    # two shards on the GPU, then the fold
+    two = torch.from_numpy(buf).cuda()
+    end2 = end.copy()
+    guess = X.assumed_boundary(pkts[:b])
+    recs = []
+    for r, (a, z) in enumerate(((0, b), (b, n))):
+        c = P.Srtp(suite, key)
+        st0 = X.state(*guess) if r else X.state()
+        if r:
+            assert c.import_(st0) == 0
+        res = run(torch, "srtp_decrypt", c, two, pos, end2, cap, a, z)
+        recs.append(S.rx_records(st0, buf, pos[a:z], end[a:z], res))
+        c.close()
+    rec = np.concatenate(recs)
+    assert (rec["res"] != truth).any()     # the ranks alone disagree
+    st = X.state()
+    err, nd = S.rx_fold(st, suite, rec)
+    assert nd == n and (err == truth).all()
+    assert (st.roc, st.s_l, st.s_l_set, st.replay_rtp_lix,
+            st.replay_rtp_bitmap) == st_one
+    assert (st.roc, st.s_l, st.replay_rtp_lix, st.replay_rtp_bitmap) == fin

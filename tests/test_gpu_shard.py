@@ -197,17 +197,20 @@ def test_split_stream_fold_on_device_results(torch_cuda):
     host = dev.cpu().numpy()
     prot = {ix: host[pos[i]:end[i]].tobytes() for i, ix in enumerate(ixs)}
     tx.close()
-    order = list(ixs)
-    b = len(order) // 2
-    # the packet just before the boundary arrives 3 packets after it
-    late = order.pop(b - 1)
-    order.insert(b + 2, late)
-    pkts = [prot[ix] for ix in order]
-    pkts.insert(b + 5, prot[order[b - 10]])          # replay across it
-    pkts.insert(b - 20, pkts[b - 40])                # replay before it
-    f = bytearray(pkts[b + 30])
+    # rank 0 gets the first half minus one late packet, which arrives as
+    # rank 1's third packet, below the top rank 1 guesses as seen
+    L, R = list(ixs[:len(ixs) // 2]), list(ixs[len(ixs) // 2:])
+    late = L.pop(-3)
+    R.insert(2, late)
+    left = [prot[ix] for ix in L]
+    left.insert(len(left) - 20, prot[L[-40]])        # replay inside rank 0
+    right = [prot[ix] for ix in R]
+    right.insert(5, prot[L[-10]])                    # replay across it
+    f = bytearray(right[30])
     f[24] ^= 1
-    pkts.insert(b + 31, bytes(f))                    # forged
+    right.insert(31, bytes(f))                       # forged
+    pkts = left + right
+    b = len(left)
     n = len(pkts)
     truth, fin = X.receive(O, suite, pkts)
 

@@ -151,8 +151,10 @@ def test_srtcp_then_rtcp_decode(torch_cuda):
                                 c_d.data_ptr(), er.data_ptr(), n)
         assert rc == 0 and not bool(er.any())
     torch.cuda.synchronize()
-    assert torch.equal(dev[:n * 1232].view(n, 1232)[:, :1200],
-                       torch.from_numpy(arena).cuda().view(n, 1232)[:, :1200])
+    slot = int(pos[1] - pos[0])          # make_rtcp_arena's slot
+    assert slot % 64 == 0 and arena.size == n * slot
+    assert torch.equal(dev[:n * slot].view(n, slot)[:, :1200],
+                       torch.from_numpy(arena).cuda().view(n, slot)[:, :1200])
     maxmsg = 4
     desc = torch.zeros(n * maxmsg * 5, dtype=torch.int32, device="cuda")
     nm, ee, st = (torch.zeros(n, dtype=torch.int32, device="cuda")

@@ -106,7 +106,9 @@ __global__ void k_mp_iota(uint32_t *v, const uint32_t *sess, K *kin,
 
 /* per packet: its (clamped) session's count, the unstable slot in it;
  * MP_HPER packets per thread, their atomics in flight together */
+#ifndef MP_HPER
 #define MP_HPER 4
+#endif
 __global__ void k_mp_hist(const uint32_t *sess, uint32_t *cnt,
 			  uint32_t *slot, uint32_t n, uint32_t nsess,
 			  struct sgpu_plan_out *out)

@@ -620,6 +620,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     c_rerun0 = (P.counter("rejects"), P.counter("folds"), P.counter("gated"))
+    voided0 = P.counter("prof_voided")
     t0 = time.perf_counter()
     errors = run_steps(sess_sets)
     torch.cuda.synchronize()
@@ -627,6 +628,9 @@ def main():
     if world > 1:
         dist.barrier()
     prof = P.prof_read_named()
+    # launches behind a rejected device plan exit at once: the profiler
+    # leaves them out of every slot (srtp_kernels.hip launch/prof_drain)
+    voided = P.counter("prof_voided") - voided0
     P.prof_enable(False)
     elapsed = t1 - t0
     if forge_pk is not None and pipelined:
@@ -697,6 +701,13 @@ def main():
                      "gbs": nbytes / (avg_ms * 1e-3) / 1e9})
     kern.sort(key=lambda d: -d["avg_ms"] * d["launches"])
     dom = kern[0] if kern else None
+    if dom:
+        # a roofline no launch could reach means the profiler counted work
+        # that did not run: fail loudly rather than print it
+        per_step = dom["avg_ms"] * dom["launches"] / args.steps
+        assert dom["gbs"] <= HBM_PEAK_GBS, ("impossible roofline", dom)
+        assert per_step <= T / args.steps * 1e3 * 1.001 or world > 1, \
+            ("dominant kernel longer than the step", dom, T)
     # HBM traffic and the integer roofline of the SAME kernel on the SAME
     # workload, from the committed rocprofv3 PMC passes (scripts/
     # gpu_pmc_r03.sh -> scripts/pmc_r03.py); omitted when no pass matches
@@ -772,7 +783,8 @@ def main():
         "folds": {"device": P.counter("devfolds"),
                   "host": P.counter("folds")},
         "plans": {"rejected": P.counter("rejects"),
-                  "per_stream": P.counter("splans")},
+                  "per_stream": P.counter("splans"),
+                  "voided_launches": voided},
         "verified_roundtrip": verified,
         "roofline": roof,
     }

@@ -192,8 +192,11 @@ int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
  * before packet 0): err[i] = the reference receiver's result.  Stops at
  * the first packet whose true index differs from the one its rank
  * authenticated at (the rank's boundary state was wrong, so its verdict
- * is void): *ndone = that packet's position and *st = the exact state
- * before it -- re-run packets ndone.. from *st (srtp_stream_import).
+ * is void), or whose replay verdict the whole stream's window changes
+ * (0 <-> EALREADY: the rank's bytes, pos and end for it are then those of
+ * the other outcome, src/srtp/srtp.c:355-368, 413-429): *ndone = that
+ * packet's position and *st = the exact state before it -- re-run packets
+ * ndone.. from *st (srtp_stream_import) on their received bytes.
  * *ndone == n when every verdict stands; *st is then the final state.
  * 0 or EINVAL.
  */

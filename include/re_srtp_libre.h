@@ -13,7 +13,10 @@
  * udp_send_helper() (:874-928): the helpers below, then the socket's
  * receive handler or sendto().  Bytes, pos/end and stream states are those
  * of srtp_decrypt() / srtp_encrypt() in datagram order; a datagram that
- * fails to unprotect is dropped and counted.  Deviation: udp_send()
+ * fails to unprotect is dropped and counted.  rtcp-mux sockets work: a
+ * datagram whose payload type is RTCP's (rtp_pt_is_rtcp(), include/
+ * re_rtp.h:333, as src/rtp/rtp.c:184-196 demultiplexes) takes the SRTCP
+ * transform, srtcp_decrypt() / srtcp_encrypt().  Deviation: udp_send()
  * returns 0 when the packet is queued; a later failure is counted, not
  * returned.
  */

@@ -30,12 +30,14 @@
  * PLI/SLI/AFB/FIR, XR RRTR/DLRR, unknown types), then the same with
  * truncations, bad versions, bad lengths and counts, and random bytes.
  *
- * Usage: oracle/_ref/gen_rtcp_golden > tests/golden/rtcp_decode_golden.json
+ * Usage: scripts/make_rtcp_golden.sh (decode cases; `encode`: rtcp_encode
+ * cases, tests/golden/rtcp_encode_golden.json.gz)
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <re.h>
+#include "rtcp.h"          /* rtcp_rr_encode, rtcp_encode_h (src/rtp) */
 
 static uint64_t rng_s = 0x7C7C7C7Cull;
 
@@ -326,6 +328,133 @@ static void fields(const struct rtcp_msg *m, uint32_t *ssrc, uint32_t *aux)
 	}
 }
 
+/* ---- the decoded contents as items (include/re_rtcp_batch.h struct
+ * rtcp_item): [msg, kind, sub, v0..v6, "hex"], where the reference copied
+ * variable data out of the packet (SDES item data, BYE reason, APP data)
+ * the offset word is 0 and "hex" holds the copied bytes; TWCC chunks /
+ * deltas and AFB stay in the packet (mbuf_alloc_ref) and their offsets
+ * are the reference's own ---- */
+static int nitem;
+
+static void item(int msg, int kind, int sub, uint32_t v0, uint32_t v1,
+		 uint32_t v2, uint32_t v3, uint32_t v4, uint32_t v5,
+		 uint32_t v6, const uint8_t *data, size_t dlen)
+{
+	size_t i;
+	printf("%s[%d,%d,%d,%u,%u,%u,%u,%u,%u,%u,\"", nitem++ ? "," : "", msg,
+	       kind, sub, v0, v1, v2, v3, v4, v5, v6);
+	for (i = 0; i < dlen; i++)
+		printf("%02x", data[i]);
+	printf("\"]");
+}
+
+static void items(const struct rtcp_msg *m, int k)
+{
+	uint32_t i, j;
+	switch (m->hdr.pt) {
+	case RTCP_SR:
+		item(k, 1, 0, m->r.sr.ntp_sec, m->r.sr.ntp_frac, m->r.sr.rtp_ts,
+		     m->r.sr.psent, m->r.sr.osent, 0, 0, NULL, 0);
+		/*@fallthrough@*/
+	case RTCP_RR: {
+		const struct rtcp_rr *rrv = m->hdr.pt == RTCP_SR ?
+			m->r.sr.rrv : m->r.rr.rrv;
+		for (i = 0; i < m->hdr.count; i++)
+			item(k, 2, 0, rrv[i].ssrc, rrv[i].fraction,
+			     (uint32_t)rrv[i].lost & 0xffffffu, rrv[i].last_seq,
+			     rrv[i].jitter, rrv[i].lsr, rrv[i].dlsr, NULL, 0);
+		break;
+	}
+	case RTCP_SDES:
+		for (i = 0; i < m->hdr.count && m->r.sdesv; i++) {
+			const struct rtcp_sdes *sd = &m->r.sdesv[i];
+			item(k, 3, 0, sd->src, sd->n, 0, 0, 0, 0, 0, NULL, 0);
+			for (j = 0; j < sd->n; j++)
+				item(k, 4, sd->itemv[j].type,
+				     sd->itemv[j].length, 0, 0, 0, 0, 0, 0,
+				     (const uint8_t *)sd->itemv[j].data,
+				     sd->itemv[j].length);
+		}
+		break;
+	case RTCP_BYE:
+		for (i = 0; i < m->hdr.count; i++)
+			item(k, 5, 0, m->r.bye.srcv[i], 0, 0, 0, 0, 0, 0, NULL,
+			     0);
+		if (m->r.bye.reason)
+			item(k, 6, 0, (uint32_t)strlen(m->r.bye.reason), 0, 0,
+			     0, 0, 0, 0, (const uint8_t *)m->r.bye.reason,
+			     strlen(m->r.bye.reason));
+		break;
+	case RTCP_APP:
+		item(k, 7, m->hdr.count, m->r.app.src,
+		     be32(m->r.app.name), 0, (uint32_t)m->r.app.data_len, 0,
+		     0, 0, m->r.app.data, m->r.app.data_len);
+		break;
+	case RTCP_FIR:
+		item(k, 8, 0, m->r.fir.ssrc, 0, 0, 0, 0, 0, 0, NULL, 0);
+		break;
+	case RTCP_NACK:
+		item(k, 9, 0, m->r.nack.ssrc, m->r.nack.fsn, m->r.nack.blp, 0,
+		     0, 0, 0, NULL, 0);
+		break;
+	case RTCP_RTPFB:
+	case RTCP_PSFB:
+		item(k, 10, m->hdr.count, m->r.fb.ssrc_packet,
+		     m->r.fb.ssrc_media, m->r.fb.n, 0, 0, 0, 0, NULL, 0);
+		if (m->hdr.pt == RTCP_RTPFB && m->hdr.count == RTCP_RTPFB_GNACK)
+			for (i = 0; i < m->r.fb.n; i++)
+				item(k, 11, 0, m->r.fb.fci.gnackv[i].pid,
+				     m->r.fb.fci.gnackv[i].blp, 0, 0, 0, 0, 0,
+				     NULL, 0);
+		else if (m->hdr.pt == RTCP_RTPFB &&
+			 m->hdr.count == RTCP_RTPFB_TWCC) {
+			const struct twcc *t = m->r.fb.fci.twccv;
+			if (t->deltas->pos != t->chunks->end) {
+				fprintf(stderr, "TWCC deltas not after chunks\n");
+				exit(1);
+			}
+			item(k, 12, 0, t->seq, t->count, t->reftime, t->fbcount,
+			     (uint32_t)t->chunks->pos,
+			     (uint32_t)(t->chunks->end - t->chunks->pos),
+			     (uint32_t)(t->deltas->end - t->deltas->pos), NULL,
+			     0);
+		}
+		else if (m->hdr.pt == RTCP_PSFB &&
+			 m->hdr.count == RTCP_PSFB_SLI)
+			for (i = 0; i < m->r.fb.n; i++)
+				item(k, 13, 0, m->r.fb.fci.sliv[i].first,
+				     m->r.fb.fci.sliv[i].number,
+				     m->r.fb.fci.sliv[i].picid, 0, 0, 0, 0, NULL,
+				     0);
+		else if (m->hdr.pt == RTCP_PSFB &&
+			 m->hdr.count == RTCP_PSFB_AFB)
+			item(k, 14, 0, (uint32_t)m->r.fb.fci.afb->pos,
+			     (uint32_t)(m->r.fb.fci.afb->end -
+					m->r.fb.fci.afb->pos), 0, 0, 0, 0, 0,
+			     NULL, 0);
+		else if (m->hdr.pt == RTCP_PSFB &&
+			 m->hdr.count == RTCP_PSFB_FIR)
+			for (i = 0; i < m->r.fb.n; i++)
+				item(k, 15, 0, m->r.fb.fci.firv[i].ssrc,
+				     m->r.fb.fci.firv[i].seq_n, 0, 0, 0, 0, 0,
+				     NULL, 0);
+		break;
+	case RTCP_XR:
+		item(k, 16, 0, m->r.xr.ssrc, m->r.xr.bt, m->r.xr.block_len, 0,
+		     0, 0, 0, NULL, 0);
+		if (m->r.xr.bt == RTCP_XR_RRTR)
+			item(k, 17, 0, m->r.xr.rb.rrtrb.ntp_msw,
+			     m->r.xr.rb.rrtrb.ntp_lsw, 0, 0, 0, 0, 0, NULL, 0);
+		else if (m->r.xr.bt == RTCP_XR_DLRR)
+			item(k, 18, 0, m->r.xr.rb.dlrrb.ssrc,
+			     m->r.xr.rb.dlrrb.lrr, m->r.xr.rb.dlrrb.dlrr, 0, 0,
+			     0, 0, NULL, 0);
+		break;
+	default:
+		break;
+	}
+}
+
 static void emit(const uint8_t *pkt, size_t len)
 {
 	struct mbuf *mb = mbuf_alloc(len + 1);
@@ -344,6 +473,8 @@ static void emit(const uint8_t *pkt, size_t len)
 	for (i = 0; i < len; i++)
 		printf("%02x", pkt[i]);
 	printf("\",\"msgs\":[");
+	struct rtcp_msg *msgv[256];
+	int nkeep = 0;
 	for (;;) {
 		uint32_t ssrc, aux;
 		start = mb->pos;
@@ -354,17 +485,315 @@ static void emit(const uint8_t *pkt, size_t len)
 		printf("%s[%zu,%zu,%u,%u,%u,%u,%u]", nm++ ? "," : "", start,
 		       mb->pos - start, msg->hdr.pt, msg->hdr.count,
 		       msg->hdr.length, ssrc, aux);
-		mem_deref(msg);
+		if (nkeep < 256)
+			msgv[nkeep++] = msg;
+		else
+			mem_deref(msg);
+	}
+	printf("],\"items\":[");
+	nitem = 0;
+	for (i = 0; i < (size_t)nkeep; i++) {
+		items(msgv[i], (int)i);
+		mem_deref(msgv[i]);
 	}
 	printf("],\"err\":%d,\"stop\":%zu}", err, start);
 	mem_deref(mb);
 }
 
-int main(void)
+/* ---- encode cases (`gen_rtcp_golden encode`) --------------------------
+ * Random compound specs in the form of include/re_rtcp_batch.h
+ * (struct rtcp_enc_msg and its arrays), each packet built by the
+ * reference's own rtcp_encode() calls on one mbuf (src/rtp/pkt.c:316,
+ * rtcp_vencode :136-313) with rtcp_rr_encode (rr.c:35) / rtcp_sdes_encode
+ * (sdes.c:36) / raw-byte handlers; the output bytes, or the errno of the
+ * first call that failed. */
+#define EMAX 64
+struct espec {
+	uint32_t msg[EMAX][14];         /* pt count flags w0..w5 first num off
+					   len */
+	uint32_t nmsg;
+	uint32_t rb[EMAX * 4][7];
+	uint32_t nrb;
+	uint32_t chunk[EMAX * 4][3];
+	uint32_t nchunk;
+	uint32_t sdes[EMAX * 16][3];
+	uint32_t nsdes;
+	uint32_t src[EMAX * 4];
+	uint32_t nsrc;
+	uint8_t pool[16384];
+	uint32_t npool;
+};
+
+struct ectx {
+	const struct espec *e;
+	const uint32_t *m;
+};
+
+static int ench_rb(struct mbuf *mb, void *arg)
+{
+	const struct ectx *x = arg;
+	uint32_t i;
+	int err = 0;
+	for (i = 0; i < x->m[10] && !err; i++) {
+		const uint32_t *r = x->e->rb[x->m[9] + i];
+		struct rtcp_rr rr;
+		memset(&rr, 0, sizeof(rr));
+		rr.ssrc = r[0];
+		rr.fraction = r[1] & 0xff;
+		rr.lost = (int)(r[2] << 8) >> 8;
+		rr.last_seq = r[3];
+		rr.jitter = r[4];
+		rr.lsr = r[5];
+		rr.dlsr = r[6];
+		err = rtcp_rr_encode(mb, &rr);
+	}
+	return err;
+}
+
+static int ench_sdes(struct mbuf *mb, void *arg)
+{
+	const struct ectx *x = arg;
+	uint32_t i, j;
+	int err = 0;
+	for (i = 0; i < x->m[10] && !err; i++) {
+		const uint32_t *ch = x->e->chunk[x->m[9] + i];
+		char str[4][300];
+		int ty[4];
+		for (j = 0; j < ch[2] && j < 4; j++) {
+			const uint32_t *it = x->e->sdes[ch[1] + j];
+			ty[j] = (int)it[0];
+			memcpy(str[j], x->e->pool + it[2], it[1]);
+			str[j][it[1]] = 0;
+		}
+		switch (ch[2]) {
+		case 0: err = rtcp_sdes_encode(mb, ch[0], 0); break;
+		case 1: err = rtcp_sdes_encode(mb, ch[0], 1, ty[0], str[0]);
+			break;
+		case 2: err = rtcp_sdes_encode(mb, ch[0], 2, ty[0], str[0],
+					       ty[1], str[1]);
+			break;
+		case 3: err = rtcp_sdes_encode(mb, ch[0], 3, ty[0], str[0],
+					       ty[1], str[1], ty[2], str[2]);
+			break;
+		default: err = rtcp_sdes_encode(mb, ch[0], 4, ty[0], str[0],
+						ty[1], str[1], ty[2], str[2],
+						ty[3], str[3]);
+			break;
+		}
+	}
+	return err;
+}
+
+static int ench_raw(struct mbuf *mb, void *arg)
+{
+	const struct ectx *x = arg;
+	return x->m[13] ? mbuf_write_mem(mb, x->e->pool + x->m[12], x->m[13])
+			: 0;
+}
+
+/* pool bytes of the given alphabet (no NUL: the reference takes C strings) */
+static uint32_t pool_str(struct espec *e, uint32_t len)
+{
+	uint32_t off = e->npool, i;
+	for (i = 0; i < len; i++)
+		e->pool[e->npool++] = (uint8_t)('!' + rndn(94));
+	return off;
+}
+
+static uint32_t pool_raw(struct espec *e, uint32_t len)
+{
+	uint32_t off = e->npool, i;
+	for (i = 0; i < len; i++)
+		e->pool[e->npool++] = (uint8_t)rnd();
+	return off;
+}
+
+static void espec_msg(struct espec *e, int bad)
+{
+	static const uint32_t pts[] = {200, 201, 202, 203, 204, 192, 193, 205,
+				       206, 207};
+	uint32_t *m = e->msg[e->nmsg++], i, j;
+	memset(m, 0, 14 * 4);
+	m[0] = pts[rndn(10)];
+	if (bad == 1 || bad == 2)
+		m[0] = 202;
+	else if (bad == 3)
+		m[0] = 204;
+	m[1] = rndn(8) ? rndn(32) : rndn(256);  /* count > 31: pkt.c:92 */
+	for (i = 0; i < 6; i++)
+		m[3 + i] = (uint32_t)rnd();
+	switch (m[0]) {
+	case 200:
+	case 201:
+		m[9] = e->nrb;
+		m[10] = rndn(4);
+		for (i = 0; i < m[10]; i++)
+			for (j = 0; j < 7; j++)
+				e->rb[e->nrb + i][j] = (uint32_t)rnd();
+		e->nrb += m[10];
+		if (rndn(8))
+			m[1] = m[10];   /* as callers set it, mostly */
+		break;
+	case 202:
+		m[9] = e->nchunk;
+		m[10] = bad ? 1 + rndn(3) : rndn(4);
+		for (i = 0; i < m[10]; i++) {
+			uint32_t *ch = e->chunk[e->nchunk + i];
+			ch[0] = (uint32_t)rnd();
+			ch[1] = e->nsdes;
+			ch[2] = (bad == 1 && i == 0) ? 0 : 1 + rndn(4);
+			for (j = 0; j < ch[2]; j++) {
+				uint32_t *it = e->sdes[e->nsdes++];
+				it[0] = 1 + rndn(8);
+				it[1] = (bad == 2 && j == 0) ? 256 + rndn(20)
+							      : rndn(40);
+				it[2] = pool_str(e, it[1]);
+			}
+		}
+		e->nchunk += m[10];
+		if (rndn(8))
+			m[1] = m[10];
+		break;
+	case 203:
+		m[1] = rndn(5);
+		m[9] = e->nsrc;
+		for (i = 0; i < m[1]; i++)
+			e->src[e->nsrc++] = (uint32_t)rnd();
+		if (rndn(2)) {
+			m[2] = 1;
+			m[13] = rndn(8) ? rndn(30) : 250 + rndn(60);
+			m[12] = pool_str(e, m[13]);
+		}
+		break;
+	case 204:
+		m[13] = bad == 3 ? 1 + 4 * rndn(4) + rndn(3) : 4 * rndn(5);
+		m[12] = pool_raw(e, m[13]);
+		break;
+	case 205:
+	case 206:
+	case 207:
+		m[13] = 4 * rndn(6) + (rndn(6) ? 0 : 1 + rndn(3));
+		m[12] = pool_raw(e, m[13]);
+		break;
+	default:
+		break;
+	}
+	if (bad == 4)
+		m[0] = 194 + rndn(6);           /* no such type: EINVAL */
+}
+
+static int espec_encode(const struct espec *e, uint32_t k, struct mbuf *mb)
+{
+	const uint32_t *m = e->msg[k];
+	struct ectx x = {e, m};
+	const uint32_t *w = m + 3;
+	uint8_t name[4];
+	switch (m[0]) {
+	case 200:
+		return rtcp_encode(mb, RTCP_SR, m[1], w[0], w[1], w[2], w[3],
+				   w[4], w[5], ench_rb, &x);
+	case 201:
+		return rtcp_encode(mb, RTCP_RR, m[1], w[0], ench_rb, &x);
+	case 202:
+		return rtcp_encode(mb, RTCP_SDES, m[1], ench_sdes, &x);
+	case 203: {
+		char reason[400];
+		memcpy(reason, e->pool + m[12], m[13]);
+		reason[m[13]] = 0;
+		return rtcp_encode(mb, RTCP_BYE, m[1], e->src + m[9],
+				   m[2] ? reason : NULL);
+	}
+	case 204:
+		name[0] = (uint8_t)(w[1] >> 24);
+		name[1] = (uint8_t)(w[1] >> 16);
+		name[2] = (uint8_t)(w[1] >> 8);
+		name[3] = (uint8_t)w[1];
+		return rtcp_encode(mb, RTCP_APP, m[1], w[0], name,
+				   m[13] ? e->pool + m[12] : NULL,
+				   (size_t)m[13]);
+	case 192:
+		return rtcp_encode(mb, RTCP_FIR, m[1], w[0]);
+	case 193:
+		return rtcp_encode(mb, RTCP_NACK, m[1], w[0], w[1], w[2]);
+	case 205:
+	case 206:
+		return rtcp_encode(mb, (enum rtcp_type)m[0], m[1], w[0], w[1],
+				   ench_raw, &x);
+	case 207:
+		return rtcp_encode(mb, RTCP_XR, m[1], w[0], ench_raw, &x);
+	default:
+		return rtcp_encode(mb, (enum rtcp_type)m[0], m[1], w[0]);
+	}
+}
+
+static void put_arr(const char *name, const uint32_t *a, uint32_t n,
+		    uint32_t width)
+{
+	uint32_t i, j;
+	printf(",\"%s\":[", name);
+	for (i = 0; i < n; i++) {
+		printf("%s", i ? "," : "");
+		if (width > 1)
+			printf("[");
+		for (j = 0; j < width; j++)
+			printf("%s%u", j ? "," : "", a[i * width + j]);
+		if (width > 1)
+			printf("]");
+	}
+	printf("]");
+}
+
+static int encode_main(void)
+{
+	static struct espec e;
+	int k, first_case = 1;
+	uint32_t i;
+
+	rng_s = 0xE5C0DEull;
+	printf("{\"generator\":\"oracle/gen_rtcp_golden.c encode (reference "
+	       "src/rtp/pkt.c rtcp_encode, rr.c rtcp_rr_encode, sdes.c "
+	       "rtcp_sdes_encode)\",\"cases\":[");
+	for (k = 0; k < 1500; k++) {
+		struct mbuf *mb = mbuf_alloc(256);
+		uint32_t nm = 1 + rndn(6);
+		/* one case in 8 carries one invalid message */
+		int bad = rndn(8) ? 0 : 1 + (int)rndn(4), err = 0;
+		uint32_t badat = rndn(nm);
+		memset(&e, 0, sizeof(e));
+		for (i = 0; i < nm; i++)
+			espec_msg(&e, i == badat ? bad : 0);
+		for (i = 0; i < nm && !err; i++)
+			err = espec_encode(&e, i, mb);
+		printf("%s\n{", first_case ? "" : ",");
+		first_case = 0;
+		printf("\"err\":%d", err);
+		put_arr("msgs", &e.msg[0][0], e.nmsg, 14);
+		put_arr("rb", &e.rb[0][0], e.nrb, 7);
+		put_arr("chunks", &e.chunk[0][0], e.nchunk, 3);
+		put_arr("sdes", &e.sdes[0][0], e.nsdes, 3);
+		put_arr("srcs", e.src, e.nsrc, 1);
+		printf(",\"pool\":\"");
+		for (i = 0; i < e.npool; i++)
+			printf("%02x", e.pool[i]);
+		printf("\",\"out\":\"");
+		if (!err)
+			for (i = 0; i < mb->end; i++)
+				printf("%02x", mb->buf[i]);
+		printf("\"}");
+		mem_deref(mb);
+	}
+	printf("\n]}\n");
+	return 0;
+}
+
+int main(int argc, char **argv)
 {
 	struct pb p;
 	int c, k;
 	uint32_t i;
+
+	if (argc > 1 && !strcmp(argv[1], "encode"))
+		return encode_main();
 
 	printf("{\"generator\":\"oracle/gen_rtcp_golden.c (reference "
 	       "src/rtp/pkt.c rtcp_decode loop, rtp.c:164)\",\"cases\":[");

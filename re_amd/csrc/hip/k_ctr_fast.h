@@ -624,9 +624,12 @@ k_ctr_fast_any(const KArgs a)
 /*
  * The lean kernel for multi-session batches (the multi-session device
  * planner's shape: every packet planned, one suite, per-lane keys, packets
- * taken in the planner's launch order c.idx).  A forged packet is left
- * decrypted with SV_CIPHERED: the caller undoes the whole batch (general
- * kernel, c.undo) before the host fold, so no restore pass runs here.
+ * taken in the planner's launch order c.idx).  A forged packet is listed
+ * in c.flist and left decrypted with SV_CIPHERED; the pass behind this
+ * launch (k_ctr_refix_list<NR, true>, one workgroup per listed packet with
+ * its own session's keys) puts it back to its ciphertext, and the device
+ * verdict fold (sgpu_mfold_rtp) writes the EAUTH results and states --
+ * only a fold the device cannot settle undoes the batch for the host.
  */
 #ifndef CTRF_MK_BLOCK
 #define CTRF_MK_BLOCK 768

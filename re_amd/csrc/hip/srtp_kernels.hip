@@ -1030,10 +1030,17 @@ extern "C" int sgpu_setup_sessions(const struct sgpu_keyreq *req,
 #include <pthread.h>
 static pthread_mutex_t g_prof_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_prof_on;
-struct prof_ev { hipEvent_t a, b; int slot; uint32_t jobs; const char *name;
-		  int nr, prot; };
+struct prof_ev { hipEvent_t a, b, c; int slot; uint32_t jobs;
+		  const char *name; int nr, prot; int gw; };
 static struct prof_ev *g_pev;
 static size_t g_npev, g_pev_cap;
+/* a launch behind a device plan does nothing when the plan was rejected
+ * (its guard words, k_ctr_fast.h fast_class, k_ctr.h k_ctr_hmac_any, the
+ * single-word guards): the words are copied to pinned memory right behind
+ * the launch and such a launch is not counted as work (sgpu_prof_voided) */
+#define PROF_GRING 65536
+static uint32_t *g_pguard;              /* pinned, 4 words per event */
+static uint64_t g_prof_voided;
 static double g_prof_ms[32];
 static uint64_t g_prof_launch[32], g_prof_jobs[32];
 /* the kernel a slot's launches ran ("<name><nr,prot>"; "+" appended when
@@ -1052,8 +1059,20 @@ static void prof_drain_locked(void)
 {
 	for (size_t k = 0; k < g_npev; k++) {
 		float ms = 0;
-		(void)hipEventSynchronize(g_pev[k].b);
+		(void)hipEventSynchronize(g_pev[k].gw ? g_pev[k].c : g_pev[k].b);
 		(void)hipEventElapsedTime(&ms, g_pev[k].a, g_pev[k].b);
+		if (g_pev[k].gw) {
+			const uint32_t *w = g_pguard + 4 * k;
+			const bool work = g_pev[k].gw == 4 ?
+				(!w[0] || !w[1] || !w[2] || !w[3]) : !w[0];
+			(void)hipEventDestroy(g_pev[k].c);
+			if (!work) {
+				g_prof_voided++;
+				(void)hipEventDestroy(g_pev[k].a);
+				(void)hipEventDestroy(g_pev[k].b);
+				continue;
+			}
+		}
 		const int sl = g_pev[k].slot;
 		char nm[SGPU_PROF_NAME];
 		snprintf(nm, sizeof(nm), "%s<%d,%d>", g_pev[k].name,
@@ -1092,9 +1111,20 @@ extern "C" void sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs,
 	pthread_mutex_unlock(&g_prof_lock);
 }
 
+extern "C" uint64_t sgpu_prof_voided(void)
+{
+	pthread_mutex_lock(&g_prof_lock);
+	prof_drain_locked();
+	const uint64_t v = g_prof_voided;
+	pthread_mutex_unlock(&g_prof_lock);
+	return v;
+}
+
+/* gw: the launch's guard (a.c.guard) is 4 class words, work iff one is 0
+ * (the any-class kernels), or 1 word, work iff 0 */
 static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		  hipStream_t stream, uint32_t block, const char *name,
-		  int nr, int prot)
+		  int nr, int prot, int gw = 1)
 {
 	struct prof_ev pe;
 	int prof = 0;
@@ -1114,6 +1144,7 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		pe.name = name;
 		pe.nr = nr;
 		pe.prot = prot;
+		pe.gw = 0;
 		pthread_mutex_lock(&g_prof_lock);
 		if (g_npev == g_pev_cap) {
 			size_t nc = g_pev_cap ? 2 * g_pev_cap : 64;
@@ -1123,6 +1154,19 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 				g_pev = np;
 				g_pev_cap = nc;
 			}
+		}
+		if (!g_pguard &&
+		    hipHostMalloc((void **)&g_pguard, PROF_GRING * 16,
+				  hipHostMallocDefault) != hipSuccess)
+			g_pguard = NULL;
+		if (a.c.guard && g_pguard && g_npev < PROF_GRING &&
+		    g_npev < g_pev_cap &&
+		    hipEventCreate(&pe.c) == hipSuccess) {
+			pe.gw = gw == 4 ? 4 : 1;
+			(void)hipMemcpyAsync(g_pguard + 4 * g_npev, a.c.guard,
+					     4u * pe.gw, hipMemcpyDeviceToHost,
+					     stream);
+			(void)hipEventRecord(pe.c, stream);
 		}
 		if (g_npev < g_pev_cap)
 			g_pev[g_npev++] = pe;
@@ -1230,7 +1274,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				    : sgpu_pick_ctr14_fast(prot, 0);
 		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
 			       (hipStream_t)stream, sgpu_ctr_fast_block(prot),
-			       "k_ctr_fast_any", nr, prot);
+			       "k_ctr_fast_any", nr, prot, 4);
 		if (!e && !prot && c->flist) {
 			/* one workgroup per listed forged packet (grid-
 			 * strided past 1024); all exit at once if none */
@@ -1287,7 +1331,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				       : sgpu_pick_ctr14_fast_mk(prot),
 			      a, c->n, prof_slot(mode, nr, 3, prot),
 			      (hipStream_t)stream, sgpu_ctr_fast_mk_block(),
-			      "k_ctr_fast_mk", nr, prot);
+			      "k_ctr_fast_mk", nr, prot, 4);
 		if (!e && !prot && c->flist) {
 			/* forged packets back to their ciphertext, each with
 			 * its own session's keys (the device verdict fold of
@@ -1331,7 +1375,7 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 					      : "k_ctr_hmac_any") :
 				  (c->uniform ? "k_ctr_hmac_uni"
 					      : "k_ctr_hmac_compact"),
-		      nr, prot);
+		      nr, prot, mode == SGPU_MODE_CTR && shift < 0 ? 4 : 1);
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,

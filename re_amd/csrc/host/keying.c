@@ -11,6 +11,7 @@
 #include "re_srtp_batch.h"
 #include "re_srtp_keying.h"
 #include "../srtpgpu.h"
+#include "fault.h"
 
 /* the profiles tls_srtp_keyinfo maps (tls.c:1101-1132) */
 static int profile(enum srtp_suite suite, size_t *key, size_t *salt)
@@ -78,7 +79,7 @@ int srtp_dtls_keying_many(const struct srtp_dtls_secret *sec, size_t n,
 		if (sec[i].prf != SRTP_DTLS_PRF_SHA256 &&
 		    sec[i].prf != SRTP_DTLS_PRF_SHA384)
 			return EINVAL;
-	km = malloc(n * 2 * size);
+	km = fi_malloc(n * 2 * size);
 	if (!km)
 		return ENOMEM;
 	err = sgpu_dtls_prf((const uint8_t *)sec, (uint32_t)n,
@@ -105,8 +106,8 @@ int srtp_alloc_dtls_many(struct srtp **txv, struct srtp **rxv, size_t n,
 		return EINVAL;
 	if (!size)
 		return ENOSYS;
-	cli = malloc((n ? n : 1) * size);
-	srv = malloc((n ? n : 1) * size);
+	cli = fi_malloc((n ? n : 1) * size);
+	srv = fi_malloc((n ? n : 1) * size);
 	if (!cli || !srv) {
 		err = ENOMEM;
 		goto out;

@@ -16,6 +16,13 @@ struct mem_hdr {
 	size_t pad;          /* keep the payload 32-byte aligned */
 };
 
+static size_t g_live;           /* live blocks (leak checks) */
+
+size_t re_amd_mem_live(void)
+{
+	return __atomic_load_n(&g_live, __ATOMIC_RELAXED);
+}
+
 static struct mem_hdr *hdr_of(const void *p)
 {
 	return (struct mem_hdr *)((uint8_t *)(uintptr_t)p - sizeof(struct mem_hdr));
@@ -29,6 +36,7 @@ void *mem_alloc(size_t size, mem_destroy_h *dh)
 	m->nrefs = 1;
 	m->dh = dh;
 	m->size = size;
+	__atomic_add_fetch(&g_live, 1, __ATOMIC_RELAXED);
 	return m + 1;
 }
 
@@ -71,6 +79,7 @@ void *mem_deref(void *data)
 	if (m->dh)
 		m->dh(data);
 	free(m);
+	__atomic_sub_fetch(&g_live, 1, __ATOMIC_RELAXED);
 	return NULL;
 }
 

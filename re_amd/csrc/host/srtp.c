@@ -33,6 +33,7 @@
 #include "re_srtp_batch.h"
 #include "re_rtcp_batch.h"
 #include "../srtpgpu.h"
+#include "fault.h"
 #include "pool.h"
 
 #ifndef EAUTH
@@ -105,7 +106,7 @@ static __thread struct tk_owner *t_own;
 static struct tk_owner *tk_me(void)
 {
 	if (!t_own)
-		t_own = calloc(1, sizeof(*t_own));
+		t_own = fi_calloc(1, sizeof(*t_own));
 	return t_own;
 }
 
@@ -195,6 +196,12 @@ static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
  * now fails with ENOMEM */
 static long g_fail_grow;
+/* fault.h: the k-th allocation from now fails (srtp_gpu_tune "fail_alloc") */
+long re_amd_fail_alloc;
+/* live mem_* blocks of the standalone allocator (mem.c; absent when libre
+ * provides mem_*, LIBRE=1) */
+extern size_t re_amd_mem_live(void) __attribute__((weak));
+static uint32_t slots_live(void);
 
 static void count(uint64_t *c, uint64_t v)
 {
@@ -221,6 +228,15 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
 	if (!strcmp(name, "gated"))
 		return __atomic_load_n(&g_cnt_gated, __ATOMIC_RELAXED);
+	if (!strcmp(name, "prof_voided"))
+		return sgpu_prof_voided();
+	if (!strcmp(name, "fail_alloc"))
+		return (uint64_t)__atomic_load_n(&re_amd_fail_alloc,
+						 __ATOMIC_RELAXED);
+	if (!strcmp(name, "mem_live"))
+		return re_amd_mem_live ? re_amd_mem_live() : 0;
+	if (!strcmp(name, "slots_live"))
+		return slots_live();
 	return 0;
 }
 
@@ -259,6 +275,9 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.par_min = value > 0 ? (size_t)value : 4096;
 	else if (!strcmp(name, "fail_grow"))
 		__atomic_store_n(&g_fail_grow, value > 0 ? value : 0,
+				 __ATOMIC_RELAXED);
+	else if (!strcmp(name, "fail_alloc"))
+		__atomic_store_n(&re_amd_fail_alloc, value > 0 ? value : 0,
 				 __ATOMIC_RELAXED);
 	else
 		return EINVAL;
@@ -317,9 +336,34 @@ static int slots_get(uint32_t *slots, size_t n)
 		pthread_rwlock_wrlock(&g_table_rw);
 		held = 1;
 	}
-	for (i = 0; i < n; i++)
-		slots[i] = g_nfree ? g_free[--g_nfree] : g_next_slot++;
-	err = sgpu_table_reserve(g_next_slot);
+	err = 0;
+	/* the free list can hold every slot ever handed out, so slot_put
+	 * never allocates (and never loses a slot) */
+	if ((uint64_t)g_next_slot + n > g_free_cap) {
+		uint64_t nc = g_free_cap ? g_free_cap : 256;
+		uint32_t *nf;
+		while (nc < (uint64_t)g_next_slot + n)
+			nc *= 2;
+		nf = nc <= UINT32_MAX ? fi_realloc(g_free, nc * sizeof(*nf))
+				      : NULL;
+		if (nf) {
+			g_free = nf;
+			g_free_cap = (uint32_t)nc;
+		}
+		else
+			err = ENOMEM;
+	}
+	if (!err) {
+		const uint32_t next0 = g_next_slot, nfree0 = g_nfree;
+		for (i = 0; i < n; i++)
+			slots[i] = g_nfree ? g_free[--g_nfree]
+					   : g_next_slot++;
+		err = sgpu_table_reserve(g_next_slot);
+		if (err) {
+			g_next_slot = next0;    /* nothing handed out */
+			g_nfree = nfree0;
+		}
+	}
 	pthread_mutex_unlock(&g_lock);
 	if (held)
 		pthread_rwlock_unlock(&g_table_rw);
@@ -337,18 +381,20 @@ static void table_unlock(void)
 	pthread_rwlock_unlock(&g_table_rw);
 }
 
+/* device table slots held by live contexts (leak checks) */
+static uint32_t slots_live(void)
+{
+	uint32_t n;
+	pthread_mutex_lock(&g_lock);
+	n = g_next_slot - g_nfree;
+	pthread_mutex_unlock(&g_lock);
+	return n;
+}
+
 static void slot_put(uint32_t s)
 {
 	pthread_mutex_lock(&g_lock);
-	if (g_nfree == g_free_cap) {
-		uint32_t nc = g_free_cap ? 2 * g_free_cap : 256;
-		uint32_t *nf = realloc(g_free, nc * sizeof(*nf));
-		if (nf) {
-			g_free = nf;
-			g_free_cap = nc;
-		}
-	}
-	if (g_nfree < g_free_cap)
+	if (g_nfree < g_free_cap)       /* always: slots_get sized it */
 		g_free[g_nfree++] = s;
 	pthread_mutex_unlock(&g_lock);
 }
@@ -426,8 +472,8 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 	 * them) */
 	tk_drain();
 
-	req = calloc(n ? n : 1, sizeof(*req));
-	slots = calloc(n ? n : 1, sizeof(*slots));
+	req = fi_calloc(n ? n : 1, sizeof(*req));
+	slots = fi_calloc(n ? n : 1, sizeof(*slots));
 	if (!req || !slots) {
 		err = ENOMEM;
 		goto out;
@@ -453,7 +499,7 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
 		goto out;
 	}
 	for (i = 0; i < n; i++) {
-		struct srtp *s = mem_zalloc(sizeof(*s), destructor);
+		struct srtp *s = fi_mem_zalloc(sizeof(*s), destructor);
 		if (!s) {
 			size_t k;
 			for (k = i; k < n; k++)
@@ -1157,11 +1203,11 @@ static int engine_init(struct engine *E, int op, size_t n,
 	memset(E, 0, sizeof(*E));
 	E->op = op;
 	E->n = n;
-	E->sess = malloc((n ? n : 1) * sizeof(*E->sess));
-	E->pi = calloc(n ? n : 1, sizeof(*E->pi));
-	E->rec = calloc(n ? n : 1, sizeof(*E->rec));
-	E->uniq = malloc((nsess ? nsess : 1) * sizeof(*E->uniq));
-	E->snap = malloc((nsess ? nsess : 1) * sizeof(*E->snap));
+	E->sess = fi_malloc((n ? n : 1) * sizeof(*E->sess));
+	E->pi = fi_calloc(n ? n : 1, sizeof(*E->pi));
+	E->rec = fi_calloc(n ? n : 1, sizeof(*E->rec));
+	E->uniq = fi_malloc((nsess ? nsess : 1) * sizeof(*E->uniq));
+	E->snap = fi_malloc((nsess ? nsess : 1) * sizeof(*E->snap));
 	if (!E->sess || !E->pi || !E->rec || !E->uniq || !E->snap)
 		return ENOMEM;
 	for (i = 0; i < n; i++) {
@@ -1172,7 +1218,7 @@ static int engine_init(struct engine *E, int op, size_t n,
 	}
 	/* distinct sessions referenced (array order of sessv) */
 	{
-		uint8_t *used = calloc(nsess ? nsess : 1, 1);
+		uint8_t *used = fi_calloc(nsess ? nsess : 1, 1);
 		if (!used)
 			return ENOMEM;
 		for (i = 0; i < n; i++)
@@ -1243,7 +1289,7 @@ static __thread struct ws *t_ws;
 
 static struct ws *ws_new(void)
 {
-	struct ws *w = calloc(1, sizeof(*w));
+	struct ws *w = fi_calloc(1, sizeof(*w));
 	if (!w)
 		return NULL;
 	w->stream = sgpu_stream_create();
@@ -1273,8 +1319,8 @@ static int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
 	sgpu_stream_sync(w->stream);
 	sgpu_host_free(p->h);
 	sgpu_free(p->d);
-	p->h = sgpu_host_alloc(c);
-	p->d = sgpu_malloc(c);
+	p->h = fi_sgpu_host_alloc(c);
+	p->d = fi_sgpu_malloc(c);
 	if (!p->h || !p->d) {
 		sgpu_host_free(p->h);
 		sgpu_free(p->d);
@@ -1290,7 +1336,7 @@ static int idx_reserve(struct ws *w, size_t n)
 {
 	if (n > w->cls_cap) {
 		size_t c = n + n / 2 + 64;
-		uint32_t *ix = realloc(w->cls_idx, c * sizeof(*ix));
+		uint32_t *ix = fi_realloc(w->cls_idx, c * sizeof(*ix));
 		if (!ix)
 			return ENOMEM;
 		w->cls_idx = ix;
@@ -1480,9 +1526,9 @@ static int sess_host(struct srtp **sessv, size_t nsess)
 			m++;
 	}
 	if (m) {
-		lst = malloc(m * sizeof(*lst));
-		slots = malloc(m * sizeof(*slots));
-		st = malloc(m * sizeof(*st));
+		lst = fi_malloc(m * sizeof(*lst));
+		slots = fi_malloc(m * sizeof(*slots));
+		st = fi_malloc(m * sizeof(*st));
 		if (!lst || !slots || !st) {
 			err = ENOMEM;
 			goto out;
@@ -1553,9 +1599,9 @@ static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 	err = engine_init(&E, op, n, sessv, nsess, sidx);
 	if (err)
 		goto out;
-	outp = calloc(n ? n : 1, sizeof(*outp));
-	soff = calloc(n ? n : 1, sizeof(*soff));
-	koff = calloc(n ? n : 1, sizeof(*koff));
+	outp = fi_calloc(n ? n : 1, sizeof(*outp));
+	soff = fi_calloc(n ? n : 1, sizeof(*soff));
+	koff = fi_calloc(n ? n : 1, sizeof(*koff));
 	if (!outp || !soff || !koff) {
 		err = ENOMEM;
 		goto out;
@@ -1599,7 +1645,7 @@ static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 					koff[i] = tot;
 					tot += E.rec[i].ext_end - E.pi[i].start;
 				}
-			keep = malloc(tot ? tot : 1);
+			keep = fi_malloc(tot ? tot : 1);
 			if (!keep) {
 				err = ENOMEM;
 				goto out;
@@ -1758,7 +1804,7 @@ static void pc_run(struct pc_req *list)
 			table_rdlock();
 			err = sess_host(sv, n);
 			if (!err) {
-				uint32_t *idx = malloc(n * sizeof(*idx));
+				uint32_t *idx = fi_malloc(n * sizeof(*idx));
 				if (!idx)
 					err = ENOMEM;
 				for (i = 0; !err && i < n; i++)
@@ -2065,7 +2111,7 @@ static int ulog_push(struct ulogv *L, struct srtp *s, struct srtp_stream *st)
 	struct ulog *u;
 	if (L->n == L->cap) {
 		size_t nc = L->cap ? 2 * L->cap : 256;
-		struct ulog *nu = realloc(L->v, nc * sizeof(*nu));
+		struct ulog *nu = fi_realloc(L->v, nc * sizeof(*nu));
 		if (!nu)
 			return ENOMEM;
 		L->v = nu;
@@ -2836,7 +2882,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 	if (err)
 		return err;
 	if (w->nev < nch) {
-		void **ne = realloc(w->ev, nch * sizeof(*ne));
+		void **ne = fi_realloc(w->ev, nch * sizeof(*ne));
 		if (!ne)
 			return ENOMEM;
 		w->ev = ne;
@@ -2847,7 +2893,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			w->nev++;
 		}
 	}
-	fl = malloc(4 * nch * sizeof(*fl) + 4 * sizeof(*fl));
+	fl = fi_malloc(4 * nch * sizeof(*fl) + 4 * sizeof(*fl));
 	if (!fl)
 		return ENOMEM;
 
@@ -4263,7 +4309,7 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 			return EINVAL;
 	if (d->n > UINT32_MAX / 4 || d->arena_size > UINT32_MAX)
 		return EINVAL;
-	t = calloc(1, sizeof(*t));
+	t = fi_calloc(1, sizeof(*t));
 	if (!t)
 		return ENOMEM;
 	t->owner = pthread_self();
@@ -4280,7 +4326,7 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 	while (t_tk_n >= TK_MAX)
 		tk_finish_one();
 	if (!t_gates) {
-		t_gates = sgpu_malloc(TK_GATES * 4);
+		t_gates = fi_sgpu_malloc(TK_GATES * 4);
 		if (!t_gates || sgpu_memset(t_gates, 0, TK_GATES * 4, NULL) ||
 		    sgpu_stream_sync(NULL)) {
 			t->kind = TK_DONE;
@@ -4411,9 +4457,9 @@ static int dev_staged(int op, struct srtp **sessv, size_t nsess,
 {
 	const size_t n = d->n;
 	struct srtp_batch hb;
-	uint32_t *hpos = malloc(n * 4), *hend = malloc(n * 4);
-	uint32_t *hcap = malloc(n * 4), *hsess = d->sess ? malloc(n * 4) : NULL;
-	int32_t *herrv = malloc(n * 4);
+	uint32_t *hpos = fi_malloc(n * 4), *hend = fi_malloc(n * 4);
+	uint32_t *hcap = fi_malloc(n * 4), *hsess = d->sess ? fi_malloc(n * 4) : NULL;
+	int32_t *herrv = fi_malloc(n * 4);
 	void *stream = d->stream;
 	int err = 0, r;
 
@@ -4755,9 +4801,21 @@ int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
 			err[i] = r->res;        /* tag verdict: ROC bump stays */
 			continue;
 		}
-		if (!replay_check(&rp, ix)) {
-			err[i] = EALREADY;
-			continue;
+		/* a replay verdict the fold changes voids the packet's side
+		 * effects as well: HMAC suites return EALREADY before the
+		 * decrypt with pos at the payload (srtp.c:355-368), GCM leaves
+		 * pos there (:413-422), success restores it (:429).  Check
+		 * the window on a copy so the state stays the one before it */
+		{
+			struct replay tmp = rp;
+			const int ok = replay_check(&tmp, ix);
+			if (ok != (r->res == 0))
+				goto void_verdict;
+			rp = tmp;
+			if (!ok) {
+				err[i] = EALREADY;
+				continue;
+			}
 		}
 		err[i] = 0;
 		if (r->seq > s_l)
@@ -4780,22 +4838,57 @@ int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
 
 /* ---- RTCP compound decode (include/re_rtcp_batch.h) ------------------- */
 
+int rtcp_decode_full_batch_dev(const uint8_t *arena, size_t arena_size,
+			       const uint32_t *pos, const uint32_t *end,
+			       size_t n, struct rtcp_desc *descv,
+			       uint32_t maxmsg, uint32_t *nmsg,
+			       struct rtcp_item *itemv, uint32_t maxitem,
+			       uint32_t *nitem, int32_t *err, uint32_t *stop,
+			       void *stream)
+{
+	if (!n)
+		return 0;
+	if (!arena || !pos || !end || !nmsg || !err || !stop ||
+	    (maxmsg && !descv) || (maxitem && (!itemv || !nitem)) ||
+	    (itemv && !nitem) || n > UINT32_MAX ||
+	    (uint64_t)n * maxmsg > ((uint64_t)1 << 40) ||
+	    (uint64_t)n * maxitem > ((uint64_t)1 << 40))
+		return EINVAL;
+	if (!gpu_ready())
+		return ENOSYS;
+	return sgpu_rtcp_walk(arena, arena_size, pos, end, (uint32_t)n, descv,
+			      maxmsg, nmsg, maxitem ? itemv : NULL, maxitem,
+			      nitem, err, stop, stream);
+}
+
 int rtcp_decode_batch_dev(const uint8_t *arena, size_t arena_size,
 			  const uint32_t *pos, const uint32_t *end, size_t n,
 			  struct rtcp_desc *descv, uint32_t maxmsg,
 			  uint32_t *nmsg, int32_t *err, uint32_t *stop,
 			  void *stream)
 {
-	if (!n)
+	return rtcp_decode_full_batch_dev(arena, arena_size, pos, end, n,
+					  descv, maxmsg, nmsg, NULL, 0, NULL,
+					  err, stop, stream);
+}
+
+/* ---- RTCP compound encode (include/re_rtcp_batch.h) ------------------- */
+
+int rtcp_encode_batch_dev(const struct rtcp_enc_batch *b)
+{
+	if (!b)
+		return EINVAL;
+	if (!b->n)
 		return 0;
-	if (!arena || !pos || !end || !nmsg || !err || !stop ||
-	    (maxmsg && !descv) || n > UINT32_MAX ||
-	    (uint64_t)n * maxmsg > ((uint64_t)1 << 40))
+	if (!b->arena || !b->pos || !b->end || !b->cap || !b->mfirst ||
+	    !b->err || b->n >= UINT32_MAX || b->arena_size > UINT32_MAX ||
+	    (b->nmsg && !b->msgv) || (b->nrb && !b->rbv) ||
+	    (b->nchunk && !b->chunkv) || (b->nsdes && !b->sdesv) ||
+	    (b->nsrc && !b->srcv) || (b->pool_size && !b->pool))
 		return EINVAL;
 	if (!gpu_ready())
 		return ENOSYS;
-	return sgpu_rtcp_walk(arena, arena_size, pos, end, (uint32_t)n, descv,
-			      maxmsg, nmsg, err, stop, stream);
+	return sgpu_rtcp_encode(b);
 }
 
 /* ---- diagnostics: per-kernel-class device time (HIP events) ----------- */

@@ -32,6 +32,7 @@
 #include "re_srtp_batch.h"
 #include "re_srtp_udp.h"
 #include "../srtpgpu.h"
+#include "fault.h"
 
 #define SEND_RETRY_MS 2000      /* bound on a full socket buffer */
 
@@ -86,15 +87,15 @@ static void dir_free(struct dir *d)
 
 static int dir_alloc(struct dir *d, size_t batch, size_t slot)
 {
-	d->h = sgpu_host_alloc(batch * slot);
-	d->d = sgpu_malloc(batch * slot);
-	d->hw = sgpu_host_alloc(batch * 12);
-	d->dw = sgpu_malloc(batch * 12);
-	d->he = sgpu_host_alloc(batch * 4);
-	d->de = sgpu_malloc(batch * 4);
-	d->msg = calloc(batch, sizeof(*d->msg));
-	d->iov = calloc(batch, sizeof(*d->iov));
-	d->src = calloc(batch, sizeof(*d->src));
+	d->h = fi_sgpu_host_alloc(batch * slot);
+	d->d = fi_sgpu_malloc(batch * slot);
+	d->hw = fi_sgpu_host_alloc(batch * 12);
+	d->dw = fi_sgpu_malloc(batch * 12);
+	d->he = fi_sgpu_host_alloc(batch * 4);
+	d->de = fi_sgpu_malloc(batch * 4);
+	d->msg = fi_calloc(batch, sizeof(*d->msg));
+	d->iov = fi_calloc(batch, sizeof(*d->iov));
+	d->src = fi_calloc(batch, sizeof(*d->src));
 	return d->h && d->d && d->hw && d->dw && d->he && d->de && d->msg &&
 	       d->iov && d->src ? 0 : ENOMEM;
 }
@@ -134,7 +135,7 @@ int srtp_udp_alloc(struct srtp_udp **sup, int fd, struct srtp *rx,
 	slot = (slot + 15) & ~(size_t)15;
 	if ((uint64_t)batch * slot > UINT32_MAX)
 		return EINVAL;
-	su = mem_zalloc(sizeof(*su), destructor);
+	su = fi_mem_zalloc(sizeof(*su), destructor);
 	if (!su)
 		return ENOMEM;
 	su->fd = fd;
@@ -289,6 +290,17 @@ static void rx_deliver(struct srtp_udp *su, struct dir *d)
 	su->ns[SRTP_UDP_RX_DELIVER] += now_ns() - t0;
 }
 
+/* hand a batch over undecrypted with one error for every datagram (a
+ * failed issue or completion): each received datagram still reaches the
+ * handler exactly once */
+static void rx_fail(struct srtp_udp *su, struct dir *d, int err)
+{
+	size_t i;
+	for (i = 0; i < d->n; i++)
+		d->he[i] = err;
+	rx_deliver(su, d);
+}
+
 int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
 {
 	struct dir *d;
@@ -312,16 +324,29 @@ int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
 	if (n > 0) {
 		/* batch k+1 queued behind batch k on the GPU */
 		err = gpu_issue(su, d, 0, su->rx);
-		if (err)
+		if (err) {
+			/* batch k is in flight: complete and deliver it
+			 * first, then k+1 with the error */
+			if (prev >= 0) {
+				struct dir *p = &su->in[prev];
+				if (gpu_finish(su, p, SRTP_UDP_RX_GPU))
+					rx_fail(su, p, err);
+				else
+					rx_deliver(su, p);
+			}
+			rx_fail(su, d, err);
 			return -err;
+		}
 		if (su->pipeline) {
 			su->rpend = su->rcur;
 			su->rcur ^= 1;
 		}
 		else {
 			err = gpu_finish(su, d, SRTP_UDP_RX_GPU);
-			if (err)
+			if (err) {
+				rx_fail(su, d, err);
 				return -err;
+			}
 			done = n;
 			rx_deliver(su, d);
 		}
@@ -331,21 +356,27 @@ int srtp_udp_recv(struct srtp_udp *su, int timeout_ms)
 		 * runs on the GPU now) */
 		struct dir *p = &su->in[prev];
 		err = gpu_finish(su, p, SRTP_UDP_RX_GPU);
-		if (err)
+		if (err) {
+			rx_fail(su, p, err);
 			return -err;
+		}
 		done = (int)p->n;
 		rx_deliver(su, p);
 	}
 	return done;
 }
 
-/* sendmmsg of chunk d's protected datagrams; sent count or -errno */
-static long tx_send(struct srtp_udp *su, struct dir *d,
-		    const struct sockaddr *dst, socklen_t dstlen, int *errv)
+/* sendmmsg of chunk d's protected datagrams: 0 or errno, *nsent = the
+ * datagrams that went out.  errv[i] = the protect result, or, after a
+ * failed sendmmsg, the errno for each datagram that was not sent */
+static int tx_send(struct srtp_udp *su, struct dir *d,
+		   const struct sockaddr *dst, socklen_t dstlen, int *errv,
+		   size_t *nsent)
 {
 	const uint64_t t0 = now_ns();
 	const size_t m = d->n;
 	size_t i, k, waited = 0;
+	int err = 0;
 
 	for (i = 0, k = 0; i < m; i++) {
 		if (errv)
@@ -373,15 +404,25 @@ static long tx_send(struct srtp_udp *su, struct dir *d,
 				waited += 10;
 				continue;
 			}
-			su->ns[SRTP_UDP_TX_SYSCALL] += now_ns() - t0;
-			su->n_tx += i;
-			return -errno;
+			err = errno;
+			break;
 		}
 		i += (size_t)r;
 	}
 	su->ns[SRTP_UDP_TX_SYSCALL] += now_ns() - t0;
-	su->n_tx += k;
-	return (long)k;
+	su->n_tx += i;
+	*nsent = i;
+	if (err && errv) {
+		/* the (i+1)-th protected datagram and every later one */
+		size_t j, c = 0;
+		for (j = 0; j < m; j++) {
+			if (d->he[j])
+				continue;
+			if (c++ >= i)
+				errv[j] = err;
+		}
+	}
+	return err;
 }
 
 static void tx_stage(struct srtp_udp *su, struct dir *d, struct mbuf **mbv,
@@ -430,34 +471,27 @@ int srtp_udp_send(struct srtp_udp *su, const struct sockaddr *dst,
 			if (err)
 				break;
 			if (!su->pipeline) {
-				long r;
+				size_t r = 0;
 				err = gpu_finish(su, d, SRTP_UDP_TX_GPU);
 				if (err)
 					break;
-				r = tx_send(su, d, dst, dstlen,
-					    errv ? errv + a : NULL);
-				if (r < 0) {
-					err = (int)-r;
-					break;
-				}
-				sent += (size_t)r;
-				done = a + m;
+				err = tx_send(su, d, dst, dstlen,
+					      errv ? errv + a : NULL, &r);
+				sent += r;
+				done = a + m;   /* the chunk's errv are set */
 				continue;
 			}
 		}
 		if (su->pipeline && j > 0) {
 			struct dir *p = &su->out[(j - 1) & 1];
-			long r;
+			size_t r = 0;
 			err = gpu_finish(su, p, SRTP_UDP_TX_GPU);
 			if (err)
 				break;
-			r = tx_send(su, p, dst, dstlen,
-				    errv ? errv + (j - 1) * su->batch : NULL);
-			if (r < 0) {
-				err = (int)-r;
-				break;
-			}
-			sent += (size_t)r;
+			err = tx_send(su, p, dst, dstlen,
+				      errv ? errv + (j - 1) * su->batch : NULL,
+				      &r);
+			sent += r;
 			done = (j - 1) * su->batch + p->n;
 		}
 	}

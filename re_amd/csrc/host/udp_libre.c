@@ -19,6 +19,15 @@
  * states are those of srtp_decrypt()/srtp_encrypt() in datagram order; a
  * packet that fails to unprotect is dropped (counted), as an SRTP media
  * transform does.
+ *
+ * rtcp-mux (RFC 5761; libre demultiplexes it in src/rtp/rtp.c:184-196 by
+ * rtp_pt_is_rtcp(), include/re_rtp.h:333): a datagram whose second byte
+ * carries a payload type in 64..95 is RTCP and takes the SRTCP transform
+ * (srtcp_decrypt / srtcp_encrypt semantics).  One queue keeps datagram
+ * order; at a flush its RTP packets run as one srtp_*_batch_dev call and
+ * its RTCP packets as one srtcp_*_batch_dev call on the same arena (the
+ * two have separate state: ROC / s_l / RTP window vs SRTCP index / RTCP
+ * window), then every packet continues down the chain in arrival order.
  */
 #include <errno.h>
 #include <stdbool.h>
@@ -48,8 +57,19 @@ struct q {                      /* one direction's queue */
 	struct sa *sa;          /* source / destination per packet */
 	size_t *pre;            /* the mbuf's pos before the packet */
 	uint32_t *len;          /* packet length */
+	uint8_t *rtcp;          /* the packet is RTCP (rtcp-mux) */
+	uint32_t *win;          /* its index in the window arrays: the RTP
+				   packets first, then the RTCP ones */
 	size_t n;
 };
+
+/* include/re_rtp.h:333 rtp_pt_is_rtcp() on the second byte, as
+ * src/rtp/rtp.c:184-196 demultiplexes rtcp-mux */
+static bool is_rtcp(const uint8_t *p, size_t len)
+{
+	const uint8_t pt = len >= 2 ? (p[1] & 0x7f) : 0;
+	return pt >= 64 && pt <= 95;
+}
 
 struct srtp_udp_helper {
 	struct udp_helper *uh;
@@ -74,6 +94,8 @@ static void q_free(struct q *q)
 	free(q->sa);
 	free(q->pre);
 	free(q->len);
+	free(q->rtcp);
+	free(q->win);
 }
 
 static int q_alloc(struct q *q, size_t batch, size_t slot)
@@ -87,41 +109,58 @@ static int q_alloc(struct q *q, size_t batch, size_t slot)
 	q->sa = calloc(batch, sizeof(*q->sa));
 	q->pre = calloc(batch, sizeof(*q->pre));
 	q->len = calloc(batch, sizeof(*q->len));
+	q->rtcp = calloc(batch, sizeof(*q->rtcp));
+	q->win = calloc(batch, sizeof(*q->win));
 	return q->h && q->d && q->hw && q->dw && q->he && q->de && q->sa &&
-	       q->pre && q->len ? 0 : ENOMEM;
+	       q->pre && q->len && q->rtcp && q->win ? 0 : ENOMEM;
 }
 
-/* one GPU call over the queue: windows + arena up, batch, all down */
+/* the queue's GPU calls: windows + arena up, the RTP packets as one
+ * SRTP batch and the RTCP packets as one SRTCP batch, all down */
 static int q_run(struct srtp_udp_helper *h, struct q *q, int prot,
 		 struct srtp *ctx)
 {
 	const size_t n = q->n, used = n * h->slot;
 	struct srtp_batch_dev b;
-	size_t i;
-	int err;
+	size_t i, nrtp = 0, k;
+	int err, pass;
 
-	for (i = 0; i < n; i++) {
+	for (i = 0; i < n; i++)
+		nrtp += !q->rtcp[i];
+	for (i = 0, k = 0; i < n; i++) {
 		const uint32_t base = (uint32_t)(i * h->slot);
-		q->hw[i] = base;
-		q->hw[n + i] = base + q->len[i];
-		q->hw[2 * n + i] = base + (uint32_t)h->slot;
+		const size_t w = q->rtcp[i] ? nrtp + (i - k) : k;
+		if (!q->rtcp[i])
+			k++;
+		q->win[i] = (uint32_t)w;
+		q->hw[w] = base;
+		q->hw[n + w] = base + q->len[i];
+		q->hw[2 * n + w] = base + (uint32_t)h->slot;
 	}
 	err = sgpu_memcpy_h2d(q->d, q->h, used, h->stream);
 	if (!err)
 		err = sgpu_memcpy_h2d(q->dw, q->hw, n * 12, h->stream);
-	if (err)
-		return err;
-	memset(&b, 0, sizeof(b));
-	b.arena = q->d;
-	b.arena_size = used;
-	b.pos = q->dw;
-	b.end = q->dw + n;
-	b.cap = q->dw + 2 * n;
-	b.err = q->de;
-	b.n = n;
-	b.stream = h->stream;
-	err = prot ? srtp_encrypt_batch_dev(&ctx, 1, &b)
-		   : srtp_decrypt_batch_dev(&ctx, 1, &b);
+	for (pass = 0; pass < 2 && !err; pass++) {
+		const size_t off = pass ? nrtp : 0;
+		const size_t m = pass ? n - nrtp : nrtp;
+		if (!m)
+			continue;
+		memset(&b, 0, sizeof(b));
+		b.arena = q->d;
+		b.arena_size = used;
+		b.pos = q->dw + off;
+		b.end = q->dw + n + off;
+		b.cap = q->dw + 2 * n + off;
+		b.err = q->de + off;
+		b.n = m;
+		b.stream = h->stream;
+		if (!pass)
+			err = prot ? srtp_encrypt_batch_dev(&ctx, 1, &b)
+				   : srtp_decrypt_batch_dev(&ctx, 1, &b);
+		else
+			err = prot ? srtcp_encrypt_batch_dev(&ctx, 1, &b)
+				   : srtcp_decrypt_batch_dev(&ctx, 1, &b);
+	}
 	if (!err)
 		err = sgpu_memcpy_d2h(q->h, q->d, used, h->stream);
 	if (!err)
@@ -139,7 +178,8 @@ static struct mbuf *q_mbuf(const struct srtp_udp_helper *h,
 			   const struct q *q, size_t i)
 {
 	const uint32_t base = (uint32_t)(i * h->slot);
-	const size_t len = q->hw[q->n + i] - base;
+	const uint32_t w = q->win[i];
+	const size_t len = q->hw[q->n + w] - base;
 	struct mbuf *mb = mbuf_alloc(q->pre[i] + len);
 	if (!mb)
 		return NULL;
@@ -148,7 +188,7 @@ static struct mbuf *q_mbuf(const struct srtp_udp_helper *h,
 		mem_deref(mb);
 		return NULL;
 	}
-	mb->pos = q->pre[i] + (q->hw[i] - base);
+	mb->pos = q->pre[i] + (q->hw[w] - base);
 	return mb;
 }
 
@@ -164,7 +204,7 @@ static void flush_rx(struct srtp_udp_helper *h)
 	h->n_rx += q->n;
 	for (i = 0; i < q->n; i++) {
 		struct mbuf *mb;
-		if (err || q->he[i]) {
+		if (err || q->he[q->win[i]]) {
 			h->n_drop++;
 			continue;
 		}
@@ -191,7 +231,7 @@ static void flush_tx(struct srtp_udp_helper *h)
 	err = q_run(h, q, 1, h->tx);
 	for (i = 0; i < q->n; i++) {
 		struct mbuf *mb;
-		if (err || q->he[i]) {
+		if (err || q->he[q->win[i]]) {
 			h->n_drop++;
 			continue;
 		}
@@ -231,6 +271,7 @@ static bool q_push(struct srtp_udp_helper *h, struct q *q,
 		return false;
 	memcpy(q->h + q->n * h->slot, mbuf_buf(mb), len);
 	q->len[q->n] = (uint32_t)len;
+	q->rtcp[q->n] = is_rtcp(mbuf_buf(mb), len);
 	sa_cpy(&q->sa[q->n], sa);
 	q->pre[q->n] = mb->pos;
 	q->n++;
@@ -248,7 +289,8 @@ static bool recv_h(struct sa *src, struct mbuf *mb, void *arg)
 		 * and on down the chain in place */
 		flush_rx(h);
 		h->n_rx++;
-		if (srtp_decrypt(h->rx, mb)) {
+		if (is_rtcp(mbuf_buf(mb), mbuf_get_left(mb)) ?
+		    srtcp_decrypt(h->rx, mb) : srtp_decrypt(h->rx, mb)) {
 			h->n_drop++;
 			return true;
 		}
@@ -271,7 +313,8 @@ static bool send_h(int *err, struct sa *dst, struct mbuf *mb, void *arg)
 		return false;
 	if (!q_push(h, &h->sq, dst, mb)) {
 		flush_tx(h);
-		*err = srtp_encrypt(h->tx, mb);
+		*err = is_rtcp(mbuf_buf(mb), mbuf_get_left(mb)) ?
+		       srtcp_encrypt(h->tx, mb) : srtp_encrypt(h->tx, mb);
 		return *err != 0;       /* on down the chain, protected */
 	}
 	if (h->sq.n == h->batch)

@@ -564,12 +564,20 @@ int   sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
 
 /* kernel timing (HIP events recorded on the launch stream) */
 void  sgpu_prof_enable(int on);
+/* launches behind a rejected device plan (they did nothing), not counted
+ * by sgpu_prof_read */
+uint64_t sgpu_prof_voided(void);
 /* RTCP compound decode (rtcp_walk.hip, include/re_rtcp_batch.h) */
 struct rtcp_desc;
+struct rtcp_item;
+struct rtcp_enc_batch;
 int sgpu_rtcp_walk(const uint8_t *arena, uint64_t arena_size,
 		   const uint32_t *pos, const uint32_t *end, uint32_t n,
 		   struct rtcp_desc *descv, uint32_t maxmsg, uint32_t *nmsg,
+		   struct rtcp_item *itemv, uint32_t maxitem, uint32_t *nitem,
 		   int32_t *err, uint32_t *stop, void *stream);
+/* rtcp_encode.hip: the batch's packets into its arena (re_rtcp_batch.h) */
+int sgpu_rtcp_encode(const struct rtcp_enc_batch *b);
 
 #define SGPU_PROF_NAME 48
 void  sgpu_prof_read(double *ms, uint64_t *launches, uint64_t *jobs,

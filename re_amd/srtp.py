@@ -182,6 +182,10 @@ def load():
                                      ctypes.POINTER(ctypes.c_uint64)]
     L.rtcp_decode_batch_dev.argtypes = [vp, sz, vp, vp, sz, vp,
                                         ctypes.c_uint32, vp, vp, vp, vp]
+    L.rtcp_decode_full_batch_dev.argtypes = [vp, sz, vp, vp, sz, vp,
+                                             ctypes.c_uint32, vp, vp,
+                                             ctypes.c_uint32, vp, vp, vp, vp]
+    L.rtcp_encode_batch_dev.argtypes = [ctypes.POINTER(RtcpEncBatch)]
     L.srtp_udp_alloc.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, vp,
                                  sz, sz, UDP_RECV_H, vp]
     L.srtp_udp_recv.argtypes = [vp, ctypes.c_int]
@@ -477,6 +481,61 @@ def device_batch_dev(opname, sessions, arena_ptr, arena_size, pos_ptr,
     sv = session_array(sessions)
     return getattr(lib(), opname + "_batch_dev")(sv, len(sv),
                                                  ctypes.byref(b))
+
+
+class RtcpEncBatch(ctypes.Structure):
+    """struct rtcp_enc_batch (include/re_rtcp_batch.h); every pointer is
+    device memory"""
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_size", ctypes.c_size_t),
+                ("pos", ctypes.c_void_p), ("end", ctypes.c_void_p),
+                ("cap", ctypes.c_void_p), ("mfirst", ctypes.c_void_p),
+                ("msgv", ctypes.c_void_p), ("rbv", ctypes.c_void_p),
+                ("chunkv", ctypes.c_void_p), ("sdesv", ctypes.c_void_p),
+                ("srcv", ctypes.c_void_p), ("pool", ctypes.c_void_p),
+                ("nmsg", ctypes.c_uint32), ("nrb", ctypes.c_uint32),
+                ("nchunk", ctypes.c_uint32), ("nsdes", ctypes.c_uint32),
+                ("nsrc", ctypes.c_uint32), ("pool_size", ctypes.c_uint32),
+                ("err", ctypes.c_void_p), ("n", ctypes.c_size_t),
+                ("stream", ctypes.c_void_p)]
+
+
+# numpy layouts of the encode inputs (include/re_rtcp_batch.h)
+def rtcp_enc_dtypes():
+    import numpy as np
+    msg = np.dtype([("pt", "u1"), ("count", "u1"), ("flags", "<u2"),
+                    ("w", "<u4", (6,)), ("first", "<u4"), ("num", "<u4"),
+                    ("off", "<u4"), ("len", "<u4")])
+    rb = np.dtype([("ssrc", "<u4"), ("fraction", "<u4"), ("lost", "<u4"),
+                   ("last_seq", "<u4"), ("jitter", "<u4"), ("lsr", "<u4"),
+                   ("dlsr", "<u4")])
+    chunk = np.dtype([("src", "<u4"), ("first", "<u4"), ("num", "<u4")])
+    sdes = np.dtype([("type", "u1"), ("pad", "u1"), ("len", "<u2"),
+                     ("off", "<u4")])
+    assert msg.itemsize == 44 and rb.itemsize == 28 and sdes.itemsize == 8
+    return msg, rb, chunk, sdes
+
+
+def rtcp_encode_dev(arena_ptr, arena_size, pos_ptr, end_ptr, cap_ptr, n,
+                    mfirst_ptr, msg_ptr, nmsg, rb_ptr=None, nrb=0,
+                    chunk_ptr=None, nchunk=0, sdes_ptr=None, nsdes=0,
+                    src_ptr=None, nsrc=0, pool_ptr=None, pool_size=0,
+                    err_ptr=None, stream=None):
+    """rtcp_encode_batch_dev over device arrays; returns rc"""
+    b = RtcpEncBatch(arena_ptr, arena_size, pos_ptr, end_ptr, cap_ptr,
+                     mfirst_ptr, msg_ptr, rb_ptr, chunk_ptr, sdes_ptr,
+                     src_ptr, pool_ptr, nmsg, nrb, nchunk, nsdes, nsrc,
+                     pool_size, err_ptr, n, stream)
+    return lib().rtcp_encode_batch_dev(ctypes.byref(b))
+
+
+def rtcp_decode_full_dev(arena_ptr, arena_size, pos_ptr, end_ptr, n,
+                         desc_ptr, maxmsg, nmsg_ptr, item_ptr, maxitem,
+                         nitem_ptr, err_ptr, stop_ptr, stream=None):
+    """rtcp_decode_full_batch_dev: descriptors plus every message's items
+    (struct rtcp_item: 8 x uint32, word 0 = msg | kind << 16 | sub << 24)"""
+    return lib().rtcp_decode_full_batch_dev(
+        arena_ptr, arena_size, pos_ptr, end_ptr, n, desc_ptr, maxmsg,
+        nmsg_ptr, item_ptr, maxitem, nitem_ptr, err_ptr, stop_ptr, stream)
 
 
 def rtcp_decode_dev(arena_ptr, arena_size, pos_ptr, end_ptr, n, desc_ptr,

@@ -12,7 +12,10 @@ into libre) with its SRTP helper registered on a udp_sock
   receive: the protected datagrams from a plain socket through udp_read()
            -> the helper (GPU unprotect in batches, udp_recv_helper()) ->
            the socket's receive handler;
-  errors:  a forged and a replayed datagram among them are dropped.
+  errors:  a forged and a replayed datagram among them are dropped;
+  rtcp-mux: RTP and RTCP datagrams interleaved on one socket (fresh
+           contexts, a second helper): RTCP takes the SRTCP transform both
+           ways, in datagram order.
 
 Prints one JSON line with what the handler and the plain socket saw.
 """
@@ -174,8 +177,50 @@ def main():
                               ctypes.byref(t), ctypes.byref(dr))
     out["stats"] = [r.value, ok.value, t.value, dr.value]
     net.mem_deref(h)
+
+    # ---- rtcp-mux: every 10th datagram an RTCP receiver report ----
+    mux = mux_packets(arena, pos, end)
+    tx2, rx2, h2 = c_p(), c_p(), c_p()
+    assert lib.srtp_alloc(ctypes.byref(tx2), 1, key, 30, 0) == 0
+    assert lib.srtp_alloc(ctypes.byref(rx2), 1, key, 30, 0) == 0
+    got.clear()
+    want[0] = 1 << 30
+    assert lib.srtp_udp_helper_alloc(ctypes.byref(h2), us, 0, rx2, tx2, 64,
+                                     256, 1) == 0
+    for pkt in mux:
+        mb = net.mbuf_alloc(256)
+        net.mbuf_write_mem(mb, pkt, len(pkt))
+        mb.contents.pos = 0
+        assert net.udp_send(us, dst, mb) == 0
+        net.mem_deref(mb)
+    run(50)
+    wire2 = [peer.recv(2048) for _ in range(len(mux))]
+    out["mux_wire"] = [w.hex() for w in wire2]
+    want[0] = len(mux)
+    for d in wire2:
+        peer.sendto(d, addr)
+    run(2000)
+    out["mux_got"] = [(p, e, b.hex()) for p, e, b in got]
+    net.mem_deref(h2)
     net.mem_deref(us)
     print(json.dumps(out))
+
+
+def mux_packets(arena, pos, end, n=200):
+    """n datagrams of one rtcp-mux socket: config-1 RTP packets with an
+    RTCP receiver report (PT 201, SSRC 0x01020304, one report block) as
+    every 10th (tests/test_gpu_libre.py rebuilds the same list)"""
+    out = []
+    k = 0
+    for i in range(n):
+        if i % 10 == 9:
+            rr = bytes([0x81, 201, 0, 7]) + (0x01020304).to_bytes(4, "big") \
+                + bytes((i * 7 + j) & 0xff for j in range(24))
+            out.append(rr)
+        else:
+            out.append(arena[pos[k]:end[k]].tobytes())
+            k += 1
+    return out
 
 
 if __name__ == "__main__":

@@ -239,3 +239,44 @@ def test_async_pending_session_busy_for_other_threads(torch_cuda):
     assert e == 0 and st.s_l == 1109
     tx.close()
     other.close()
+
+
+def test_profiler_counts_only_launches_that_did_work(torch_cuda):
+    """srtp_gpu_prof: a lean-kernel launch queued behind a device plan that
+    the device rejects exits at once; it must not count as work (jobs, ms),
+    or a bench line would price it as a full launch.  The accepted plan's
+    launch counts its packets exactly."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    key = keys_for(1, 1)[0]
+    seqs = list(range(100, 1100))
+    seqs[500], seqs[501] = seqs[501], seqs[500]
+    bad = seq_batch(rng, seqs)
+    good = seq_batch(rng, range(2000, 3000))
+    tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+    P.prof_enable(True)
+    try:
+        P.prof_read()
+        v0, r0 = P.counter("prof_voided"), P.counter("rejects")
+        run_chain(torch, roundtrip_calls(torch, [tx], [rx], bad)[:1],
+                  "async")
+        prof = P.prof_read_named()
+        assert P.counter("rejects") > r0
+        assert P.counter("prof_voided") > v0
+        assert not any(v[3].startswith("k_ctr_fast_any")
+                       for v in prof.values()), prof
+        # the host completed that call: its kernels did the 1000 packets
+        assert sum(v[2] for v in prof.values()) >= 1000
+        v1 = P.counter("prof_voided")
+        run_chain(torch, roundtrip_calls(torch, [tx], [rx], good)[:1],
+                  "async")
+        prof = P.prof_read_named()
+        lean = [v for v in prof.values()
+                if v[3].startswith("k_ctr_fast_any")]
+        assert len(lean) == 1 and lean[0][1] == 1 and lean[0][2] == 1000, \
+            prof
+        assert P.counter("prof_voided") == v1
+    finally:
+        P.prof_enable(False)
+        tx.close()
+        rx.close()

@@ -91,3 +91,130 @@ def test_failed_growth_leaves_windows(torch_cuda, op):
         seen.add(_in_thread(body))
     import errno
     assert errno.ENOMEM in seen       # some growth was hit
+
+
+def _windows_dev(torch, pos, end, cap):
+    return [torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32)
+                             .view(np.int32)).cuda() for a in (pos, end, cap)]
+
+
+def _scenario(torch, keys, inject):
+    """alloc, host-window multi-session protect + unprotect, an async
+    device-window call, per-packet srtp/srtcp calls, free.  inject(step)
+    arms the fault before each step; a step that fails must return ENOMEM,
+    change nothing the caller sees, and succeed when re-run without it.
+    Returns (outputs, steps that failed)."""
+    import errno
+    failed = []
+    out = []
+
+    def step(name, fn, snap=None, restore=None):
+        inject()
+        try:
+            r = fn()
+        finally:
+            P.lib().srtp_gpu_tune(b"fail_alloc", 0)
+        rc = r[0] if isinstance(r, tuple) else r
+        if rc:
+            assert rc == errno.ENOMEM, (name, rc)
+            if snap is not None:
+                assert snap(), name                  # nothing changed
+            failed.append(name)
+            if restore is not None:
+                restore()
+            r = fn()
+            rc = r[0] if isinstance(r, tuple) else r
+            assert rc == 0, (name, "re-run", rc)
+        return r
+
+    nsess = 4
+    ctx = step("alloc_many", lambda: P.alloc_many(nsess, 1, keys[0]))[1]
+    rxc = step("alloc_many_rx", lambda: P.alloc_many(nsess, 1, keys[0]))[1]
+    n = 256
+    s = np.arange(n, dtype=np.uint32) % nsess
+    a, p, q, c = W.make_arena(n, 300, sess=s)
+    d = torch.from_numpy(a).cuda()
+    p0, q0 = p.copy(), q.copy()
+    h0 = d.cpu()
+
+    def same_windows():
+        return np.array_equal(p, p0) and np.array_equal(q, q0) and \
+            torch.equal(d.cpu(), h0)
+    for op, sess in (("srtp_encrypt", ctx), ("srtp_decrypt", rxc)):
+        p0, q0, h0 = p.copy(), q.copy(), d.cpu()
+        rc, err = step(op + "_batch",
+                       lambda: P.device_batch(op, sess, d.data_ptr(),
+                                              d.numel(), p, q, c, s),
+                       same_windows)
+        assert not err.any(), op
+    out += [d.cpu().numpy().tobytes(), q.copy()]
+
+    # asynchronous device-window call on one session
+    m = 64
+    a2, p2, q2, c2 = W.make_arena(m, 1200)
+    d2 = torch.from_numpy(a2).cuda()
+    pd, qd, cd = _windows_dev(torch, p2, q2, c2)
+    ed = torch.full((m,), -1, dtype=torch.int32, device="cuda")
+    h2 = d2.cpu()
+    tx1 = step("alloc", lambda: P.alloc_many(1, 1, keys[1]))[1]
+
+    def async_call():
+        rc, t, keep = P.device_batch_dev_async(
+            "srtp_encrypt", tx1, d2.data_ptr(), d2.numel(), pd.data_ptr(),
+            qd.data_ptr(), cd.data_ptr(), ed.data_ptr(), m)
+        if rc:
+            return rc
+        return P.batch_wait(t)
+
+    def async_same():
+        torch.cuda.synchronize()
+        return torch.equal(d2.cpu(), h2) and \
+            np.array_equal(qd.cpu().numpy().view(np.uint32), q2)
+    step("encrypt_batch_dev_async", async_call, async_same)
+    torch.cuda.synchronize()
+    out += [d2.cpu().numpy().tobytes(), qd.cpu().numpy().tobytes(),
+            ed.cpu().numpy().tobytes()]
+
+    # per-packet calls (the unchanged reference API)
+    pkt = bytes([0x80, 0, 0x12, 0x34]) + bytes(4) + \
+        (0xCAFE).to_bytes(4, "big") + bytes(range(200))
+    for op in ("encrypt", "rtcp_encrypt"):
+        mb = P.new_mbuf(pkt, 512)
+
+        def same_mb(mb=mb):
+            return P.mbuf_bytes(mb) == pkt and mb.contents.pos == 0
+        step(op, lambda mb=mb, op=op: getattr(tx1[0], op)(mb), same_mb)
+        out.append(P.mbuf_bytes(mb))
+        P.free_mbuf(mb)
+    for x in ctx + rxc + tx1:
+        x.close()
+    return out, failed
+
+
+def test_allocation_failure_sweep(torch_cuda):
+    """the reference's `retest -o` (test/test.c:468-560) over this
+    library: for k = 1, 2, ... the k-th allocation from the start of each
+    step fails (srtp_gpu_tune "fail_alloc", every host and device
+    allocation site of the host C, src/host/fault.h).  Each failing step
+    returns ENOMEM with the caller's arena, windows and mbuf unchanged and
+    goes through when re-run; the outputs equal a run without faults, and
+    no mem block or device session slot leaks."""
+    torch = torch_cuda
+    keys = [W.make_keys(4, 30).tobytes(), W.make_keys(1, 30, seed=7).tobytes()]
+    want, f0 = _in_thread(lambda: _scenario(torch, keys, lambda: None))
+    assert not f0
+    mem0, slots0 = P.counter("mem_live"), P.counter("slots_live")
+    hit = set()
+    for k in range(1, 40):
+        def inject(k=k):
+            P.lib().srtp_gpu_tune(b"fail_alloc", k)
+        got, failed = _in_thread(lambda: _scenario(torch, keys, inject))
+        assert got == want, (k, failed)
+        hit |= set(failed)
+        assert P.counter("mem_live") == mem0, k
+        assert P.counter("slots_live") == slots0, k
+        if not failed:
+            break
+    # every kind of step met an allocation failure at some k
+    assert {"alloc_many", "srtp_encrypt_batch", "srtp_decrypt_batch",
+            "encrypt_batch_dev_async", "encrypt"} <= hit, hit

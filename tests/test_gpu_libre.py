@@ -14,7 +14,11 @@ oracle/ref_digest.c):
   * those datagrams received through udp_read(): the socket's handler gets
     every plaintext in order at the reference's pos/end, a replayed and a
     forged datagram are dropped (EALREADY / EAUTH), and the receiver state
-    is the reference's.
+    is the reference's;
+  * rtcp-mux (RTP and RTCP on one socket, libre's src/rtp/rtp.c:184-196):
+    the RTCP datagrams take the SRTCP transform in datagram order -- the
+    wire equals the oracle's srtp_encrypt / srtcp_encrypt sequence, and the
+    handler gets every plaintext back in order.
 """
 import hashlib
 import json
@@ -70,3 +74,20 @@ def test_libre_helper_chain_vs_reference():
     st = F.state_bytes([tuple(out["rx_state"])])
     assert hashlib.sha256(st).hexdigest() == ref["unprotect"]["states"]
     assert out["stats"] == [n + 1, n - 1, n, 2]
+
+    # rtcp-mux: the oracle's per-packet sequence on one context pair
+    from tests import oracle_lib as O
+    from tests.libre_udp_driver import mux_packets
+    mux = mux_packets(arena, pos, end)
+    ob = O.OracleBackend()
+    otx = ob.alloc(1, W.CONFIG1_KEY, 0)[0]
+    wire2 = [bytes.fromhex(w) for w in out["mux_wire"]]
+    assert len(wire2) == len(mux)
+    for i, (pkt, w) in enumerate(zip(mux, wire2)):
+        op = "srtcp_encrypt" if i % 10 == 9 else "srtp_encrypt"
+        e, _, en, _, buf = ob.call(otx, op, 256, 0, len(pkt), pkt,
+                                   len(pkt) + 20)
+        assert e == 0 and buf[:en] == w, (i, op)
+    got2 = out["mux_got"]
+    assert [(p, e, bytes.fromhex(b)) for p, e, b in got2] == \
+        [(0, len(m), m) for m in mux]

@@ -39,8 +39,9 @@ def i32(torch, a):
         np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).cuda()
 
 
-def run(torch, op, ctx, dev, pos, end, cap, a, b):
-    """srtp_*_batch_dev over packets [a, b) of the arena"""
+def run(torch, op, ctx, dev, pos, end, cap, a, b, pos_out=None):
+    """srtp_*_batch_dev over packets [a, b) of the arena (the windows
+    after the call: end in place, pos into pos_out)"""
     n = b - a
     pos_d, end_d, cap_d = i32(torch, pos[a:b]), i32(torch, end[a:b]), \
         i32(torch, cap[a:b])
@@ -52,6 +53,8 @@ def run(torch, op, ctx, dev, pos, end, cap, a, b):
     assert rc == 0, (rc, P.lib().srtp_gpu_error())
     torch.cuda.synchronize()
     end[a:b] = end_d.cpu().numpy().view(np.uint32)
+    if pos_out is not None:
+        pos_out[a:b] = pos_d.cpu().numpy().view(np.uint32)
     return err.cpu().numpy()
 
 
@@ -218,7 +221,9 @@ def test_split_stream_fold_on_device_results(torch_cuda):
     buf, pos, end, cap = arena_dev(pkts, 0)
     one = torch.from_numpy(buf).cuda()
     rx = P.Srtp(suite, key)
-    e1 = run(torch, "srtp_decrypt", rx, one, pos, end.copy(), cap, 0, n)
+    pos1 = pos.copy()
+    end1 = end.copy()
+    e1 = run(torch, "srtp_decrypt", rx, one, pos, end1, cap, 0, n, pos1)
     assert (e1 == truth).all()
     e, so = rx.export(X.SSRC)
     assert e == 0
@@ -226,9 +231,11 @@ def test_split_stream_fold_on_device_results(torch_cuda):
               so.replay_rtp_bitmap)
     rx.close()
 
-    # two shards on the GPU, then the fold
+    # two shards on the GPU, then the fold; a voided tail re-runs from the
+    # fold's state on its received bytes (what the rank holding it does)
     two = torch.from_numpy(buf).cuda()
     end2 = end.copy()
+    pos2 = pos.copy()
     guess = X.assumed_boundary(pkts[:b])
     recs = []
     for r, (a, z) in enumerate(((0, b), (b, n))):
@@ -236,14 +243,40 @@ def test_split_stream_fold_on_device_results(torch_cuda):
         st0 = X.state(*guess) if r else X.state()
         if r:
             assert c.import_(st0) == 0
-        res = run(torch, "srtp_decrypt", c, two, pos, end2, cap, a, z)
+        res = run(torch, "srtp_decrypt", c, two, pos, end2, cap, a, z, pos2)
         recs.append(S.rx_records(st0, buf, pos[a:z], end[a:z], res))
         c.close()
     rec = np.concatenate(recs)
     assert (rec["res"] != truth).any()     # the ranks alone disagree
     st = X.state()
-    err, nd = S.rx_fold(st, suite, rec)
-    assert nd == n and (err == truth).all()
+    done, reruns, errs = 0, 0, []
+    while True:
+        err, nd = S.rx_fold(st, suite, rec[done:])
+        errs.append(err)
+        done += nd
+        if done == n:
+            break
+        reruns += 1
+        assert reruns <= 4
+        lo, hi = int(pos[done]), int(cap[n - 1])
+        two[lo:hi] = torch.from_numpy(buf[lo:hi]).cuda()
+        end2[done:] = end[done:]
+        st0 = X.state(st.roc, st.s_l, st.s_l_set, st.replay_rtp_lix,
+                      st.replay_rtp_bitmap)
+        c = P.Srtp(suite, key)
+        assert c.import_(st0) == 0
+        res = run(torch, "srtp_decrypt", c, two, pos, end2, cap, done, n,
+                  pos2)
+        c.close()
+        rec = np.concatenate([rec[:done],
+                              S.rx_records(st0, buf, pos[done:], end[done:],
+                                           res)])
+    # the late packet the rank rejected as a replay is accepted by the one
+    # receiver: its bytes were voided and re-run
+    assert reruns >= 1
+    assert (np.concatenate(errs) == truth).all()
     assert (st.roc, st.s_l, st.s_l_set, st.replay_rtp_lix,
             st.replay_rtp_bitmap) == st_one
     assert (st.roc, st.s_l, st.replay_rtp_lix, st.replay_rtp_bitmap) == fin
+    assert (end2 == end1).all() and (pos2 == pos1).all()
+    assert torch.equal(two, one)

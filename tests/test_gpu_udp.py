@@ -209,3 +209,68 @@ def test_udp_send_checks_every_mbuf_first(torch_cuda):
     su.close()
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_udp_receive_failure_delivers_each_datagram_once(torch_cuda,
+                                                         pipeline):
+    """a batch whose GPU issue or completion fails (allocation failure
+    injected, srtp_gpu_tune "fail_alloc") still reaches the handler, once,
+    with the errno; the batch in flight before it is completed and
+    delivered first, and later batches run normally"""
+    import errno
+    key = W.CONFIG1_KEY
+    arena, pos, end, cap, _, _ = W.build_config(1, n=192)
+    ob = O.OracleBackend()
+    otx = ob.alloc(1, key, 0)[0]
+    wire = []
+    for i in range(192):
+        p = arena[pos[i]:end[i]].tobytes()
+        e, _, en, _, buf = ob.call(otx, "srtp_encrypt", 256, 0, len(p), p,
+                                   len(p) + 16)
+        wire.append(buf[:en])
+    a, b = udp_pair()
+    for k in range(1, 30):
+        got = []
+
+        def handler(src, mb, err):
+            got.append((slot_view(mb, err)[0], bytes(src)))
+
+        rx = P.Srtp(1, key)
+        sr = P.SrtpUdp(b.fileno(), rx=rx, batch=64, slot=256,
+                       handler=handler, pipeline=pipeline)
+        assert sr.err == 0
+        for d in wire[:64]:
+            a.sendto(d, b.getsockname())
+        rets = [sr.recv(200)]
+        for d in wire[64:128]:
+            a.sendto(d, b.getsockname())
+        P.lib().srtp_gpu_tune(b"fail_alloc", k)
+        try:
+            rets.append(sr.recv(200))
+        finally:
+            left = P.counter("fail_alloc")
+            P.lib().srtp_gpu_tune(b"fail_alloc", 0)
+        for d in wire[128:]:
+            a.sendto(d, b.getsockname())
+        for _ in range(100):
+            if len(got) >= 192:
+                break
+            rets.append(sr.recv(200))
+        errs = [g[0] for g in got]
+        assert len(got) == 192, (k, len(got), rets)
+        assert sr.stats()[0] == 192
+        sr.close()
+        rx.close()
+        if left:                      # the fault was never reached
+            assert errs == [0] * 192 and min(rets) >= 0
+            continue
+        assert min(rets) == -errno.ENOMEM, (k, rets)
+        # batch 0 authentic; batch 1 failed as a whole; batch 2 authentic
+        assert errs[:64] == [0] * 64 and errs[128:] == [0] * 64, k
+        assert errs[64:128] == [errno.ENOMEM] * 64, (k, errs[64:128])
+        break
+    else:
+        raise AssertionError("no allocation fault reached")
+    a.close()
+    b.close()

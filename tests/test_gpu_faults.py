@@ -147,7 +147,7 @@ def _scenario(torch, keys, inject):
                                               d.numel(), p, q, c, s),
                        same_windows)
         assert not err.any(), op
-    out += [d.cpu().numpy().tobytes(), q.copy()]
+    out += [d.cpu().numpy().tobytes(), q.tobytes()]
 
     # asynchronous device-window call on one session
     m = 64

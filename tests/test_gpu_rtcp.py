@@ -388,6 +388,7 @@ def test_rtcp_report_round_trip(torch_cuda):
     msg["count"][0::2] = 1
     msg["count"][1::2] = 1
     w = rng.integers(0, 2**32, (n, 6), dtype=np.uint64).astype(np.uint32)
+    w[:, 0] = 0x5EED0001        # one sender: the session's one SSRC
     msg["w"][0::2] = w
     msg["first"][0::2] = np.arange(n)
     msg["num"][0::2] = 1
@@ -415,7 +416,8 @@ def test_rtcp_report_round_trip(torch_cuda):
     pos = np.arange(n, dtype=np.uint32) * slot
     arena, end, err = encode_dev(torch, A, pos, pos + slot, n * slot)
     assert not err.any()
-    L = 4 + 24 + 24 + ((4 + 4 + 2 + cname_len + 1 + 3) & ~3)
+    cl = cname_len.astype(np.int64)
+    L = 4 + 24 + 24 + ((4 + 4 + 2 + cl + 1 + 3) & ~3)
     assert (end - pos == L).all()
     # SRTCP protect + unprotect in place
     key = bytes(range(30))

@@ -188,6 +188,19 @@ int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
 		  const int32_t *res, size_t n, struct srtp_rx_rec *rec);
 
 /**
+ * The same for a rank whose arena, windows and results (the
+ * srtp_decrypt_batch_dev outputs) are DEVICE memory: the headers are
+ * parsed on the device and 16 bytes per packet come down, the arena does
+ * not; rec is host memory.  Queued on stream (hipStream_t, NULL: default)
+ * and synchronised.  0 or EINVAL / ENOMEM / EIO / ENOSYS.
+ */
+int srtp_rx_index_dev(const struct srtp_stream_state *st0,
+		      const uint8_t *arena, size_t arena_size,
+		      const uint32_t *pos, const uint32_t *end,
+		      const int32_t *res, size_t n, struct srtp_rx_rec *rec,
+		      void *stream);
+
+/**
  * Fold the gathered records of the whole stream from *st (the true state
  * before packet 0): err[i] = the reference receiver's result.  Stops at
  * the first packet whose true index differs from the one its rank

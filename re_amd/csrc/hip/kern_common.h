@@ -720,6 +720,13 @@ __device__ __forceinline__ void store_region(uint8_t *pkt, uint32_t c0,
 
 typedef void (*kfn_t)(const KArgs);
 
+/* small.hip: the per-packet path's fused kernel over (mapped) memory */
+#define SGPU_SMALL_MAX_BYTES 2048
+int small_launch(uint8_t *arena, uint64_t arena_size,
+		 const struct sgpu_job *jobs, uint32_t njobs, uint8_t *verdict,
+		 uint32_t *save, const struct sgpu_comp *comps,
+		 const uint32_t *t0, int prot, void *stream);
+
 /* kernel pickers, one per translation unit */
 unsigned sgpu_ctr_block(bool uni, int prot);
 kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);

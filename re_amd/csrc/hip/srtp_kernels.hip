@@ -1245,6 +1245,17 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 	return e;
 }
 
+/* the per-packet path's fused kernel over pinned host memory (small.hip) */
+extern "C" int sgpu_run_small(uint8_t *arena, uint64_t arena_size,
+			      const struct sgpu_job *jobs, uint32_t njobs,
+			      uint8_t *verdict, uint32_t *save, int prot,
+			      void *stream)
+{
+	return small_launch(arena, arena_size, jobs, njobs, verdict, save,
+			    (const struct sgpu_comp *)g_table, g_T0_dev, prot,
+			    stream);
+}
+
 /* srtp_gpu_tune nocoop (A/B): small general launches fused as usual */
 extern "C" void sgpu_set_coop(int on)
 {

@@ -149,6 +149,9 @@ static struct {
 				   group by the radix sort (not counting) */
 	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
 				   device-planned batch fold on the host */
+	int nosmall;            /* RE_SRTP_NOSMALL: the per-packet path's small
+				   CTR launches take the general kernels
+				   with copies (not sgpu_run_small) */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
 	int times;              /* RE_SRTP_TIMES: multi-session phases */
 	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
@@ -166,6 +169,7 @@ static void env_read(void)
 	g_env.nolean = getenv("RE_SRTP_NOLEAN") != NULL;
 	g_env.nodevfold = getenv("RE_SRTP_NODEVFOLD") != NULL;
 	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
+	g_env.nosmall = getenv("RE_SRTP_NOSMALL") != NULL;
 	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
 	if (getenv("RE_SRTP_NOCOOP"))
 		sgpu_set_coop(0);
@@ -265,6 +269,8 @@ int srtp_gpu_tune(const char *name, long value)
 		sgpu_set_coop(value <= 0);
 	else if (!strcmp(name, "nocombine"))
 		g_env.nocombine = value > 0;
+	else if (!strcmp(name, "nosmall"))
+		g_env.nosmall = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -1503,6 +1509,64 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 	}
 }
 
+/*
+ * The per-packet path's round (few packets, CTR + HMAC-SHA1 suites): the
+ * staged packets and the jobs stay in pinned host memory and one fused
+ * kernel reads and writes them there (sgpu_run_small, small.hip) -- no
+ * copies; the verdicts land where round_collect reads them.  0 with *pm
+ * jobs, errno, or -1: not eligible (a GCM job, a packet past
+ * SGPU_SMALL_MAX, more than SGPU_COOP_MAX jobs) -- nothing launched.
+ */
+static int round_small(struct ws *w, struct engine *E, uint64_t asz,
+		       const uint32_t *joff, int prot, uint32_t *pm,
+		       void *stream)
+{
+	struct sgpu_job *jh;
+	uint8_t *vh;
+	size_t i, need = 0;
+	uint32_t m = 0;
+	int err;
+
+	*pm = 0;
+	if (g_env.nosmall)
+		return -1;
+	for (i = 0; i < E->n; i++) {
+		const struct rec *r = &E->rec[i];
+		if (!r->need_run)
+			continue;
+		if ((r->job.flags & (SJ_GCM | SJ_UNDO)) ||
+		    r->ext_end - E->pi[i].start > SGPU_SMALL_MAX ||
+		    r->in_end - E->pi[i].start > SGPU_SMALL_MAX)
+			return -1;
+		need++;
+	}
+	if (!need)
+		return 0;
+	if (need > SGPU_COOP_MAX)
+		return -1;
+	err = pool_reserve(w, &w->ctl, need * (sizeof(struct sgpu_job) + 5));
+	if (!err)
+		err = idx_reserve(w, need);
+	if (err)
+		return err;
+	jh = (struct sgpu_job *)w->ctl.h;
+	for (i = 0; i < E->n; i++) {
+		const struct rec *r = &E->rec[i];
+		if (!r->need_run)
+			continue;
+		jh[m] = r->job;
+		jh[m].off = joff[i];
+		w->cls_idx[m] = (uint32_t)i;
+		m++;
+	}
+	vh = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
+	err = sgpu_run_small(w->stage.h, asz, jh, m, vh, (uint32_t *)(vh + m),
+			     prot, stream);
+	if (!err)
+		*pm = m;
+	return err;
+}
+
 /* ---- host-resident front-end (mbufs) -------------------------------- */
 
 /*
@@ -1677,6 +1741,25 @@ static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 			memcpy(w->stage.h + soff[i], mbv[i]->buf + E.pi[i].start,
 			       r->in_end - E.pi[i].start);
 		}
+		{
+			/* few packets of the CTR suites: the fused kernel over
+			 * the pinned staging memory itself */
+			int rs;
+			for (i = 0; i < n; i++)
+				if (E.rec[i].need_run)
+					E.rec[i].job.off = E.pi[i].start;
+			rs = round_small(w, &E, bytes, soff, prot, &m, w->stream);
+			if (rs >= 0) {
+				err = rs ? rs : sgpu_stream_sync(w->stream);
+				if (err)
+					goto out;
+				round_collect(w, &E, m);
+				for (i = 0; i < n; i++)
+					if (E.rec[i].need_run)
+						outp[i] = w->stage.h + soff[i];
+				continue;
+			}
+		}
 		err = sgpu_memcpy_h2d(w->stage.d, w->stage.h, bytes, w->stream);
 		if (!err) {
 			/* job offsets are relative to the packet start */
@@ -1756,25 +1839,57 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
  * share GPU launches: a calling thread queues its packet; if no thread is
  * running a batch it becomes the runner, takes everything queued (the
  * packets of other threads that arrived meanwhile) and runs it as one
- * multi-session batch per operation, then wakes their callers.  No timer
- * and no waiting at low load: a lone caller runs its packet at once.  A
- * struct srtp is used by one thread at a time (the reference's contract),
- * so the packets of one batch belong to distinct sessions, and each
- * thread's calls stay in its own order.
+ * multi-session batch per operation.  No timer and no waiting at low
+ * load: a lone caller runs its packet at once.  A struct srtp is used by
+ * one thread at a time (the reference's contract), so the packets of one
+ * batch belong to distinct sessions, and each thread's calls stay in its
+ * own order.
+ *
+ * Completion is per request: the runner marks each request done and wakes
+ * only its owner (a futex on the request's state word; owners spin
+ * briefly first), then hands the runner role to the owner of the first
+ * request queued meanwhile -- no broadcast, so 64 callers do not convoy
+ * through one mutex on every batch.
  */
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+enum { PC_QUEUED = 0, PC_DONE = 1, PC_RUN = 2 };
+
 struct pc_req {
 	struct pc_req *next;
 	int op;
 	struct srtp *s;
 	struct mbuf *mb;
 	int err;
-	int done;
+	int state;              /* PC_*, atomic: the owner waits on it */
 };
 
 static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t pc_cond = PTHREAD_COND_INITIALIZER;
 static struct pc_req *pc_head, *pc_tail;
 static int pc_running;
+
+static void pc_wake(int *state, int v)
+{
+	__atomic_store_n(state, v, __ATOMIC_RELEASE);
+	(void)syscall(SYS_futex, state, FUTEX_WAKE_PRIVATE, 1, NULL, NULL, 0);
+}
+
+static int pc_wait(const int *state)
+{
+	int spin, v;
+	for (spin = 0; spin < 2000; spin++) {
+		v = __atomic_load_n(state, __ATOMIC_ACQUIRE);
+		if (v != PC_QUEUED)
+			return v;
+		__builtin_ia32_pause();
+	}
+	while ((v = __atomic_load_n(state, __ATOMIC_ACQUIRE)) == PC_QUEUED)
+		(void)syscall(SYS_futex, state, FUTEX_WAIT_PRIVATE, PC_QUEUED,
+			      NULL, NULL, 0);
+	return v;
+}
 
 static void pc_run(struct pc_req *list)
 {
@@ -1823,7 +1938,7 @@ static void pc_run(struct pc_req *list)
 static int one(int op, struct srtp *srtp, struct mbuf *mb)
 {
 	struct pc_req req;
-	int e = 0, err;
+	int e = 0, err, run;
 
 	if (!srtp || !mb)
 		return EINVAL;
@@ -1843,25 +1958,33 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 	else
 		pc_head = &req;
 	pc_tail = &req;
-	while (!req.done) {
-		if (!pc_running) {
-			struct pc_req *list = pc_head, *r, *nx;
-			pc_head = pc_tail = NULL;
-			pc_running = 1;
-			pthread_mutex_unlock(&pc_lock);
-			pc_run(list);
-			pthread_mutex_lock(&pc_lock);
-			for (r = list; r; r = nx) {
-				nx = r->next;
-				r->done = 1;    /* r may be gone once woken */
-			}
-			pc_running = 0;
-			pthread_cond_broadcast(&pc_cond);
-			continue;
-		}
-		pthread_cond_wait(&pc_cond, &pc_lock);
-	}
+	run = !pc_running;
+	pc_running = 1;
 	pthread_mutex_unlock(&pc_lock);
+	if (!run && pc_wait(&req.state) == PC_DONE)
+		return req.err;
+	/* the runner: everything queued so far, then the role to the first
+	 * request queued meanwhile (or none) */
+	{
+		struct pc_req *list, *r, *nx, *next_runner;
+		pthread_mutex_lock(&pc_lock);
+		list = pc_head;
+		pc_head = pc_tail = NULL;
+		pthread_mutex_unlock(&pc_lock);
+		pc_run(list);
+		for (r = list; r; r = nx) {
+			nx = r->next;   /* r may be gone once woken */
+			if (r != &req)
+				pc_wake(&r->state, PC_DONE);
+		}
+		pthread_mutex_lock(&pc_lock);
+		next_runner = pc_head;
+		if (!next_runner)
+			pc_running = 0;
+		pthread_mutex_unlock(&pc_lock);
+		if (next_runner)
+			pc_wake(&next_runner->state, PC_RUN);
+	}
 	return req.err;
 }
 
@@ -4693,57 +4816,126 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 
 /* ---- cross-rank replay fold (include/re_srtp_batch.h) ----------------- */
 
+/* the rank's own receiver over one packet (srtp.c:310-321 + the s_l
+ * update of :426-427); ok: rtp_hdr_decode succeeded.  0 or EINVAL (another
+ * SSRC) */
+struct rx_walk {
+	uint32_t ssrc, roc;
+	uint16_t s_l;
+	uint8_t set;
+};
+
+static int rx_step(struct rx_walk *x, int ok, uint32_t ssrc, uint16_t seq,
+		   int32_t res, struct srtp_rx_rec *r)
+{
+	int diff;
+	memset(r, 0, sizeof(*r));
+	r->res = res;
+	if (!ok) {
+		r->stage = SRTP_RX_NOHDR;
+		return 0;
+	}
+	if (ssrc != x->ssrc)
+		return EINVAL;
+	r->seq = seq;
+	if (!x->set) {
+		x->s_l = seq;
+		x->set = 1;
+	}
+	diff = (int)seq - (int)x->s_l;
+	if (diff > 32768) {
+		r->stage = SRTP_RX_NOIX;
+		return 0;
+	}
+	if (diff <= -32768) {
+		x->roc++;
+		x->s_l = 0;
+	}
+	r->stage = SRTP_RX_IX;
+	r->ix = get_index(x->roc, x->s_l, seq);
+	if (res == 0 && seq > x->s_l)
+		x->s_l = seq;
+	return 0;
+}
+
 int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
 		  const uint32_t *pos, const uint32_t *end,
 		  const int32_t *res, size_t n, struct srtp_rx_rec *rec)
 {
-	uint32_t roc;
-	uint16_t s_l;
-	uint8_t set;
+	struct rx_walk x;
 	size_t i;
 
 	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)))
 		return EINVAL;
-	roc = st0->roc;
-	s_l = st0->s_l;
-	set = st0->s_l_set;
+	x.ssrc = st0->ssrc;
+	x.roc = st0->roc;
+	x.s_l = st0->s_l;
+	x.set = st0->s_l_set;
 	for (i = 0; i < n; i++) {
-		struct srtp_rx_rec *r = &rec[i];
 		struct pinfo pi;
-		int diff;
-
-		memset(r, 0, sizeof(*r));
 		memset(&pi, 0, sizeof(pi));
-		r->res = res[i];
 		pi.start = pos[i];
 		pi.end = end[i];
 		parse_rtp(&pi, arena);
-		if (pi.hdr_len == UINT32_MAX) {
-			r->stage = SRTP_RX_NOHDR;
-			continue;
-		}
-		if (pi.ssrc != st0->ssrc)
+		if (rx_step(&x, pi.hdr_len != UINT32_MAX, pi.ssrc, pi.seq,
+			    res[i], &rec[i]))
 			return EINVAL;
-		r->seq = pi.seq;
-		/* the rank's own receiver, step by step (srtp.c:310-321) */
-		if (!set) {
-			s_l = pi.seq;
-			set = 1;
-		}
-		diff = (int)pi.seq - (int)s_l;
-		if (diff > 32768) {
-			r->stage = SRTP_RX_NOIX;
-			continue;
-		}
-		if (diff <= -32768) {
-			roc++;
-			s_l = 0;
-		}
-		r->stage = SRTP_RX_IX;
-		r->ix = get_index(roc, s_l, pi.seq);
-		if (res[i] == 0 && pi.seq > s_l)
-			s_l = pi.seq;
 	}
+	return 0;
+}
+
+int srtp_rx_index_dev(const struct srtp_stream_state *st0,
+		      const uint8_t *arena, size_t arena_size,
+		      const uint32_t *pos, const uint32_t *end,
+		      const int32_t *res, size_t n, struct srtp_rx_rec *rec,
+		      void *stream)
+{
+	const struct sgpu_hdr *hh;
+	const int32_t *rh;
+	struct rx_walk x;
+	struct ws *w;
+	size_t i;
+	int err;
+
+	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)) ||
+	    n > UINT32_MAX)
+		return EINVAL;
+	if (!n)
+		return 0;
+	if (!gpu_ready())
+		return ENOSYS;
+	w = ws_get();
+	if (!w)
+		return ENOMEM;
+	/* the headers parsed where the packets lie (k_parse: rtp_hdr_decode,
+	 * rtp.c:88-137), 12 B per packet down with the results: the arena
+	 * stays on the device */
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = sgpu_parse_headers(arena, arena_size, pos, end,
+					 (struct sgpu_hdr *)w->hd.d, NULL,
+					 (uint32_t)n, 0, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(w->hd.h, w->hd.d,
+				      n * sizeof(struct sgpu_hdr), stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(w->es.h, res, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	hh = (const struct sgpu_hdr *)w->hd.h;
+	rh = (const int32_t *)w->es.h;
+	x.ssrc = st0->ssrc;
+	x.roc = st0->roc;
+	x.s_l = st0->s_l;
+	x.set = st0->s_l_set;
+	for (i = 0; i < n; i++)
+		if (rx_step(&x, hh[i].hdr_len != UINT32_MAX, hh[i].ssrc,
+			    hh[i].seq, rh[i], &rec[i]))
+			return EINVAL;
 	return 0;
 }
 

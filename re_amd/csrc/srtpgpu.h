@@ -114,6 +114,14 @@ uint64_t sgpu_table_device_ptr(void);
 				   run their cipher regions one packet per
 				   workgroup (k_ctr_coop, k_gcm_coop) */
 void  sgpu_set_coop(int on);
+/* the per-packet path (few packets, CTR + HMAC-SHA1 suites): one fused
+ * kernel, one packet per workgroup, over jobs, packets, verdicts and saved
+ * words in PINNED HOST memory (sgpu_host_alloc: device-accessible), no
+ * copies; packets of at most SGPU_SMALL_MAX bytes from their start */
+#define SGPU_SMALL_MAX 2048
+int   sgpu_run_small(uint8_t *arena, uint64_t arena_size,
+		     const struct sgpu_job *jobs, uint32_t njobs,
+		     uint8_t *verdict, uint32_t *save, int prot, void *stream);
 int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,
 		     uint8_t *verdict, uint32_t *save, int mode, int nr,

@@ -135,6 +135,26 @@ def rx_records(st0, arena, pos, end, res):
     return rec
 
 
+def rx_records_dev(st0, arena, pos, end, res, stream=None):
+    """the rank's records from its DEVICE outputs (srtp_rx_index_dev): arena
+    a torch uint8 CUDA tensor, pos/end/res int32 CUDA tensors of the rank's
+    srtp_decrypt_batch_dev call (the arena never leaves the device)"""
+    import ctypes
+    import numpy as np
+    from . import srtp as S
+    n = int(pos.numel())
+    if int(end.numel()) != n or int(res.numel()) != n:
+        raise ValueError("rx_records_dev: pos, end and res differ in length")
+    rec = np.zeros(n, dtype=_rx_rec_dtype())
+    e = S.lib().srtp_rx_index_dev(ctypes.byref(st0), arena.data_ptr(),
+                                  arena.numel(), pos.data_ptr(),
+                                  end.data_ptr(), res.data_ptr(), n,
+                                  rec.ctypes.data, stream)
+    if e:
+        raise OSError(e, "srtp_rx_index_dev")
+    return rec
+
+
 def rx_fold(st, suite, rec):
     """fold the whole stream's records from StreamState st (the true state
     before its first packet; updated in place).  Returns (err int32 array

@@ -171,6 +171,8 @@ def load():
                                   ctypes.c_char_p, sz, ctypes.c_int]
     L.srtp_rx_index.argtypes = [ctypes.POINTER(StreamState), vp, vp, vp, vp,
                                 sz, vp]
+    L.srtp_rx_index_dev.argtypes = [ctypes.POINTER(StreamState), vp, sz, vp,
+                                    vp, vp, sz, vp, vp]
     L.srtp_rx_fold.argtypes = [ctypes.POINTER(StreamState), ctypes.c_int, vp,
                                sz, vp, ctypes.POINTER(sz)]
     L.srtp_gpu_prof.argtypes = [ctypes.c_int]

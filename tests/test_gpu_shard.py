@@ -245,6 +245,12 @@ def test_split_stream_fold_on_device_results(torch_cuda):
             assert c.import_(st0) == 0
         res = run(torch, "srtp_decrypt", c, two, pos, end2, cap, a, z, pos2)
         recs.append(S.rx_records(st0, buf, pos[a:z], end[a:z], res))
+        # the same records from the device outputs (the arena stays there)
+        dv = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(
+            np.int32)).cuda()
+        recd = S.rx_records_dev(st0, two, dv(pos[a:z]), dv(end[a:z]),
+                                dv(res))
+        assert (recd == recs[-1]).all(), r
         c.close()
     rec = np.concatenate(recs)
     assert (rec["res"] != truth).any()     # the ranks alone disagree

@@ -1891,47 +1891,122 @@ static int pc_wait(const int *state)
 	return v;
 }
 
-static void pc_run(struct pc_req *list)
+/* one operation's requests of a list, as multi-session batches */
+static void pc_run_op(struct pc_req *list, int op)
 {
 	enum { MAXB = 1024 };
 	struct srtp *sv[MAXB];
 	struct mbuf *mv[MAXB];
 	struct pc_req *rq[MAXB];
 	int ev[MAXB];
-	int op;
+	struct pc_req *r = list;
 
-	for (op = 0; op < 4; op++) {
-		struct pc_req *r = list;
-		while (r) {
-			size_t n = 0, i;
-			int err;
-			for (; r && n < MAXB; r = r->next) {
-				if (r->op != op)
-					continue;
-				rq[n] = r;
-				sv[n] = r->s;
-				mv[n++] = r->mb;
-			}
-			if (!n)
-				break;
-			count(&g_cnt_pcbatch, 1);
-			count(&g_cnt_pcpkts, n);
-			table_rdlock();
-			err = sess_host(sv, n);
-			if (!err) {
-				uint32_t *idx = fi_malloc(n * sizeof(*idx));
-				if (!idx)
-					err = ENOMEM;
-				for (i = 0; !err && i < n; i++)
-					idx[i] = (uint32_t)i;
-				if (!err)
-					err = run_mbufs_(op, sv, n, idx, mv, ev, n);
-				free(idx);
-			}
-			table_unlock();
-			for (i = 0; i < n; i++)
-				rq[i]->err = err ? err : ev[i];
+	while (r) {
+		size_t n = 0, i;
+		int err;
+		for (; r && n < MAXB; r = r->next) {
+			if (r->op != op)
+				continue;
+			rq[n] = r;
+			sv[n] = r->s;
+			mv[n++] = r->mb;
 		}
+		if (!n)
+			break;
+		count(&g_cnt_pcbatch, 1);
+		count(&g_cnt_pcpkts, n);
+		table_rdlock();
+		err = sess_host(sv, n);
+		if (!err) {
+			uint32_t *idx = fi_malloc(n * sizeof(*idx));
+			if (!idx)
+				err = ENOMEM;
+			for (i = 0; !err && i < n; i++)
+				idx[i] = (uint32_t)i;
+			if (!err)
+				err = run_mbufs_(op, sv, n, idx, mv, ev, n);
+			free(idx);
+		}
+		table_unlock();
+		for (i = 0; i < n; i++)
+			rq[i]->err = err ? err : ev[i];
+	}
+}
+
+/*
+ * A list usually mixes operations (callers alternate srtp_encrypt and
+ * srtp_decrypt): each operation is its own batch, and the batches of two
+ * operations run at once -- one on a persistent helper thread (its own
+ * workspace and HIP stream), the rest on the runner -- instead of one
+ * GPU round trip after the other.  The sessions of one list are distinct
+ * (one request per calling thread, one thread per struct srtp), so the
+ * operations share no stream state.
+ */
+static struct {
+	pthread_once_t once;
+	int ok;
+	int state;              /* 0 idle, 1 posted, 2 done (futex word) */
+	struct pc_req *list;
+	int op;
+} pc_h = {PTHREAD_ONCE_INIT, 0, 0, NULL, 0};
+
+static void *pc_helper(void *arg)
+{
+	(void)arg;
+	for (;;) {
+		while (__atomic_load_n(&pc_h.state, __ATOMIC_ACQUIRE) != 1)
+			(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAIT_PRIVATE,
+				      __atomic_load_n(&pc_h.state,
+						      __ATOMIC_RELAXED),
+				      NULL, NULL, 0);
+		pc_run_op(pc_h.list, pc_h.op);
+		__atomic_store_n(&pc_h.state, 2, __ATOMIC_RELEASE);
+		(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAKE_PRIVATE, 1,
+			      NULL, NULL, 0);
+	}
+	return NULL;
+}
+
+static void pc_helper_start(void)
+{
+	pthread_t t;
+	pthread_attr_t a;
+	pthread_attr_init(&a);
+	pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
+	pc_h.ok = pthread_create(&t, &a, pc_helper, NULL) == 0;
+	pthread_attr_destroy(&a);
+}
+
+static void pc_run(struct pc_req *list)
+{
+	unsigned ops = 0;
+	int op, first = -1;
+	struct pc_req *r;
+
+	for (r = list; r; r = r->next)
+		ops |= 1u << r->op;
+	if (ops & (ops - 1)) {
+		pthread_once(&pc_h.once, pc_helper_start);
+		if (pc_h.ok) {
+			/* the lowest operation to the helper (only the
+			 * runner posts: runners are serialised) */
+			first = __builtin_ctz(ops);
+			pc_h.list = list;
+			pc_h.op = first;
+			__atomic_store_n(&pc_h.state, 1, __ATOMIC_RELEASE);
+			(void)syscall(SYS_futex, &pc_h.state,
+				      FUTEX_WAKE_PRIVATE, 1, NULL, NULL, 0);
+		}
+	}
+	for (op = 0; op < 4; op++)
+		if ((ops >> op) & 1 && op != first)
+			pc_run_op(list, op);
+	if (first >= 0) {
+		int v;
+		while ((v = __atomic_load_n(&pc_h.state, __ATOMIC_ACQUIRE)) != 2)
+			(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAIT_PRIVATE,
+				      v, NULL, NULL, 0);
+		__atomic_store_n(&pc_h.state, 0, __ATOMIC_RELAXED);
 	}
 }
 

@@ -136,7 +136,18 @@ int main(int argc, char **argv)
 		struct job w = {200, 99, NULL, NULL, 0, 0, 0};
 		run(&w);
 	}
+	const uint64_t c0 = srtp_gpu_counter("small_launches"),
+		       l0 = srtp_gpu_counter("small_ns_launch"),
+		       s0 = srtp_gpu_counter("small_ns_sync"),
+		       m0 = srtp_gpu_counter("mbufs_ns");
 	run(&j0);
+	const double nl = (double)(srtp_gpu_counter("small_launches") - c0);
+	const double us_launch = nl ? (srtp_gpu_counter("small_ns_launch") -
+				       l0) / nl / 1e3 : 0;
+	const double us_sync = nl ? (srtp_gpu_counter("small_ns_sync") - s0) /
+				    nl / 1e3 : 0;
+	const double us_mbufs = (srtp_gpu_counter("mbufs_ns") - m0) /
+				(2.0 * calls) / 1e3;
 	if (j0.errors) {
 		fprintf(stderr, "percall: %ld errors (%s)\n", j0.errors,
 			srtp_gpu_error());
@@ -148,12 +159,14 @@ int main(int argc, char **argv)
 	       "\"suite\":\"%s\","
 	       "\"encrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
 	       "\"decrypt_us\":{\"p50\":%.2f,\"p99\":%.2f,\"min\":%.2f},"
-	       "\"pairs_per_s_1thread\":%.0f,\"threads\":[",
+	       "\"pairs_per_s_1thread\":%.0f,"
+	       "\"per_call_us\":{\"run_mbufs\":%.2f,\"small_launch\":%.2f,"
+	       "\"small_sync\":%.2f},\"threads\":[",
 	       calls, srtp_suite_name(g_suite),
 	       pct(j0.lat_e, calls, 0.5), pct(j0.lat_e, calls, 0.99),
 	       j0.lat_e[0], pct(j0.lat_d, calls, 0.5),
 	       pct(j0.lat_d, calls, 0.99), j0.lat_d[0],
-	       calls / ((j0.t1 - j0.t0) * 1e-6));
+	       calls / ((j0.t1 - j0.t0) * 1e-6), us_mbufs, us_launch, us_sync);
 	for (a = 2; a < argc; a++) {
 		const int T = atoi(argv[a]);
 		struct job *js = calloc(T, sizeof(*js));
@@ -161,6 +174,8 @@ int main(int argc, char **argv)
 		double t0 = 1e300, t1 = 0;
 		long err = 0;
 		int t;
+		const uint64_t b0 = srtp_gpu_counter("pcbatches"),
+			       p0 = srtp_gpu_counter("pcpackets");
 		for (t = 0; t < T; t++) {
 			js[t].calls = calls / 4 > 1000 ? calls / 4 : 1000;
 			js[t].id = t;
@@ -172,9 +187,11 @@ int main(int argc, char **argv)
 			t1 = js[t].t1 > t1 ? js[t].t1 : t1;
 			err += js[t].errors;
 		}
-		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld}",
+		const double nb = (double)(srtp_gpu_counter("pcbatches") - b0);
+		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld,"
+		       "\"packets_per_launch\":%.1f}",
 		       a > 2 ? "," : "", T, T * js[0].calls / ((t1 - t0) * 1e-6),
-		       err);
+		       err, nb ? (srtp_gpu_counter("pcpackets") - p0) / nb : 0);
 		free(js);
 		free(th);
 	}

@@ -78,7 +78,7 @@ __device__ __forceinline__ void region_ks(const uint32_t *T, const uint32_t *rk,
 					  uint32_t nr, const uint32_t iv[4],
 					  uint32_t c_off, uint32_t c_end,
 					  uint32_t *dst, bool xr, uint32_t b0,
-					  uint32_t step)
+					  uint32_t step, uint32_t *done = nullptr)
 {
 	for (uint32_t b = b0; c_off + 16u * b < c_end; b += step) {
 		uint32_t ks[4];
@@ -94,8 +94,33 @@ __device__ __forceinline__ void region_ks(const uint32_t *T, const uint32_t *rk,
 			uint32_t *p = dst + bp / 4u;
 			*p = xr ? *p ^ (ks[q] & m) : (ks[q] & m);
 		}
+		if (done)
+			__hip_atomic_store(done + b, 1u, __ATOMIC_RELEASE,
+					   __HIP_MEMORY_SCOPE_WORKGROUP);
 	}
 }
+
+/* protect: the MAC of chunk k waits until the keystream blocks that
+ * overlap [64k, 64k+64) of the cipher region are applied */
+struct ks_wait {
+	const uint32_t *done;           /* per block, or NULL: nothing */
+	uint32_t c_off, c_end;
+
+	__device__ __forceinline__ void operator()(uint32_t k) const
+	{
+		if (!done)
+			return;
+		const uint32_t lo = max(64u * k, c_off), hi = min(64u * k + 64u,
+								  c_end);
+		if (lo >= hi)
+			return;
+		for (uint32_t b = (lo - c_off) / 16u; b <= (hi - 1u - c_off) / 16u;
+		     b++)
+			while (!__hip_atomic_load(done + b, __ATOMIC_ACQUIRE,
+						  __HIP_MEMORY_SCOPE_WORKGROUP))
+				__builtin_amdgcn_s_sleep(1);
+	}
+};
 
 /* SHA-1 compression for ONE packet's chain (a latency, not a throughput
  * problem): per round only rotl(a, 5) and one v_add3 lie on the serial
@@ -150,7 +175,7 @@ __device__ __forceinline__ void sha1_compress_lat(uint32_t h[5],
 __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 					 const struct sgpu_comp *cp, uint32_t A,
 					 bool trail, uint32_t trailer,
-					 uint32_t h[5])
+					 uint32_t h[5], const ks_wait &wait)
 {
 	const uint64_t X = trail ? ((uint64_t)trailer << 32 | 0x80000000u)
 				 : 0x8000000000000000ull;
@@ -161,6 +186,7 @@ __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 	h[3] = cp->ipad[3]; h[4] = cp->ipad[4];
 	const uint32_t kA = A / 64u;
 	uint4 nx[4];
+	wait(0);
 #pragma unroll
 	for (int g = 0; g < 4; g++)
 		nx[g] = *(const uint4 *)(buf + 4 * g);
@@ -175,6 +201,7 @@ __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 			w[4 * g + 3] = bswap32(nx[g].w);
 		}
 		if (16u * (k + 1) < SMALL_MAX / 4) {
+			wait(k + 1);
 #pragma unroll
 			for (int g = 0; g < 4; g++)
 				nx[g] = *(const uint4 *)(buf + 16u * (k + 1) +
@@ -185,6 +212,7 @@ __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 #pragma unroll 1
 	for (uint32_t k = kA; k < nb; k++) {
 		uint32_t w[16];
+		wait(k);
 #pragma unroll
 		for (int g = 0; g < 4; g++) {
 			const uint32_t gw = 16u * k + 4u * g;
@@ -224,6 +252,7 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	__shared__ __attribute__((aligned(16))) uint32_t buf[SMALL_MAX / 4];
 	__shared__ __attribute__((aligned(16))) uint32_t ksb[SMALL_MAX / 4];
 	__shared__ uint32_t s_tag_ok;
+	__shared__ uint32_t bdone[SMALL_MAX / 16 + 1];  /* protect: block done */
 	const uint32_t i = blockIdx.x, tid = threadIdx.x;
 	if (i >= a.njobs)
 		return;
@@ -269,6 +298,9 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	const uint32_t *src = (const uint32_t *)(a.arena + j.off);
 	for (uint32_t w = tid; w < nw_out; w += blockDim.x)
 		buf[w] = w < nw_in ? src[w] : 0u;
+	if (PROT)
+		for (uint32_t b = tid; b < SMALL_MAX / 16 + 1; b += blockDim.x)
+			bdone[b] = 0;
 
 	if (tid < 4 * (nr + 1)) {
 		const uint32_t v = cp->rk[tid];
@@ -288,17 +320,21 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	uint8_t vd = 0;
 	uint32_t h[5];
 	if (PROT) {
-		/* the MAC covers the ciphertext: keystream first */
-		if (do_cipher)
-			region_ks(T, rk, nr, iv, c_off, c_end, buf, true, tid,
-				  blockDim.x);
-		__syncthreads();
+		/* the MAC covers the ciphertext: the other waves apply the
+		 * keystream while lane 0 hashes each chunk as soon as its
+		 * blocks are done */
+		if (do_cipher && tid >= 64u)
+			region_ks(T, rk, nr, iv, c_off, c_end, buf, true, tid - 64u,
+				  blockDim.x - 64u, bdone);
 		if (tid == 0 && do_hmac) {
-			hmac_lds(buf, cp, A, trail, j.trailer, h);
+			const ks_wait kw = {do_cipher ? bdone : nullptr, c_off,
+					    c_end};
+			hmac_lds(buf, cp, A, trail, j.trailer, h, kw);
 			uint8_t *tp = (uint8_t *)buf + j.tag_off;
 			for (uint32_t q = 0; q < tag_len; q++)
 				tp[q] = (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
 		}
+		__syncthreads();
 		if (tid == 0 && (j.flags & SJ_STORE_TRAIL)) {
 			uint8_t *tp = (uint8_t *)buf + j.t_off;
 			tp[0] = (uint8_t)(j.trailer >> 24);
@@ -313,7 +349,8 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 		if (tid == 0) {
 			uint32_t ok = 1;
 			if (do_hmac) {
-				hmac_lds(buf, cp, A, trail, j.trailer, h);
+				const ks_wait none = {nullptr, 0, 0};
+				hmac_lds(buf, cp, A, trail, j.trailer, h, none);
 				const uint8_t *tp = (const uint8_t *)buf + j.tag_off;
 				uint32_t diff = 0;
 				for (uint32_t q = 0; q < tag_len; q++)

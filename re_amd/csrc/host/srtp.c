@@ -196,6 +196,16 @@ static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
 static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
 static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
 				   host completed, re-run when waited for */
+/* the per-packet path's small launches and where their time goes (ns):
+ * the host work of run_mbufs_, the launch call, the synchronisation */
+static uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
+
+static uint64_t mono_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 /* fault injection (srtp_gpu_tune "fail_grow", like the reference's
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
  * now fails with ENOMEM */
@@ -232,6 +242,14 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
 	if (!strcmp(name, "gated"))
 		return __atomic_load_n(&g_cnt_gated, __ATOMIC_RELAXED);
+	if (!strcmp(name, "small_launches"))
+		return __atomic_load_n(&g_cnt_small, __ATOMIC_RELAXED);
+	if (!strcmp(name, "small_ns_launch"))
+		return __atomic_load_n(&g_ns_small_launch, __ATOMIC_RELAXED);
+	if (!strcmp(name, "small_ns_sync"))
+		return __atomic_load_n(&g_ns_small_sync, __ATOMIC_RELAXED);
+	if (!strcmp(name, "mbufs_ns"))
+		return __atomic_load_n(&g_ns_mbufs, __ATOMIC_RELAXED);
 	if (!strcmp(name, "prof_voided"))
 		return sgpu_prof_voided();
 	if (!strcmp(name, "fail_alloc"))
@@ -1642,9 +1660,23 @@ static int sess_host(struct srtp **sessv, size_t nsess)
 	return err;
 }
 
+static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
+			  const uint32_t *sidx, struct mbuf **mbv, int *errv,
+			  size_t n);
+
 static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 		      const uint32_t *sidx, struct mbuf **mbv, int *errv,
 		      size_t n)
+{
+	const uint64_t t0 = mono_ns();
+	const int err = run_mbufs_core(op, sessv, nsess, sidx, mbv, errv, n);
+	count(&g_ns_mbufs, mono_ns() - t0);
+	return err;
+}
+
+static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
+			  const uint32_t *sidx, struct mbuf **mbv, int *errv,
+			  size_t n)
 {
 	const int prot = op == OP_RTP_ENC || op == OP_RTCP_ENC;
 	struct engine E;
@@ -1748,9 +1780,16 @@ static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 			for (i = 0; i < n; i++)
 				if (E.rec[i].need_run)
 					E.rec[i].job.off = E.pi[i].start;
+			const uint64_t t0 = mono_ns();
 			rs = round_small(w, &E, bytes, soff, prot, &m, w->stream);
 			if (rs >= 0) {
+				const uint64_t t1 = mono_ns();
 				err = rs ? rs : sgpu_stream_sync(w->stream);
+				if (m) {
+					count(&g_cnt_small, 1);
+					count(&g_ns_small_launch, t1 - t0);
+					count(&g_ns_small_sync, mono_ns() - t1);
+				}
 				if (err)
 					goto out;
 				round_collect(w, &E, m);
@@ -1855,7 +1894,7 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 #include <sys/syscall.h>
 #include <unistd.h>
 
-enum { PC_QUEUED = 0, PC_DONE = 1, PC_RUN = 2 };
+enum { PC_QUEUED = 0, PC_DONE = 1, PC_RUN = 2, PC_SLEEP = 3 };
 
 struct pc_req {
 	struct pc_req *next;
@@ -1870,25 +1909,35 @@ static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct pc_req *pc_head, *pc_tail;
 static int pc_running;
 
+/* the owner learns v; a futex wake only if it went to sleep (PC_SLEEP) */
 static void pc_wake(int *state, int v)
 {
-	__atomic_store_n(state, v, __ATOMIC_RELEASE);
-	(void)syscall(SYS_futex, state, FUTEX_WAKE_PRIVATE, 1, NULL, NULL, 0);
+	if (__atomic_exchange_n(state, v, __ATOMIC_ACQ_REL) == PC_SLEEP)
+		(void)syscall(SYS_futex, state, FUTEX_WAKE_PRIVATE, 1, NULL,
+			      NULL, 0);
 }
 
-static int pc_wait(const int *state)
+static int pc_wait(int *state)
 {
 	int spin, v;
-	for (spin = 0; spin < 2000; spin++) {
+	for (spin = 0; spin < 4000; spin++) {
 		v = __atomic_load_n(state, __ATOMIC_ACQUIRE);
 		if (v != PC_QUEUED)
 			return v;
 		__builtin_ia32_pause();
 	}
-	while ((v = __atomic_load_n(state, __ATOMIC_ACQUIRE)) == PC_QUEUED)
-		(void)syscall(SYS_futex, state, FUTEX_WAIT_PRIVATE, PC_QUEUED,
-			      NULL, NULL, 0);
-	return v;
+	for (;;) {
+		int q = PC_QUEUED;
+		if (!__atomic_compare_exchange_n(state, &q, PC_SLEEP, 0,
+						 __ATOMIC_ACQ_REL,
+						 __ATOMIC_ACQUIRE))
+			return q;       /* DONE or RUN arrived */
+		while ((v = __atomic_load_n(state, __ATOMIC_ACQUIRE)) ==
+		       PC_SLEEP)
+			(void)syscall(SYS_futex, state, FUTEX_WAIT_PRIVATE,
+				      PC_SLEEP, NULL, NULL, 0);
+		return v;
+	}
 }
 
 /* one operation's requests of a list, as multi-session batches */
@@ -1926,6 +1975,22 @@ static void pc_run_op(struct pc_req *list, int op)
 			if (!err)
 				err = run_mbufs_(op, sv, n, idx, mv, ev, n);
 			free(idx);
+		}
+		if (err && n > 1) {
+			/* a batch-level error (one session busy with another
+			 * thread's asynchronous calls, an allocation): the
+			 * failed batch changed nothing, so each request runs on
+			 * its own and gets the result its own call would */
+			for (i = 0; i < n; i++) {
+				uint32_t zero = 0;
+				int e = sess_host(&sv[i], 1);
+				if (!e)
+					e = run_mbufs_(op, &sv[i], 1, &zero, &mv[i],
+						       &ev[i], 1);
+				rq[i]->err = e ? e : ev[i];
+			}
+			table_unlock();
+			continue;
 		}
 		table_unlock();
 		for (i = 0; i < n; i++)
@@ -2047,11 +2112,8 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 		pc_head = pc_tail = NULL;
 		pthread_mutex_unlock(&pc_lock);
 		pc_run(list);
-		for (r = list; r; r = nx) {
-			nx = r->next;   /* r may be gone once woken */
-			if (r != &req)
-				pc_wake(&r->state, PC_DONE);
-		}
+		/* the next batch first: hand the runner role on, then
+		 * complete this one's callers */
 		pthread_mutex_lock(&pc_lock);
 		next_runner = pc_head;
 		if (!next_runner)
@@ -2059,6 +2121,11 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 		pthread_mutex_unlock(&pc_lock);
 		if (next_runner)
 			pc_wake(&next_runner->state, PC_RUN);
+		for (r = list; r; r = nx) {
+			nx = r->next;   /* r may be gone once woken */
+			if (r != &req)
+				pc_wake(&r->state, PC_DONE);
+		}
 	}
 	return req.err;
 }

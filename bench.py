@@ -317,6 +317,13 @@ def main():
     ap.add_argument("--percall-suite", type=int, default=1,
                     help="--percall: enum srtp_suite (1 AES_CM_128_HMAC_"
                          "SHA1_80, 4 AES_128_GCM, 5 AES_256_GCM)")
+    ap.add_argument("--rtcp-report", action="store_true",
+                    help="the RTCP report path on the device (SURVEY 8(f)4): "
+                         "1M SR + report block + SDES CNAME compounds "
+                         "encoded (rtcp_encode_batch_dev), SRTCP-protected, "
+                         "-unprotected and decoded with their contents "
+                         "(rtcp_decode_full_batch_dev), per stage and end "
+                         "to end")
     ap.add_argument("--dry-run", action="store_true",
                     help="testing only (CPU): rank plumbing, no GPU work")
     args = ap.parse_args()
@@ -336,6 +343,8 @@ def main():
                        int(os.environ.get("RANK", "0")))
     if args.percall:
         return percall_bench(args)
+    if args.rtcp_report:
+        return rtcp_report_bench(args)
 
     import torch
     import torch.distributed as dist
@@ -940,6 +949,137 @@ def percall_bench(args):
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(CONFIGS[2])
     print(json.dumps(line))
+    return 0
+
+
+def rtcp_report_bench(args):
+    """RTCP report path on one GPU: a step encodes n
+    compounds (SR with one report block + SDES CNAME, libre's rtcp_sess
+    report shape, one sender SSRC), SRTCP-protects and -unprotects them in
+    place (AES_CM_128_HMAC_SHA1_80) and decodes them with their contents.
+    value = compounds per second end to end; per-stage device times from
+    stages run one at a time; the decoded fields of every 4099th compound
+    are checked against the encode inputs after the timed steps."""
+    import numpy as np
+    import torch
+    import re_amd.srtp as P
+
+    torch.cuda.set_device(0)
+    P.load()
+    n = args.packets or (1 << 20)
+    rng = np.random.default_rng(314)
+    dm, drb, dch, dsd = P.rtcp_enc_dtypes()
+    msg = np.zeros(2 * n, dtype=dm)
+    msg["pt"][0::2], msg["pt"][1::2] = 200, 202
+    msg["count"][:] = 1
+    w = rng.integers(0, 2**32, (n, 6), dtype=np.uint64).astype(np.uint32)
+    w[:, 0] = 0x5EED0001
+    msg["w"][0::2] = w
+    msg["first"][0::2] = msg["first"][1::2] = np.arange(n)
+    msg["num"][:] = 1
+    rb = np.zeros(n, dtype=drb)
+    for f in drb.names:
+        rb[f] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    clen = np.full(n, 20, dtype=np.uint32)          # "user@host.example"
+    pool = rng.integers(33, 127, int(clen.sum()), dtype=np.uint8)
+    chunk = np.zeros(n, dtype=dch)
+    chunk["src"], chunk["first"], chunk["num"] = w[:, 0], np.arange(n), 1
+    sdes = np.zeros(n, dtype=dsd)
+    sdes["type"], sdes["len"] = 1, clen
+    sdes["off"] = np.arange(n, dtype=np.uint32) * 20
+    A = dict(msg=msg, rb=rb, chunk=chunk, sdes=sdes,
+             src=np.zeros(1, dtype=np.uint32), pool=pool,
+             mfirst=np.arange(0, 2 * n + 1, 2, dtype=np.uint32))
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(
+        np.uint8)).cuda()
+    dA = {k: dev(v) for k, v in A.items()}
+    slot = 192
+    pos = np.arange(n, dtype=np.uint32) * slot
+    arena = torch.zeros(n * slot, dtype=torch.uint8, device="cuda")
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(
+        np.int32)).cuda()
+    p_d, c_d = i32(pos), i32(pos + slot)
+    e_d = torch.zeros(n, dtype=torch.int32, device="cuda")
+    err = torch.zeros(n, dtype=torch.int32, device="cuda")
+    maxmsg, maxitem = 2, 4
+    desc = torch.zeros(n * maxmsg * 5, dtype=torch.int32, device="cuda")
+    item = torch.zeros(n * maxitem * 8, dtype=torch.int32, device="cuda")
+    nm, ni, ee, st = (torch.zeros(n, dtype=torch.int32, device="cuda")
+                      for _ in range(4))
+    key = bytes(range(30))
+    tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+
+    def enc():
+        assert P.rtcp_encode_dev(
+            arena.data_ptr(), arena.numel(), p_d.data_ptr(), e_d.data_ptr(),
+            c_d.data_ptr(), n, dA["mfirst"].data_ptr(), dA["msg"].data_ptr(),
+            2 * n, dA["rb"].data_ptr(), n, dA["chunk"].data_ptr(), n,
+            dA["sdes"].data_ptr(), n, dA["src"].data_ptr(), 1,
+            dA["pool"].data_ptr(), len(pool), err.data_ptr()) == 0
+
+    def srtcp(op, ctx):
+        assert P.device_batch_dev(op, [ctx], arena.data_ptr(), arena.numel(),
+                                  p_d.data_ptr(), e_d.data_ptr(),
+                                  c_d.data_ptr(), err.data_ptr(), n) == 0
+
+    def dec():
+        assert P.rtcp_decode_full_dev(
+            arena.data_ptr(), arena.numel(), p_d.data_ptr(), e_d.data_ptr(),
+            n, desc.data_ptr(), maxmsg, nm.data_ptr(), item.data_ptr(),
+            maxitem, ni.data_ptr(), ee.data_ptr(), st.data_ptr()) == 0
+
+    stages = [("encode", enc), ("srtcp_protect",
+                                lambda: srtcp("srtcp_encrypt", tx)),
+              ("srtcp_unprotect", lambda: srtcp("srtcp_decrypt", rx)),
+              ("decode_full", dec)]
+    for _ in range(max(1, args.warmup)):
+        for _, f in stages:
+            f()
+    torch.cuda.synchronize()
+    steps = args.steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for _, f in stages:
+            f()
+    torch.cuda.synchronize()
+    T = (time.perf_counter() - t0) / steps
+    # per stage (each idempotent on a plaintext arena; protect and
+    # unprotect as a pair)
+    per = {}
+    for name, fs in (("encode", [enc]),
+                     ("srtcp_protect_unprotect", [stages[1][1],
+                                                  stages[2][1]]),
+                     ("decode_full", [dec])):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(steps):
+            for f in fs:
+                f()
+        torch.cuda.synchronize()
+        per[name] = (time.perf_counter() - a) / steps * 1e3
+    # the last stage run was decode_full of a valid arena: check a sample
+    it = item.cpu().numpy().view(np.uint32).reshape(n, maxitem, 8)
+    ok = bool((ni.cpu().numpy() == 4).all() and not err.cpu().numpy().any())
+    for i in range(0, n, 4099):
+        ok &= bool((it[i, 0, 1:6] == w[i, 1:6]).all() and
+                   it[i, 1, 1] == rb["ssrc"][i] and it[i, 2, 1] == w[i, 0]
+                   and it[i, 3, 1] == 20)
+    line = {"metric": "RTCP report path: compound encode + SRTCP protect + "
+                      "unprotect + decode with contents, per compound",
+            "value": round(n / T, 1), "unit": "compounds/s",
+            "higher_is_better": True, "n_gpus": 1, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(T * 1e3, 3),
+            "stage_ms": {k: round(v, 3) for k, v in per.items()},
+            "bytes_per_compound": int((e_d.cpu().numpy().view(np.uint32) -
+                                       pos)[0]),
+            "verified_roundtrip": ok, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": "rtcp-report: %d x (SR + 1 RB + SDES "
+                                   "CNAME 20 B), AES_CM_128_HMAC_SHA1_80 "
+                                   "SRTCP" % n}}
+    print(json.dumps(line))
+    tx.close()
+    rx.close()
     return 0
 
 

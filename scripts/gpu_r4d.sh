@@ -11,6 +11,7 @@ rc=$?
 timeout -k 10 400 python bench.py --percall --no-cpu-baseline > $O/percall.json 2> $O/percall.err || exit $?
 RE_SRTP_NOSMALL=1 timeout -k 10 400 python bench.py --percall --no-cpu-baseline > $O/percall_nosmall.json 2> $O/percall_nosmall.err || exit $?
 timeout -k 10 300 python scripts/rx_index_timing.py > $O/rx_index.json 2> $O/rx_index.err || exit $?
+timeout -k 10 300 python bench.py --rtcp-report --steps 5 > $O/rtcp_report.json 2> $O/rtcp_report.err || exit $?
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run -- $R/re_amd/lib/percall 3000 1 > $R/$O/prof_percall.json 2> $R/$O/prof.err || exit $?

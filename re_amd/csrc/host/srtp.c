@@ -1920,7 +1920,9 @@ static void pc_wake(int *state, int v)
 static int pc_wait(int *state)
 {
 	int spin, v;
-	for (spin = 0; spin < 4000; spin++) {
+	/* a short spin, then sleep: many callers spinning on fewer cores
+	 * would take the CPU from the runner and its helper */
+	for (spin = 0; spin < 1000; spin++) {
 		v = __atomic_load_n(state, __ATOMIC_ACQUIRE);
 		if (v != PC_QUEUED)
 			return v;

@@ -20,6 +20,11 @@
  *   7  SRTCP, config-2 arena shape (1M x 1200-B RTCP packets, CM128/HMAC80,
  *      srtcp_encrypt/srtcp_decrypt, src/srtp/srtcp.c:31-287)
  *   8  SRTCP, config-3 shape (AEAD_AES_256_GCM)
+ *   9  config 2 with forged packets: after protect, every packet i with
+ *      i % 1000 == 999 gets payload byte 20 (arena offset pos + 32)
+ *      flipped (^ 0x40) -- 1048 EAUTH verdicts, the receiver states and the
+ *      post-error bytes (ciphertext kept, ROC over the tag) pinned
+ *  10  config 4 (64K sessions, mixed lengths) with the same forgeries
  *
  *   ref_digest <config> [npkts]
  */
@@ -77,9 +82,10 @@ struct cfg {
 	int test_key;
 	unsigned nssrc;         /* SSRCs of session 0: packet i -> i mod nssrc */
 	int rtcp;               /* SRTCP (workload.make_rtcp_arena) */
+	unsigned forge;         /* forge packet i when i % forge == forge-1 */
 };
 
-#define NCFG 9
+#define NCFG 11
 static const struct cfg CFG[NCFG] = {
 	{0, 0, 0, 0, 0, 0, 1, 0},
 	{1, 1024, 160, 1, 1, 1, 1, 0},
@@ -90,6 +96,8 @@ static const struct cfg CFG[NCFG] = {
 	{1, 1u << 20, 1200, 1, 65000, 0, 2, 0},
 	{1, 1u << 20, 1200, 1, 65000, 0, 1, 1},
 	{5, 1u << 20, 1200, 1, 65000, 0, 1, 1},
+	{1, 1u << 20, 1200, 1, 65000, 0, 1, 0, 1000},
+	{1, 1u << 20, 0, 1u << 16, 65000, 0, 1, 0, 1000},
 };
 
 static void hex(const uint8_t *p, size_t n)
@@ -290,8 +298,9 @@ int main(int argc, char **argv)
 	}
 
 	printf("{\"config\":%d,\"suite\":%d,\"n\":%zu,\"slot\":%zu,"
-	       "\"nsess\":%zu,\"nssrc\":%u,\"rtcp\":%d,\"plain\":", c, cf.suite,
-	       n, slot, cf.nsess, cf.nssrc, cf.rtcp);
+	       "\"nsess\":%zu,\"nssrc\":%u,\"rtcp\":%d,\"forge\":%u,"
+	       "\"plain\":", c, cf.suite, n, slot, cf.nsess, cf.nssrc, cf.rtcp,
+	       cf.forge);
 	sha(arena, n * slot);
 
 	/* protect every packet in array order, in place (the slot has room
@@ -308,6 +317,10 @@ int main(int argc, char **argv)
 	}
 	emit("protect", arena, n, slot, end, err, tx, nrows, cf.nssrc > 1,
 	     cf.rtcp, stbuf);
+	if (cf.forge)
+		for (i = 0; i < n; i++)
+			if (i % cf.forge == cf.forge - 1)
+				arena[pos[i] + 32] ^= 0x40;
 
 	for (i = 0; i < n; i++) {
 		struct mbuf mb;

@@ -175,7 +175,8 @@ int main(int argc, char **argv)
 		long err = 0;
 		int t;
 		const uint64_t b0 = srtp_gpu_counter("pcbatches"),
-			       p0 = srtp_gpu_counter("pcpackets");
+			       p0 = srtp_gpu_counter("pcpackets"),
+			       mb0 = srtp_gpu_counter("mbufs_ns");
 		for (t = 0; t < T; t++) {
 			js[t].calls = calls / 4 > 1000 ? calls / 4 : 1000;
 			js[t].id = t;
@@ -188,10 +189,15 @@ int main(int argc, char **argv)
 			err += js[t].errors;
 		}
 		const double nb = (double)(srtp_gpu_counter("pcbatches") - b0);
+		/* the launches' own time (run_mbufs_: host plan, launch,
+		 * sync, unpack) against the wall time per launch */
 		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld,"
-		       "\"packets_per_launch\":%.1f}",
+		       "\"packets_per_launch\":%.1f,\"us_per_launch\":%.1f,"
+		       "\"wall_us_per_launch\":%.1f}",
 		       a > 2 ? "," : "", T, T * js[0].calls / ((t1 - t0) * 1e-6),
-		       err, nb ? (srtp_gpu_counter("pcpackets") - p0) / nb : 0);
+		       err, nb ? (srtp_gpu_counter("pcpackets") - p0) / nb : 0,
+		       nb ? (srtp_gpu_counter("mbufs_ns") - mb0) / nb / 1e3 : 0,
+		       nb ? (t1 - t0) / nb : 0);
 		free(js);
 		free(th);
 	}

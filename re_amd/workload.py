@@ -175,6 +175,9 @@ def random_sessions(npkts, nsess, seed=SEED_PAYLOAD + 2):
 #   5  the config-5 stream, 2M packets (two 1M shards of it)
 #   6  config 2 over 2 SSRCs of one session (packet i -> SSRC i mod 2)
 #   7  SRTCP in the config-2 shape, 8  SRTCP in the config-3 shape
+#   9  config 2, 10 config 4, with the packets i % 1000 == 999 forged
+#      between protect and unprotect (FORGE_AT: payload byte 20 ^ 0x40)
+FORGE_AT = 32
 CONFIGS = {
     1: dict(suite=1, n=1024, length=160, nsess=1, s0=1, key=CONFIG1_KEY),
     2: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000),
@@ -184,6 +187,9 @@ CONFIGS = {
     6: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, nssrc=2),
     7: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, rtcp=True),
     8: dict(suite=5, n=1 << 20, length=1200, nsess=1, s0=65000, rtcp=True),
+    9: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, forge=1000),
+    10: dict(suite=1, n=1 << 20, length=None, nsess=1 << 16, s0=65000,
+             forge=1000),
 }
 
 KEY_LEN = {0: 30, 1: 30, 2: 46, 3: 46, 4: 28, 5: 44}

@@ -1,7 +1,7 @@
 #!/bin/sh
 # Regenerate tests/golden/fullsize_digests.json: the reference src/srtp
 # (oracle/_ref/ref_digest, built by `make -C oracle ref` from the sources
-# under /root/reference) over the full BASELINE.json configs 1-4 and the shapes 5-8
+# under /root/reference) over the full BASELINE.json configs 1-4 and the shapes 5-10
 # (ref_digest.c).
 # Build container only (needs /root/reference); ~15 s.
 set -e
@@ -17,7 +17,9 @@ make -s -C oracle ref
 	oracle/_ref/ref_digest 5; echo ','
 	oracle/_ref/ref_digest 6; echo ','
 	oracle/_ref/ref_digest 7; echo ','
-	oracle/_ref/ref_digest 8
+	oracle/_ref/ref_digest 8; echo ','
+	oracle/_ref/ref_digest 9; echo ','
+	oracle/_ref/ref_digest 10
 	echo ']}'
 } > tests/golden/fullsize_digests.json
 python -c "import json; json.load(open('tests/golden/fullsize_digests.json'))"

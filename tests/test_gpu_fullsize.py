@@ -99,6 +99,12 @@ def check_config(torch, ref, cfg):
     pfx = "srtcp" if rtcp else "srtp"
     for direction, op, ctxs in (("protect", pfx + "_encrypt", tx),
                                 ("unprotect", pfx + "_decrypt", rx)):
+        if direction == "unprotect" and ref.get("forge"):
+            # shapes 9, 10: forge packets i % f == f - 1 (ref_digest.c)
+            f = ref["forge"]
+            idx = torch.from_numpy(pos[f - 1::f].astype(np.int64) +
+                                   W.FORGE_AT).cuda()
+            dev[idx] ^= 0x40
         err = run_dev(torch, op, ctxs, dev, pos_d, end_d, cap_d, sess_d, n)
         m = F.compare(ref[direction], dev.cpu().numpy(), n, slot,
                       end_d.cpu().numpy().view(np.uint32),
@@ -110,10 +116,13 @@ def check_config(torch, ref, cfg):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 7, 8, 9, 10])
 def test_fullsize_vs_reference(torch_cuda, digests, cfg):
-    """configs 1-4, and SRTCP arenas of the config-2 / config-3 shape
-    (7, 8: 1M x 1200-B RTCP packets through srtcp_*_batch_dev)"""
+    """configs 1-4, SRTCP arenas of the config-2 / config-3 shape (7, 8:
+    1M x 1200-B RTCP packets through srtcp_*_batch_dev), and configs 2 / 4
+    with 0.1 % of the packets forged between protect and unprotect (9, 10:
+    the EAUTH verdicts, the post-error bytes -- ciphertext kept, the ROC
+    over the tag -- and every receiver state against the reference)"""
     check_config(torch_cuda, digests[cfg], cfg)
 
 

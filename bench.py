@@ -929,13 +929,11 @@ def percall_bench(args):
     job's cores for the same packet size"""
     exe = os.path.join(ROOT, "re_amd", "lib", "percall")
     threads = sorted({4, 16, 64})
-    # --tune knobs reach the driver's library through its environment
+    # --tune knobs reach the driver's library as srtp_gpu_tune calls
     env = dict(os.environ)
     env["PERCALL_SUITE"] = str(args.percall_suite)
-    for kv in args.tune:
-        k, v = kv.split("=")
-        if int(v):
-            env["RE_SRTP_" + k.upper()] = v
+    if args.tune:
+        env["PERCALL_TUNE"] = ",".join(args.tune)
     out = subprocess.run([exe, str(args.percall_calls)] +
                          [str(t) for t in threads], capture_output=True,
                          text=True, timeout=900, check=True, env=env).stdout

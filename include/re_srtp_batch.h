@@ -232,7 +232,10 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * CTR launches keep the cipher in the one-packet-per-lane kernel),
  * "mpradix" (multi-session plans group packets by the radix sort),
  * "nodevfold" (forged packets
- * of a device-planned batch fold on the host), "trace", "times" (phase
+ * of a device-planned batch fold on the host), "nocombine" (per-packet
+ * calls of different threads do not share launches), "nosmall" (the
+ * per-packet path's fused small kernel off), "nofuse" (the operations of
+ * a shared per-packet launch run as one launch each), "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores
  * a size's built-in default.  Results never depend on them.  0 or EINVAL.
@@ -246,7 +249,8 @@ int srtp_gpu_tune(const char *name, long value);
  * verdicts folded on the device, no re-run), "rejects" (device plans
  * rejected: the host planned instead), "splans" (per-stream device plans),
  * "pcbatches" / "pcpackets" (shared launches of per-packet calls and the
- * packets they carried), "gated" (asynchronous calls queued behind one
+ * packets they carried), "pcfused" (those of them that ran several
+ * operations as one launch), "gated" (asynchronous calls queued behind one
  * the host completed, re-run when waited for).  0 for an unknown name.
  */
 uint64_t srtp_gpu_counter(const char *name);

@@ -12,6 +12,7 @@
  * round trip is checked.
  *
  *   percall <calls per thread> <threads...>   -> one JSON line
+ *   (PERCALL_SUITE=<enum srtp_suite>, PERCALL_TUNE=name=value,...)
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -124,6 +125,21 @@ int main(int argc, char **argv)
 	const long calls = argc > 1 ? atol(argv[1]) : 20000;
 	if (getenv("PERCALL_SUITE"))
 		g_suite = (enum srtp_suite)atoi(getenv("PERCALL_SUITE"));
+	if (getenv("PERCALL_TUNE")) {
+		/* A/B knobs: "name=value,name=value" (srtp_gpu_tune) */
+		char *spec = strdup(getenv("PERCALL_TUNE")), *tok, *sp = NULL;
+		for (tok = strtok_r(spec, ",", &sp); tok;
+		     tok = strtok_r(NULL, ",", &sp)) {
+			char *eq = strchr(tok, '=');
+			if (eq)
+				*eq = 0;
+			if (srtp_gpu_tune(tok, eq ? atol(eq + 1) : 1)) {
+				fprintf(stderr, "percall: bad knob %s\n", tok);
+				return 2;
+			}
+		}
+		free(spec);
+	}
 	struct job j0;
 	int a;
 
@@ -176,6 +192,7 @@ int main(int argc, char **argv)
 		int t;
 		const uint64_t b0 = srtp_gpu_counter("pcbatches"),
 			       p0 = srtp_gpu_counter("pcpackets"),
+			       f0 = srtp_gpu_counter("pcfused"),
 			       mb0 = srtp_gpu_counter("mbufs_ns");
 		for (t = 0; t < T; t++) {
 			js[t].calls = calls / 4 > 1000 ? calls / 4 : 1000;
@@ -193,11 +210,12 @@ int main(int argc, char **argv)
 		 * sync, unpack) against the wall time per launch */
 		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld,"
 		       "\"packets_per_launch\":%.1f,\"us_per_launch\":%.1f,"
-		       "\"wall_us_per_launch\":%.1f}",
+		       "\"wall_us_per_launch\":%.1f,\"fused_frac\":%.2f}",
 		       a > 2 ? "," : "", T, T * js[0].calls / ((t1 - t0) * 1e-6),
 		       err, nb ? (srtp_gpu_counter("pcpackets") - p0) / nb : 0,
 		       nb ? (srtp_gpu_counter("mbufs_ns") - mb0) / nb / 1e3 : 0,
-		       nb ? (t1 - t0) / nb : 0);
+		       nb ? (t1 - t0) / nb : 0,
+		       nb ? (srtp_gpu_counter("pcfused") - f0) / nb : 0);
 		free(js);
 		free(th);
 	}

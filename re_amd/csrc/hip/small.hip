@@ -244,7 +244,9 @@ __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 
 } /* namespace */
 
-template <bool PROT>
+/* MODE 0 unprotect, 1 protect, 2 per job (SJ_PROTECT): the operations of
+ * one shared per-packet launch in one grid (host pc_run_fused) */
+template <int MODE>
 __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 {
 	__shared__ uint32_t T[256];
@@ -256,6 +258,7 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	if (i >= a.njobs)
 		return;
 	const struct sgpu_job j = a.jobs[i];
+	const bool PROT = MODE == 2 ? (j.flags & SJ_PROTECT) != 0 : MODE == 1;
 	if (j.flags & SJ_SKIP) {
 		if (tid == 0 && a.verdict)
 			a.verdict[i] = 0;
@@ -410,7 +413,8 @@ int small_launch(uint8_t *arena, uint64_t arena_size,
 	a.t0 = t0;
 	a.verdict = verdict;
 	a.save = save;
-	hipLaunchKernelGGL(prot ? k_ctr_small<true> : k_ctr_small<false>,
+	hipLaunchKernelGGL(prot == 2 ? k_ctr_small<2>
+			   : prot ? k_ctr_small<1> : k_ctr_small<0>,
 			   dim3(njobs), dim3(256), 0, (hipStream_t)stream, a);
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

@@ -152,6 +152,9 @@ static struct {
 	int nosmall;            /* RE_SRTP_NOSMALL: the per-packet path's small
 				   CTR launches take the general kernels
 				   with copies (not sgpu_run_small) */
+	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
+				   shared per-packet launch run as separate
+				   launches (helper thread), not one */
 	int trace;              /* RE_SRTP_TRACE: per-call phase times */
 	int times;              /* RE_SRTP_TIMES: multi-session phases */
 	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
@@ -194,6 +197,8 @@ static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
 static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
 static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
+static uint64_t g_cnt_pcfused;  /* ... of which several operations in one
+				   small launch (pc_run_fused) */
 static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
 				   host completed, re-run when waited for */
 /* the per-packet path's small launches and where their time goes (ns):
@@ -240,6 +245,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcpackets"))
 		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
+	if (!strcmp(name, "pcfused"))
+		return __atomic_load_n(&g_cnt_pcfused, __ATOMIC_RELAXED);
 	if (!strcmp(name, "gated"))
 		return __atomic_load_n(&g_cnt_gated, __ATOMIC_RELAXED);
 	if (!strcmp(name, "small_launches"))
@@ -289,6 +296,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "nosmall"))
 		g_env.nosmall = value > 0;
+	else if (!strcmp(name, "nofuse"))
+		g_env.nofuse = value > 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -1512,19 +1521,22 @@ static int round_fetch(struct ws *w, uint32_t m, void *stream)
 			       stream);
 }
 
+static void collect_rec(struct rec *r, uint8_t v, uint32_t save)
+{
+	r->ran = 1;
+	r->ran_job = r->job;
+	r->vd = v;
+	if (r->job.flags & SJ_ROC_AT_TAG)
+		r->save = save;
+}
+
 static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 {
 	const uint8_t *v = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
 	const uint32_t *sv = (const uint32_t *)(v + m);
 	uint32_t k;
-	for (k = 0; k < m; k++) {
-		struct rec *r = &E->rec[w->cls_idx[k]];
-		r->ran = 1;
-		r->ran_job = r->job;
-		r->vd = v[k];
-		if (r->job.flags & SJ_ROC_AT_TAG)
-			r->save = sv[k];
-	}
+	for (k = 0; k < m; k++)
+		collect_rec(&E->rec[w->cls_idx[k]], v[k], sv[k]);
 }
 
 /*
@@ -1535,6 +1547,24 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
  * jobs, errno, or -1: not eligible (a GCM job, a packet past
  * SGPU_SMALL_MAX, more than SGPU_COOP_MAX jobs) -- nothing launched.
  */
+/* #jobs of a planned round if the small kernel can take all of them,
+ * else (size_t)-1 */
+static size_t small_fits(const struct engine *E)
+{
+	size_t i, need = 0;
+	for (i = 0; i < E->n; i++) {
+		const struct rec *r = &E->rec[i];
+		if (!r->need_run)
+			continue;
+		if ((r->job.flags & (SJ_GCM | SJ_UNDO)) ||
+		    r->ext_end - E->pi[i].start > SGPU_SMALL_MAX ||
+		    r->in_end - E->pi[i].start > SGPU_SMALL_MAX)
+			return (size_t)-1;
+		need++;
+	}
+	return need;
+}
+
 static int round_small(struct ws *w, struct engine *E, uint64_t asz,
 		       const uint32_t *joff, int prot, uint32_t *pm,
 		       void *stream)
@@ -1548,16 +1578,9 @@ static int round_small(struct ws *w, struct engine *E, uint64_t asz,
 	*pm = 0;
 	if (g_env.nosmall)
 		return -1;
-	for (i = 0; i < E->n; i++) {
-		const struct rec *r = &E->rec[i];
-		if (!r->need_run)
-			continue;
-		if ((r->job.flags & (SJ_GCM | SJ_UNDO)) ||
-		    r->ext_end - E->pi[i].start > SGPU_SMALL_MAX ||
-		    r->in_end - E->pi[i].start > SGPU_SMALL_MAX)
-			return -1;
-		need++;
-	}
+	need = small_fits(E);
+	if (need == (size_t)-1)
+		return -1;
 	if (!need)
 		return 0;
 	if (need > SGPU_COOP_MAX)
@@ -1660,51 +1683,55 @@ static int sess_host(struct srtp **sessv, size_t nsess)
 	return err;
 }
 
-static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
-			  const uint32_t *sidx, struct mbuf **mbv, int *errv,
-			  size_t n);
-
-static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
-		      const uint32_t *sidx, struct mbuf **mbv, int *errv,
-		      size_t n)
-{
-	const uint64_t t0 = mono_ns();
-	const int err = run_mbufs_core(op, sessv, nsess, sidx, mbv, errv, n);
-	count(&g_ns_mbufs, mono_ns() - t0);
-	return err;
-}
-
-static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
-			  const uint32_t *sidx, struct mbuf **mbv, int *errv,
-			  size_t n)
-{
-	const int prot = op == OP_RTP_ENC || op == OP_RTCP_ENC;
+/*
+ * One operation's packets through the GPU rounds: plan on the host (the
+ * reference's sequential semantics), stage the packets that need a run,
+ * run them, collect the verdicts; a verdict that changes a later packet's
+ * plan (a forged packet, a replay) makes another round from the snapshot.
+ * run_mbufs_core drives one operation; pc_run_fused drives the first round
+ * of several operations as one launch.
+ */
+struct mbc {
+	int op, prot, snapped, done;
 	struct engine E;
-	struct ws *w;
-	uint8_t **outp = NULL;      /* where packet i's GPU output lives */
-	uint8_t *keep = NULL;       /* per-packet copies across rounds */
-	uint32_t *soff = NULL;      /* staging offsets */
-	size_t *koff = NULL, i, round;
-	int err, snapped = 0;
+	struct mbuf **mbv;
+	int *errv;
+	size_t n, round;
+	uint8_t **outp;         /* where packet i's GPU output lives */
+	uint8_t *keep;          /* per-packet copies across rounds */
+	uint32_t *soff;         /* staging offsets */
+	size_t *koff;
+};
 
+static int mbc_init(struct mbc *c, int op, struct srtp **sessv, size_t nsess,
+		    const uint32_t *sidx, struct mbuf **mbv, int *errv,
+		    size_t n)
+{
+	size_t i;
+	int err;
+
+	memset(c, 0, sizeof(*c));
+	c->op = op;
+	c->prot = op == OP_RTP_ENC || op == OP_RTCP_ENC;
+	c->mbv = mbv;
+	c->errv = errv;
+	c->n = n;
 	if (!sessv || !mbv)
 		return EINVAL;
 	for (i = 0; i < n; i++)
 		if (!mbv[i])
 			return EINVAL;
-	err = engine_init(&E, op, n, sessv, nsess, sidx);
+	err = engine_init(&c->E, op, n, sessv, nsess, sidx);
 	if (err)
-		goto out;
-	outp = fi_calloc(n ? n : 1, sizeof(*outp));
-	soff = fi_calloc(n ? n : 1, sizeof(*soff));
-	koff = fi_calloc(n ? n : 1, sizeof(*koff));
-	if (!outp || !soff || !koff) {
-		err = ENOMEM;
-		goto out;
-	}
+		return err;
+	c->outp = fi_calloc(n ? n : 1, sizeof(*c->outp));
+	c->soff = fi_calloc(n ? n : 1, sizeof(*c->soff));
+	c->koff = fi_calloc(n ? n : 1, sizeof(*c->koff));
+	if (!c->outp || !c->soff || !c->koff)
+		return ENOMEM;
 	for (i = 0; i < n; i++) {
 		struct mbuf *mb = mbv[i];
-		struct pinfo *pi = &E.pi[i];
+		struct pinfo *pi = &c->E.pi[i];
 		pi->start = (uint32_t)mb->pos;
 		pi->end = (uint32_t)mb->end;
 		pi->size = (uint32_t)mb->size;
@@ -1713,147 +1740,217 @@ static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
 		else
 			parse_rtcp(pi, mb->buf);
 	}
-	w = ws_get();
-	if (!w) {
-		err = ENOMEM;
-		goto out;
-	}
+	snap_take(&c->E);
+	c->snapped = 1;
+	return 0;
+}
 
-	snap_take(&E);
-	snapped = 1;
-	for (round = 0;; round++) {
-		size_t need, bytes = 0;
-		uint32_t m;
+/* the plan of the next round from the snapshot: #packets to run */
+static size_t mbc_plan(struct mbc *c)
+{
+	snap_restore(&c->E);
+	return plan_all(&c->E);
+}
 
-		snap_restore(&E);
-		need = plan_all(&E);
-		if (!need)
-			break;
-		if (round > n + 2) {
-			err = EIO;
-			goto out;
-		}
-		if (round == 1) {
-			/* staging is about to be reused: move outputs aside */
-			size_t tot = 0;
-			for (i = 0; i < n; i++)
-				if (outp[i]) {
-					koff[i] = tot;
-					tot += E.rec[i].ext_end - E.pi[i].start;
-				}
-			keep = fi_malloc(tot ? tot : 1);
-			if (!keep) {
-				err = ENOMEM;
-				goto out;
+/* staging is about to be reused: move the outputs of earlier rounds aside
+ * (from round 1 on; idempotent) */
+static int mbc_aside(struct mbc *c)
+{
+	const struct engine *E = &c->E;
+	size_t i;
+
+	if (c->round == 0)
+		return 0;
+	if (!c->keep) {
+		size_t tot = 0;
+		for (i = 0; i < c->n; i++)
+			if (c->outp[i]) {
+				c->koff[i] = tot;
+				tot += E->rec[i].ext_end - E->pi[i].start;
 			}
-		}
-		if (round >= 1) {
-			for (i = 0; i < n; i++)
-				if (outp[i] && outp[i] != keep + koff[i]) {
-					memcpy(keep + koff[i], outp[i],
-					       E.rec[i].ext_end - E.pi[i].start);
-					outp[i] = keep + koff[i];
-				}
-		}
-		/* stage the packets that need a run at 16-B aligned offsets */
-		for (i = 0; i < n; i++) {
-			const struct rec *r = &E.rec[i];
-			if (!r->need_run)
-				continue;
-			soff[i] = (uint32_t)bytes;
-			bytes += ((r->ext_end - E.pi[i].start) + 31u) & ~15u;
-		}
-		err = pool_reserve(w, &w->stage, bytes);
-		if (err)
-			goto out;
-		for (i = 0; i < n; i++) {
-			const struct rec *r = &E.rec[i];
-			if (!r->need_run)
-				continue;
-			memcpy(w->stage.h + soff[i], mbv[i]->buf + E.pi[i].start,
-			       r->in_end - E.pi[i].start);
-		}
-		{
-			/* few packets of the CTR suites: the fused kernel over
-			 * the pinned staging memory itself */
-			int rs;
-			for (i = 0; i < n; i++)
-				if (E.rec[i].need_run)
-					E.rec[i].job.off = E.pi[i].start;
-			const uint64_t t0 = mono_ns();
-			rs = round_small(w, &E, bytes, soff, prot, &m, w->stream);
-			if (rs >= 0) {
-				const uint64_t t1 = mono_ns();
-				err = rs ? rs : sgpu_stream_sync(w->stream);
-				if (m) {
-					count(&g_cnt_small, 1);
-					count(&g_ns_small_launch, t1 - t0);
-					count(&g_ns_small_sync, mono_ns() - t1);
-				}
-				if (err)
-					goto out;
-				round_collect(w, &E, m);
-				for (i = 0; i < n; i++)
-					if (E.rec[i].need_run)
-						outp[i] = w->stage.h + soff[i];
-				continue;
-			}
-		}
-		err = sgpu_memcpy_h2d(w->stage.d, w->stage.h, bytes, w->stream);
-		if (!err) {
-			/* job offsets are relative to the packet start */
-			for (i = 0; i < n; i++)
-				if (E.rec[i].need_run)
-					E.rec[i].job.off = E.pi[i].start;
-			err = round_launch(w, &E, SEL_RUN, w->stage.d, bytes,
-					   soff, prot, &m, w->stream);
-		}
-		if (!err)
-			err = round_fetch(w, m, w->stream);
-		if (!err)
-			err = sgpu_memcpy_d2h(w->stage.h, w->stage.d, bytes,
-					      w->stream);
-		if (!err)
-			err = sgpu_stream_sync(w->stream);
-		if (err)
-			goto out;
-		round_collect(w, &E, m);
-		for (i = 0; i < n; i++)
-			if (E.rec[i].need_run)
-				outp[i] = w->stage.h + soff[i];
+		c->keep = fi_malloc(tot ? tot : 1);
+		if (!c->keep)
+			return ENOMEM;
 	}
+	for (i = 0; i < c->n; i++)
+		if (c->outp[i] && c->outp[i] != c->keep + c->koff[i]) {
+			memcpy(c->keep + c->koff[i], c->outp[i],
+			       E->rec[i].ext_end - E->pi[i].start);
+			c->outp[i] = c->keep + c->koff[i];
+		}
+	return 0;
+}
 
+/* stage the packets that need a run at 16-B aligned offsets from base */
+static size_t mbc_offsets(struct mbc *c, size_t base)
+{
+	const struct engine *E = &c->E;
+	size_t i, bytes = base;
+	for (i = 0; i < c->n; i++) {
+		const struct rec *r = &E->rec[i];
+		if (!r->need_run)
+			continue;
+		c->soff[i] = (uint32_t)bytes;
+		bytes += ((r->ext_end - E->pi[i].start) + 31u) & ~15u;
+	}
+	return bytes;
+}
+
+static void mbc_stage(struct mbc *c, uint8_t *stage)
+{
+	struct engine *E = &c->E;
+	size_t i;
+	for (i = 0; i < c->n; i++) {
+		struct rec *r = &E->rec[i];
+		if (!r->need_run)
+			continue;
+		memcpy(stage + c->soff[i], c->mbv[i]->buf + E->pi[i].start,
+		       r->in_end - E->pi[i].start);
+		/* job offsets are relative to the packet start */
+		r->job.off = E->pi[i].start;
+	}
+}
+
+static void mbc_ran(struct mbc *c, uint8_t *stage)
+{
+	size_t i;
+	for (i = 0; i < c->n; i++)
+		if (c->E.rec[i].need_run)
+			c->outp[i] = stage + c->soff[i];
+	c->round++;
+}
+
+/* one round of one operation; c->done once nothing is left to run */
+static int mbc_round(struct mbc *c, struct ws *w)
+{
+	struct engine *E = &c->E;
+	size_t need, bytes;
+	uint32_t m;
+	int err, rs;
+
+	need = mbc_plan(c);
+	if (!need) {
+		c->done = 1;
+		return 0;
+	}
+	if (c->round > c->n + 2)
+		return EIO;
+	err = mbc_aside(c);
+	if (err)
+		return err;
+	bytes = mbc_offsets(c, 0);
+	err = pool_reserve(w, &w->stage, bytes);
+	if (err)
+		return err;
+	mbc_stage(c, w->stage.h);
+	{
+		/* few packets of the CTR suites: the fused kernel over the
+		 * pinned staging memory itself */
+		const uint64_t t0 = mono_ns();
+		rs = round_small(w, E, bytes, c->soff, c->prot, &m, w->stream);
+		if (rs >= 0) {
+			const uint64_t t1 = mono_ns();
+			err = rs ? rs : sgpu_stream_sync(w->stream);
+			if (m) {
+				count(&g_cnt_small, 1);
+				count(&g_ns_small_launch, t1 - t0);
+				count(&g_ns_small_sync, mono_ns() - t1);
+			}
+			if (err)
+				return err;
+			round_collect(w, E, m);
+			mbc_ran(c, w->stage.h);
+			return 0;
+		}
+	}
+	err = sgpu_memcpy_h2d(w->stage.d, w->stage.h, bytes, w->stream);
+	if (!err)
+		err = round_launch(w, E, SEL_RUN, w->stage.d, bytes, c->soff,
+				   c->prot, &m, w->stream);
+	if (!err)
+		err = round_fetch(w, m, w->stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(w->stage.h, w->stage.d, bytes, w->stream);
+	if (!err)
+		err = sgpu_stream_sync(w->stream);
+	if (err)
+		return err;
+	round_collect(w, E, m);
+	mbc_ran(c, w->stage.h);
+	return 0;
+}
+
+/* the results into the caller's mbufs */
+static int mbc_finish(struct mbc *c)
+{
+	const struct engine *E = &c->E;
+	size_t i;
+	int err;
 	/* mbuf size growth (same policy) first: a failed resize leaves
 	 * every mbuf's window and bytes, and the stream states, as before */
-	for (i = 0; i < n; i++) {
-		if (E.rec[i].size_o > mbv[i]->size) {
-			err = mbuf_resize(mbv[i], E.rec[i].size_o);
+	for (i = 0; i < c->n; i++) {
+		if (E->rec[i].size_o > c->mbv[i]->size) {
+			err = mbuf_resize(c->mbv[i], E->rec[i].size_o);
 			if (err)
-				goto out;
+				return err;
 		}
 	}
 	/* unpack: bytes, pos/end, errno */
-	for (i = 0; i < n; i++) {
-		const struct rec *r = &E.rec[i];
-		struct mbuf *mb = mbv[i];
-		const struct pinfo *pi = &E.pi[i];
-		if (r->has_job && outp[i])
-			memcpy(mb->buf + pi->start, outp[i],
+	for (i = 0; i < c->n; i++) {
+		const struct rec *r = &E->rec[i];
+		struct mbuf *mb = c->mbv[i];
+		const struct pinfo *pi = &E->pi[i];
+		if (r->has_job && c->outp[i])
+			memcpy(mb->buf + pi->start, c->outp[i],
 			       r->ext_end - pi->start);
 		mb->pos = r->pos_o;
 		mb->end = r->end_o;
-		if (errv)
-			errv[i] = r->err;
+		if (c->errv)
+			c->errv[i] = r->err;
 	}
- out:
+	return 0;
+}
+
+static void mbc_free(struct mbc *c, int err)
+{
 	/* a failed call leaves the stream states as it found them */
-	if (err && snapped)
-		snap_restore(&E);
-	free(outp);
-	free(keep);
-	free(soff);
-	free(koff);
-	engine_free(&E);
+	if (err && c->snapped)
+		snap_restore(&c->E);
+	free(c->outp);
+	free(c->keep);
+	free(c->soff);
+	free(c->koff);
+	engine_free(&c->E);
+}
+
+static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
+			  const uint32_t *sidx, struct mbuf **mbv, int *errv,
+			  size_t n)
+{
+	struct mbc c;
+	struct ws *w;
+	int err = mbc_init(&c, op, sessv, nsess, sidx, mbv, errv, n);
+
+	if (!err) {
+		w = ws_get();
+		if (!w)
+			err = ENOMEM;
+		while (!err && !c.done)
+			err = mbc_round(&c, w);
+		if (!err)
+			err = mbc_finish(&c);
+	}
+	mbc_free(&c, err);
+	return err;
+}
+
+static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
+		      const uint32_t *sidx, struct mbuf **mbv, int *errv,
+		      size_t n)
+{
+	const uint64_t t0 = mono_ns();
+	const int err = run_mbufs_core(op, sessv, nsess, sidx, mbv, errv, n);
+	count(&g_ns_mbufs, mono_ns() - t0);
 	return err;
 }
 
@@ -2044,6 +2141,193 @@ static void pc_helper_start(void)
 	pthread_attr_destroy(&a);
 }
 
+/*
+ * A list mixing operations whose packets all fit the small kernel (the CTR
+ * suites, <= SGPU_SMALL_MAX bytes): every operation plans its first round
+ * on the host and all of them run as ONE launch of the fused kernel (the
+ * protect or unprotect body per job, by SJ_PROTECT) -- one GPU round trip
+ * for the whole list instead of one per operation on two streams.  Later
+ * rounds (a verdict that changes a plan) run per operation as usual.
+ * Returns -1, with nothing changed, when the list does not qualify or a
+ * batch-level error stopped it before any result (the caller then runs
+ * the operations its usual way); else 0 with every request's result set.
+ */
+static int pc_run_fused(struct pc_req *list, unsigned ops)
+{
+	struct mbc cv[4];
+	struct srtp **sv = NULL;
+	struct mbuf **mv = NULL;
+	struct pc_req **rq = NULL;
+	int *ev = NULL;
+	uint32_t *idx = NULL, mst[5], m = 0;
+	size_t base[5], need[4], tot = 0, bytes = 0, i, k;
+	int nc = 0, opk[4], err = 0, inited = 0, redo = 0;
+	const uint64_t t0 = mono_ns();
+	struct pc_req *r;
+	struct sgpu_job *jh;
+	uint8_t *vh;
+	struct ws *w;
+
+	if (g_env.nosmall || g_env.nofuse)
+		return -1;
+	/* per operation, in list order */
+	base[0] = 0;
+	for (k = 0; k < 4; k++) {
+		size_t n = 0;
+		if (!((ops >> k) & 1))
+			continue;
+		for (r = list; r; r = r->next)
+			n += r->op == (int)k;
+		opk[nc] = (int)k;
+		base[nc + 1] = base[nc] + n;
+		nc++;
+	}
+	tot = base[nc];
+	if (!tot || tot > SGPU_COOP_MAX)
+		return -1;
+	sv = fi_malloc(tot * sizeof(*sv));
+	mv = fi_malloc(tot * sizeof(*mv));
+	rq = fi_malloc(tot * sizeof(*rq));
+	ev = fi_malloc(tot * sizeof(*ev));
+	idx = fi_malloc(tot * sizeof(*idx));
+	if (!sv || !mv || !rq || !ev || !idx) {
+		err = -1;
+		goto out_free;
+	}
+	for (k = 0; k < (size_t)nc; k++) {
+		i = base[k];
+		for (r = list; r; r = r->next)
+			if (r->op == opk[k]) {
+				rq[i] = r;
+				sv[i] = r->s;
+				mv[i] = r->mb;
+				idx[i] = (uint32_t)(i - base[k]);
+				i++;
+			}
+	}
+
+	table_rdlock();
+	w = ws_get();
+	err = w ? 0 : ENOMEM;
+	for (k = 0; !err && k < (size_t)nc; k++)
+		err = sess_host(sv + base[k], base[k + 1] - base[k]);
+	for (k = 0; !err && k < (size_t)nc; k++) {
+		const size_t b = base[k], n = base[k + 1] - b;
+		inited = (int)k + 1;
+		err = mbc_init(&cv[k], opk[k], sv + b, n, idx + b, mv + b,
+			       ev + b, n);
+	}
+	/* round 0: every operation planned; the small kernel takes all? */
+	for (k = 0; !err && k < (size_t)nc; k++) {
+		need[k] = mbc_plan(&cv[k]);
+		if (small_fits(&cv[k].E) == (size_t)-1)
+			err = -1;
+	}
+	for (k = 0; !err && k < (size_t)nc; k++)
+		bytes = mbc_offsets(&cv[k], bytes);
+	if (!err)
+		err = pool_reserve(w, &w->stage, bytes);
+	if (!err)
+		err = pool_reserve(w, &w->ctl, tot * (sizeof(struct sgpu_job) + 5));
+	if (!err)
+		err = idx_reserve(w, tot);
+	if (err)
+		goto out;
+	jh = (struct sgpu_job *)w->ctl.h;
+	for (k = 0; k < (size_t)nc; k++) {
+		struct mbc *c = &cv[k];
+		mbc_stage(c, w->stage.h);
+		mst[k] = m;
+		for (i = 0; i < c->n; i++) {
+			const struct rec *rc = &c->E.rec[i];
+			if (!rc->need_run)
+				continue;
+			jh[m] = rc->job;
+			jh[m].off = c->soff[i];
+			w->cls_idx[m++] = (uint32_t)i;
+		}
+	}
+	mst[nc] = m;
+	vh = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
+	if (m) {
+		const uint64_t t1 = mono_ns();
+		uint64_t t2;
+		err = sgpu_run_small(w->stage.h, bytes, jh, m, vh,
+				     (uint32_t *)(vh + m), 2, w->stream);
+		t2 = mono_ns();
+		if (!err)
+			err = sgpu_stream_sync(w->stream);
+		count(&g_cnt_small, 1);
+		count(&g_ns_small_launch, t2 - t1);
+		count(&g_ns_small_sync, mono_ns() - t2);
+		if (err)
+			goto out;
+	}
+	count(&g_cnt_pcbatch, 1);
+	count(&g_cnt_pcpkts, tot);
+	count(&g_cnt_pcfused, 1);
+	for (k = 0; k < (size_t)nc; k++) {
+		struct mbc *c = &cv[k];
+		uint32_t q;
+		if (!need[k]) {
+			c->done = 1;
+			continue;
+		}
+		for (q = mst[k]; q < mst[k + 1]; q++)
+			collect_rec(&c->E.rec[w->cls_idx[q]], vh[q],
+				    ((const uint32_t *)(vh + m))[q]);
+		mbc_ran(c, w->stage.h);
+	}
+	/* later rounds reuse the staging memory: every operation's outputs
+	 * aside first if any operation needs one */
+	for (k = 0; k < (size_t)nc; k++)
+		if (!cv[k].done && mbc_plan(&cv[k]))
+			break;
+	if (k < (size_t)nc)
+		for (k = 0; k < (size_t)nc; k++)
+			if (mbc_aside(&cv[k]))
+				redo = 1;
+	for (k = 0; k < (size_t)nc; k++) {
+		struct mbc *c = &cv[k];
+		const size_t b = base[k], n = base[k + 1] - b;
+		int e = redo ? ENOMEM : 0;
+		while (!e && !c->done)
+			e = mbc_round(c, w);
+		if (!e)
+			e = mbc_finish(c);
+		mbc_free(c, e);
+		if (!e) {
+			for (i = b; i < b + n; i++)
+				rq[i]->err = ev[i];
+			continue;
+		}
+		/* this operation as it found it: each request on its own,
+		 * with the result its own call would get */
+		for (i = b; i < b + n; i++) {
+			uint32_t zero = 0;
+			int e1 = sess_host(&sv[i], 1);
+			if (!e1)
+				e1 = run_mbufs_(opk[k], &sv[i], 1, &zero, &mv[i],
+						&ev[i], 1);
+			rq[i]->err = e1 ? e1 : ev[i];
+		}
+	}
+	inited = 0;
+ out:
+	/* nothing ran, or the launch failed: every operation as it was */
+	for (k = 0; k < (size_t)inited; k++)
+		mbc_free(&cv[k], 1);
+	table_unlock();
+	count(&g_ns_mbufs, mono_ns() - t0);
+ out_free:
+	free(sv);
+	free(mv);
+	free(rq);
+	free(ev);
+	free(idx);
+	return err ? -1 : 0;
+}
+
 static void pc_run(struct pc_req *list)
 {
 	unsigned ops = 0;
@@ -2052,6 +2336,8 @@ static void pc_run(struct pc_req *list)
 
 	for (r = list; r; r = r->next)
 		ops |= 1u << r->op;
+	if ((ops & (ops - 1)) && pc_run_fused(list, ops) == 0)
+		return;
 	if (ops & (ops - 1)) {
 		pthread_once(&pc_h.once, pc_helper_start);
 		if (pc_h.ok) {

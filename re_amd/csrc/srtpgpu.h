@@ -117,7 +117,8 @@ void  sgpu_set_coop(int on);
 /* the per-packet path (few packets, CTR + HMAC-SHA1 suites): one fused
  * kernel, one packet per workgroup, over jobs, packets, verdicts and saved
  * words in PINNED HOST memory (sgpu_host_alloc: device-accessible), no
- * copies; packets of at most SGPU_SMALL_MAX bytes from their start */
+ * copies; packets of at most SGPU_SMALL_MAX bytes from their start.
+ * prot: 0 unprotect, 1 protect, 2 per job (SJ_PROTECT) */
 #define SGPU_SMALL_MAX 2048
 int   sgpu_run_small(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,

@@ -102,25 +102,31 @@ def oracle_backend(suite, key):
                                                                0)[0])
 
 
-def test_threads_share_launches_exactly(torch_cuda):
+@pytest.mark.parametrize("suites,fuse", [
+    (SUITES, 1), (SUITES, 0),
+    # CTR suites only: lists mixing operations run as one fused launch
+    ([1, 0, 3, 2], 1), ([1, 0, 3, 2], 0)])
+def test_threads_share_launches_exactly(torch_cuda, suites, fuse):
     T = 16
     keys = [bytes((13 * t + i) & 0xff for i in range(46)) for t in range(T)]
     want, got = {}, {}
     for t in range(T):
-        s = SUITES[t % 4]
+        s = suites[t % 4]
         k = keys[t][:P.key_len(s) + P.salt_len(s)]
         run_thread(t, s, k, oracle_backend, want)
     b0, p0 = P.counter("pcbatches"), P.counter("pcpackets")
+    f0 = P.counter("pcfused")
     ths = []
     for t in range(T):
-        s = SUITES[t % 4]
+        s = suites[t % 4]
         k = keys[t][:P.key_len(s) + P.salt_len(s)]
         ths.append(threading.Thread(target=run_thread,
                                     args=(t, s, k, dev_backend, got)))
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join(120)
+    with P.tune(nofuse=0 if fuse else 1):
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(120)
     assert len(got) == T
     for t in range(T):
         for i, (g, w) in enumerate(zip(got[t], want[t])):
@@ -130,3 +136,9 @@ def test_threads_share_launches_exactly(torch_cuda):
     packets = P.counter("pcpackets") - p0
     assert packets == sum(len(v) for v in got.values())
     assert batches <= packets
+    fused = P.counter("pcfused") - f0
+    if not fuse:
+        assert fused == 0
+    elif suites[2] == 3:
+        # 16 threads alternating protect and unprotect: some lists mix them
+        assert fused > 0

@@ -193,6 +193,10 @@ int main(int argc, char **argv)
 		const uint64_t b0 = srtp_gpu_counter("pcbatches"),
 			       p0 = srtp_gpu_counter("pcpackets"),
 			       f0 = srtp_gpu_counter("pcfused"),
+			       sl0 = srtp_gpu_counter("small_launches"),
+			       sy0 = srtp_gpu_counter("small_ns_sync"),
+			       fp0 = srtp_gpu_counter("fused_ns_prep"),
+			       fq0 = srtp_gpu_counter("fused_ns_post"),
 			       mb0 = srtp_gpu_counter("mbufs_ns");
 		for (t = 0; t < T; t++) {
 			js[t].calls = calls / 4 > 1000 ? calls / 4 : 1000;
@@ -210,12 +214,23 @@ int main(int argc, char **argv)
 		 * sync, unpack) against the wall time per launch */
 		printf("%s{\"threads\":%d,\"pairs_per_s\":%.0f,\"errors\":%ld,"
 		       "\"packets_per_launch\":%.1f,\"us_per_launch\":%.1f,"
-		       "\"wall_us_per_launch\":%.1f,\"fused_frac\":%.2f}",
+		       "\"wall_us_per_launch\":%.1f,\"fused_frac\":%.2f,"
+		       "\"small_sync_us\":%.1f,\"fused_prep_us\":%.1f,"
+		       "\"fused_post_us\":%.1f}",
 		       a > 2 ? "," : "", T, T * js[0].calls / ((t1 - t0) * 1e-6),
 		       err, nb ? (srtp_gpu_counter("pcpackets") - p0) / nb : 0,
 		       nb ? (srtp_gpu_counter("mbufs_ns") - mb0) / nb / 1e3 : 0,
 		       nb ? (t1 - t0) / nb : 0,
-		       nb ? (srtp_gpu_counter("pcfused") - f0) / nb : 0);
+		       nb ? (srtp_gpu_counter("pcfused") - f0) / nb : 0,
+		       srtp_gpu_counter("small_launches") > sl0 ?
+		       (srtp_gpu_counter("small_ns_sync") - sy0) / 1e3 /
+		       (double)(srtp_gpu_counter("small_launches") - sl0) : 0,
+		       srtp_gpu_counter("pcfused") > f0 ?
+		       (srtp_gpu_counter("fused_ns_prep") - fp0) / 1e3 /
+		       (double)(srtp_gpu_counter("pcfused") - f0) : 0,
+		       srtp_gpu_counter("pcfused") > f0 ?
+		       (srtp_gpu_counter("fused_ns_post") - fq0) / 1e3 /
+		       (double)(srtp_gpu_counter("pcfused") - f0) : 0);
 		free(js);
 		free(th);
 	}

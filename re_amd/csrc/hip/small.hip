@@ -1,5 +1,6 @@
 /*
- * small.hip -- the per-packet path's fused kernel (AES-CM + HMAC-SHA1).
+ * small.hip -- the per-packet path's fused kernel (AES-CM + HMAC-SHA1,
+ * AES-GCM).
  *
  * Every unchanged libre caller protects one mbuf per srtp_encrypt() call
  * (reference src/srtp/srtp.c:183-285; unprotect :288-432).  Concurrent
@@ -22,6 +23,9 @@
 #include "kern_common.h"
 
 #define SMALL_MAX SGPU_SMALL_MAX_BYTES  /* from a packet's start (host-checked) */
+#ifndef SMALL_WK
+#define SMALL_WK 1      /* inner schedule formed up front (sched_lds) */
+#endif
 
 namespace {
 
@@ -168,6 +172,118 @@ __device__ __forceinline__ void sha1_compress_lat(uint32_t h[5],
 	h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }
 
+/* The inner hash's message schedule depends on the message alone, so the
+ * workgroup forms it for every block up front, one block per thread:
+ * WK[80 k + i] = W_i + K_i of inner block k (FIPS 180-4 6.1.2; the
+ * message buf[0, A) || trailer? || padding || bit length).  The hashing
+ * lane then spends five instructions a round (rotl(a, 5), f, e + WK, one
+ * v_add3, rotl(b, 30)) instead of eight -- one wave issues one instruction
+ * per four cycles whatever its type, so the count is the latency. */
+#define SMALL_NB ((SMALL_MAX + 4u + 9u + 63u) / 64u)
+
+__device__ __forceinline__ uint32_t sha_k(int i)
+{
+	return i < 20 ? 0x5a827999u : i < 40 ? 0x6ed9eba1u
+	     : i < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;
+}
+
+__device__ __forceinline__ uint32_t mac_blocks(uint32_t A, bool trail)
+{
+	return (A + (trail ? 4u : 0u) + 9u + 63u) / 64u;
+}
+
+__device__ __forceinline__ void sched_lds(const uint32_t *buf, uint32_t A,
+					  bool trail, uint32_t trailer,
+					  uint32_t *WK, uint32_t t0,
+					  uint32_t step)
+{
+	const uint64_t X = trail ? ((uint64_t)trailer << 32 | 0x80000000u)
+				 : 0x8000000000000000ull;
+	const uint32_t tl = trail ? 4u : 0u;
+	const uint32_t nb = mac_blocks(A, trail);
+	const uint64_t bitlen = (uint64_t)(64u + A + tl) * 8u;
+	for (uint32_t k = t0; k < nb; k += step) {
+		uint32_t w[16], o[80];
+#pragma unroll
+		for (int g = 0; g < 16; g++) {
+			const uint32_t gw = 16u * k + (uint32_t)g;
+			const uint32_t v = gw < SMALL_MAX / 4 ? buf[gw] : 0u;
+			w[g] = msg_word(gw, bswap32(v), A, X);
+		}
+		if (k + 1 == nb) {
+			w[14] = (uint32_t)(bitlen >> 32);
+			w[15] = (uint32_t)bitlen;
+		}
+#pragma unroll
+		for (int i = 0; i < 80; i++) {
+			if (i >= 16)
+				w[i & 15] = rotl32(xor3(w[(i + 13) & 15],
+							w[(i + 8) & 15],
+							w[(i + 2) & 15]) ^ w[i & 15], 1);
+			o[i] = w[i & 15] + sha_k(i);
+		}
+		uint4 *dst = (uint4 *)(WK + 80u * k);
+#pragma unroll
+		for (int g = 0; g < 20; g++)
+			dst[g] = make_uint4(o[4 * g], o[4 * g + 1], o[4 * g + 2],
+					    o[4 * g + 3]);
+	}
+}
+
+__device__ __forceinline__ void sha1_compress_wk(uint32_t h[5],
+						 const uint32_t *wk)
+{
+	uint32_t x[80];
+#pragma unroll
+	for (int g = 0; g < 20; g++) {
+		const uint4 v = ((const uint4 *)wk)[g];
+		x[4 * g] = v.x; x[4 * g + 1] = v.y;
+		x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
+	}
+	uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#define SW(i, f)                                                             \
+	do {                                                                 \
+		const uint32_t t = add3(rotl32(a, 5), (f), e + x[i]);        \
+		e = d; d = c; c = rotl32(b, 30); b = a; a = t;               \
+	} while (0)
+#pragma unroll
+	for (int i = 0; i < 20; i++)
+		SW(i, sha_ch(b, c, d));
+#pragma unroll
+	for (int i = 20; i < 40; i++)
+		SW(i, xor3(b, c, d));
+#pragma unroll
+	for (int i = 40; i < 60; i++)
+		SW(i, sha_maj(b, c, d));
+#pragma unroll
+	for (int i = 60; i < 80; i++)
+		SW(i, xor3(b, c, d));
+#undef SW
+	h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+/* HMAC-SHA1 over the scheduled inner blocks, then the outer block */
+__device__ __forceinline__ void hmac_wk(const uint32_t *WK, uint32_t nb,
+					const struct sgpu_comp *cp,
+					uint32_t h[5])
+{
+	h[0] = cp->ipad[0]; h[1] = cp->ipad[1]; h[2] = cp->ipad[2];
+	h[3] = cp->ipad[3]; h[4] = cp->ipad[4];
+#pragma unroll 1
+	for (uint32_t k = 0; k < nb; k++)
+		sha1_compress_wk(h, WK + 80u * k);
+	uint32_t w[16];
+	w[0] = h[0]; w[1] = h[1]; w[2] = h[2]; w[3] = h[3]; w[4] = h[4];
+	w[5] = 0x80000000u;
+#pragma unroll
+	for (int q = 6; q < 15; q++)
+		w[q] = 0;
+	w[15] = (64u + 20u) * 8u;
+	h[0] = cp->opad[0]; h[1] = cp->opad[1]; h[2] = cp->opad[2];
+	h[3] = cp->opad[3]; h[4] = cp->opad[4];
+	sha1_compress_lat(h, w);
+}
+
 /* HMAC-SHA1 (hmac.c:78-95 via the ipad/opad midstates) of the message
  * buf[0, A) || trailer? -- one lane; digest in h.  Whole 64-byte chunks
  * of [0, A) go straight in, the next chunk's words read from LDS ahead of
@@ -242,6 +358,297 @@ __device__ __forceinline__ void hmac_lds(const uint32_t *buf,
 	sha1_compress_lat(h, w);
 }
 
+
+/* ---- AES-GCM (AEAD_AES_128_GCM / AEAD_AES_256_GCM, aes.c:136-249) ----
+ * The workgroup makes the keystream (counter blocks 2.. of J0 = IV || 1,
+ * srtp_iv_calc_gcm misc.c:93-105) and wave 0 the GHASH of
+ * AAD || C || lengths (SP 800-38D 6.4) in three steps instead of one
+ * 77-block chain: lanes 0..m-1 run Horner over m contiguous chunks (the
+ * first the short one, the others c blocks each) with the 8-bit table of
+ * H, lane m forms H^c meanwhile; the table of H^c is built; lane 0 folds
+ * the chunk sums by Horner in H^c.  Results as k_gcmu's: the payload is
+ * always transformed, the tag compared (SV_TAG_OK) or written. */
+
+/* M[b] = b * V for all bytes b from the 4-bit table T4 (gh8_fill, one
+ * replica: entry b at b) */
+__device__ __forceinline__ uint4 m8_entry(const uint4 *T4, uint32_t b)
+{
+	const uint4 L = T4[b & 15u], H = T4[b >> 4];
+	const uint32_t m = L.w & 15u;
+	const uint32_t red = (m ^ (m << 5) ^ (m << 6) ^ (m << 7)) << 21;
+	return make_uint4((L.x >> 4) ^ red ^ H.x,
+			  __builtin_amdgcn_alignbit(L.x, L.y, 4) ^ H.y,
+			  __builtin_amdgcn_alignbit(L.y, L.z, 4) ^ H.z,
+			  __builtin_amdgcn_alignbit(L.z, L.w, 4) ^ H.w);
+}
+
+/* the 4-bit table entry q * V (OpenSSL gcm_init_4bit: V at 8, V x at 4,
+ * V x^2 at 2, V x^3 at 1, the rest XORs) */
+__device__ __forceinline__ uint4 t4_entry(uint4 v, uint32_t q)
+{
+	uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+	for (int bit = 8; bit >= 1; bit >>= 1) {
+		if (q & (uint32_t)bit) {
+			acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+		}
+		const uint32_t t = (v.w & 1u) ? 0xe1000000u : 0u;
+		v.w = __builtin_amdgcn_alignbit(v.z, v.w, 1);
+		v.z = __builtin_amdgcn_alignbit(v.y, v.z, 1);
+		v.y = __builtin_amdgcn_alignbit(v.x, v.y, 1);
+		v.x = (v.x >> 1) ^ t;
+	}
+	return acc;
+}
+
+/* x = x * V with V's 8-bit table M (ghash8_mul, one replica) */
+__device__ __forceinline__ void gmul8(uint32_t x[4], const uint4 *M)
+{
+	uint32_t R[8];
+#pragma unroll
+	for (int q = 3; q >= 0; q--) {
+		uint4 Mw[4];
+#pragma unroll
+		for (int w = 0; w < 4; w++)
+			Mw[w] = M[(x[w] >> (8 * (3 - q))) & 255u];
+		const uint32_t A0 = Mw[0].x;
+		const uint32_t A1 = Mw[0].y ^ Mw[1].x;
+		const uint32_t A2 = xor3(Mw[0].z, Mw[1].y, Mw[2].x);
+		const uint32_t A3 = xor3(Mw[0].w, Mw[1].z, Mw[2].y) ^ Mw[3].x;
+		const uint32_t A4 = xor3(Mw[1].w, Mw[2].z, Mw[3].y);
+		const uint32_t A5 = Mw[2].w ^ Mw[3].z;
+		const uint32_t A6 = Mw[3].w;
+		if (q == 3) {
+			R[0] = A0; R[1] = A1; R[2] = A2; R[3] = A3;
+			R[4] = A4; R[5] = A5; R[6] = A6; R[7] = 0;
+		}
+		else {
+			R[7] = __builtin_amdgcn_alignbit(R[6], R[7], 8);
+			R[6] = __builtin_amdgcn_alignbit(R[5], R[6], 8) ^ A6;
+			R[5] = __builtin_amdgcn_alignbit(R[4], R[5], 8) ^ A5;
+			R[4] = __builtin_amdgcn_alignbit(R[3], R[4], 8) ^ A4;
+			R[3] = __builtin_amdgcn_alignbit(R[2], R[3], 8) ^ A3;
+			R[2] = __builtin_amdgcn_alignbit(R[1], R[2], 8) ^ A2;
+			R[1] = __builtin_amdgcn_alignbit(R[0], R[1], 8) ^ A1;
+			R[0] = (R[0] >> 8) ^ A0;
+		}
+	}
+	const uint32_t u0 = R[4], u1 = R[5], u2 = R[6], u3 = R[7];
+	x[0] = xor3(xor3(R[0], u0, u0 >> 1), u0 >> 2, u0 >> 7);
+	x[1] = xor3(xor3(R[1], u1, __builtin_amdgcn_alignbit(u0, u1, 1)),
+		    __builtin_amdgcn_alignbit(u0, u1, 2),
+		    __builtin_amdgcn_alignbit(u0, u1, 7));
+	x[2] = xor3(xor3(R[2], u2, __builtin_amdgcn_alignbit(u1, u2, 1)),
+		    __builtin_amdgcn_alignbit(u1, u2, 2),
+		    __builtin_amdgcn_alignbit(u1, u2, 7));
+	x[3] = xor3(xor3(R[3], u3, __builtin_amdgcn_alignbit(u2, u3, 1)),
+		    __builtin_amdgcn_alignbit(u2, u3, 2),
+		    __builtin_amdgcn_alignbit(u2, u3, 7));
+}
+
+/* LDS written by some lanes of this wave, read by others next */
+__device__ __forceinline__ void wave_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct gcm_in {
+	const uint32_t *buf;    /* the packet (LDS) */
+	uint32_t A, na, nc, c_off, c_end, c_len, aad_total;
+	uint64_t Xtr;           /* trailer word for msg_word (SRTCP) */
+};
+
+/* GHASH input block i (BE words): AAD, ciphertext, lengths */
+__device__ __forceinline__ void g_block(const gcm_in &g, uint32_t i,
+					uint32_t w[4])
+{
+	if (i < g.na) {
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t gw = 4u * i + (uint32_t)q;
+			const uint32_t v = gw < SMALL_MAX / 4 ? g.buf[gw] : 0u;
+			w[q] = msg_word(gw, bswap32(v), g.A, g.Xtr);
+		}
+	}
+	else if (i < g.na + g.nc) {
+		const uint32_t p = g.c_off + 16u * (i - g.na);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t bp = p + 4u * (uint32_t)q;
+			uint32_t v = bp < g.c_end ? bswap32(g.buf[bp / 4u]) : 0u;
+			const uint32_t n = bp < g.c_end ? g.c_end - bp : 0u;
+			if (n < 4u)
+				v &= (uint32_t)(0xFFFFFFFF00000000ull >> (8u * n));
+			w[q] = v;
+		}
+	}
+	else {
+		const uint64_t al = (uint64_t)g.aad_total * 8u;
+		const uint64_t cl = (uint64_t)g.c_len * 8u;
+		w[0] = (uint32_t)(al >> 32); w[1] = (uint32_t)al;
+		w[2] = (uint32_t)(cl >> 32); w[3] = (uint32_t)cl;
+	}
+}
+
+/* GHASH by wave 0 (lane < 64); lane 0 returns it in X.  M1: H's table;
+ * scratch: Mc (256 entries), Ys (65), T4c (16) */
+__device__ __forceinline__ void ghash_wave(const gcm_in &g, const uint4 *M1,
+					   uint4 H, uint4 *Mc, uint4 *Ys,
+					   uint4 *T4c, uint32_t lane,
+					   uint32_t X[4])
+{
+	const uint32_t n = g.na + g.nc + 1u;
+	const uint32_t c = (n + 7u) / 8u;               /* chunk length */
+	const uint32_t m = (n + c - 1u) / c;            /* chunks */
+	const uint32_t n0 = n - c * (m - 1u);           /* the first's */
+	uint32_t x[4] = {0, 0, 0, 0};
+	if (lane < m) {
+		const uint32_t b0 = lane ? n0 + c * (lane - 1u) : 0u;
+		const uint32_t b1 = lane ? b0 + c : n0;
+		for (uint32_t b = b0; b < b1; b++) {
+			uint32_t w[4];
+			g_block(g, b, w);
+			x[0] ^= w[0]; x[1] ^= w[1]; x[2] ^= w[2]; x[3] ^= w[3];
+			gmul8(x, M1);
+		}
+	}
+	else if (lane == m) {
+		x[0] = H.x; x[1] = H.y; x[2] = H.z; x[3] = H.w;
+		for (uint32_t k = 1; k < c; k++)
+			gmul8(x, M1);
+	}
+	if (lane <= m)
+		Ys[lane] = make_uint4(x[0], x[1], x[2], x[3]);
+	wave_sync();
+	if (m > 1) {
+		if (lane < 16)
+			T4c[lane] = t4_entry(Ys[m], lane);
+		wave_sync();
+		for (uint32_t b = lane; b < 256u; b += 64u)
+			Mc[b] = m8_entry(T4c, b);
+		wave_sync();
+	}
+	if (lane == 0) {
+		uint4 y = Ys[0];
+		x[0] = y.x; x[1] = y.y; x[2] = y.z; x[3] = y.w;
+		for (uint32_t k = 1; k < m; k++) {
+			gmul8(x, Mc);
+			y = Ys[k];
+			x[0] ^= y.x; x[1] ^= y.y; x[2] ^= y.z; x[3] ^= y.w;
+		}
+		X[0] = x[0]; X[1] = x[1]; X[2] = x[2]; X[3] = x[3];
+	}
+}
+
+/* one GCM job by the workgroup; the packet is in buf (nw_out words,
+ * written back by the caller), returns the verdict (thread 0) */
+__device__ uint8_t gcm_small(const struct sgpu_job &j,
+			     const struct sgpu_comp *cp, bool prot,
+			     const uint32_t *T, const uint32_t *rk,
+			     uint32_t *buf, uint32_t *ksb, uint4 *gl,
+			     uint32_t tid)
+{
+	/* gl: M1[256] | Mc[256] | Ys[65] | T4c[16] | X | EJ0 */
+	uint4 *M1 = gl, *Mc = gl + 256, *Ys = gl + 512, *T4c = gl + 577;
+	uint4 *sX = gl + 593, *sE = gl + 594;
+	const uint32_t nr = cp->nr;
+	const bool trail = (j.flags & SJ_TRAILER) != 0;
+	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
+	gcm_in g;
+	g.buf = buf;
+	g.A = j.a_len;
+	g.aad_total = j.a_len + (trail ? 4u : 0u);
+	g.na = (g.aad_total + 15u) / 16u;
+	g.c_off = j.c_off;
+	g.c_len = do_cipher ? j.c_len : 0u;
+	g.c_end = g.c_off + g.c_len;
+	g.nc = (g.c_len + 15u) / 16u;
+	g.Xtr = trail ? ((uint64_t)j.trailer << 32) : 0ull;
+	/* srtp_iv_calc_gcm: IV = k_s ^ (0^16 || SSRC || ROC || SEQ) */
+	uint32_t iv[4];
+	{
+		const uint4 ks = *(const uint4 *)cp->k_s;
+		const uint32_t be0 = (j.ssrc >> 16) & 0xffffu;
+		const uint32_t be1 = ((j.ssrc & 0xffffu) << 16) | (j.ixhi >> 16);
+		const uint32_t be2 = ((j.ixhi & 0xffffu) << 16) |
+				     (j.ixlo & 0xffffu);
+		iv[0] = ks.x ^ bswap32(be0);
+		iv[1] = ks.y ^ bswap32(be1);
+		iv[2] = ks.z ^ bswap32(be2);
+		iv[3] = 0;
+	}
+	for (uint32_t b = tid; b < 256u; b += blockDim.x)
+		M1[b] = m8_entry((const uint4 *)cp->htab, b);
+	const uint4 H = *(const uint4 *)cp->htab[8];
+	__syncthreads();
+	/* data block b uses counter b + 2: region_ks's block index is the
+	 * 64-bit counter offset, so start the region 32 bytes early */
+	const uint32_t lane = tid & 63u;
+	if (prot) {
+		if (do_cipher)
+			region_ks(T, rk, nr, iv, g.c_off - 32u, g.c_end, buf,
+				  true, tid + 2u, blockDim.x);
+		__syncthreads();
+		if (tid < 64u)
+			ghash_wave(g, M1, H, Mc, Ys, T4c, lane, (uint32_t *)sX);
+		else if (tid == 64u) {
+			uint32_t e[4];
+			ks_block(T, rk, nr, iv, 1u, e);
+			*sE = make_uint4(e[0], e[1], e[2], e[3]);
+		}
+	}
+	else {
+		if (tid < 64u)
+			ghash_wave(g, M1, H, Mc, Ys, T4c, lane, (uint32_t *)sX);
+		else {
+			if (do_cipher)
+				region_ks(T, rk, nr, iv, g.c_off - 32u, g.c_end,
+					  ksb, false, tid - 64u + 2u,
+					  blockDim.x - 64u);
+			if (tid == 64u) {
+				uint32_t e[4];
+				ks_block(T, rk, nr, iv, 1u, e);
+				*sE = make_uint4(e[0], e[1], e[2], e[3]);
+			}
+		}
+	}
+	__syncthreads();
+	uint8_t vd = do_cipher ? SV_CIPHERED : 0;
+	/* tag = GHASH ^ E(K, J0) */
+	const uint4 X = *sX, E = *sE;
+	const uint32_t t[4] = {X.x ^ bswap32(E.x), X.y ^ bswap32(E.y),
+			       X.z ^ bswap32(E.z), X.w ^ bswap32(E.w)};
+	uint8_t *tp = (uint8_t *)buf + j.tag_off;
+	if (prot) {
+		if (tid == 0) {
+			for (int q = 0; q < 16; q++)
+				tp[q] = (uint8_t)(t[q >> 2] >> (24 - 8 * (q & 3)));
+			if (j.flags & SJ_STORE_TRAIL) {
+				uint8_t *tr = (uint8_t *)buf + j.t_off;
+				tr[0] = (uint8_t)(j.trailer >> 24);
+				tr[1] = (uint8_t)(j.trailer >> 16);
+				tr[2] = (uint8_t)(j.trailer >> 8);
+				tr[3] = (uint8_t)j.trailer;
+			}
+		}
+	}
+	else {
+		uint32_t diff = 0;
+		for (int q = 0; q < 16; q++)
+			diff |= tp[q] ^ (uint8_t)(t[q >> 2] >> (24 - 8 * (q & 3)));
+		if (diff == 0)
+			vd |= SV_TAG_OK;
+		__syncthreads();        /* every thread compared the tag */
+		if (do_cipher)
+			for (uint32_t w = g.c_off / 4u + tid;
+			     w < (g.c_end + 3u) / 4u; w += blockDim.x)
+				buf[w] ^= ksb[w];
+	}
+	return vd;
+}
+
 } /* namespace */
 
 /* MODE 0 unprotect, 1 protect, 2 per job (SJ_PROTECT): the operations of
@@ -253,6 +660,8 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	__shared__ uint32_t rk[60];     /* plain round keys */
 	__shared__ __attribute__((aligned(16))) uint32_t buf[SMALL_MAX / 4];
 	__shared__ __attribute__((aligned(16))) uint32_t ksb[SMALL_MAX / 4];
+	__shared__ __attribute__((aligned(16))) uint32_t WK[SMALL_NB * 80];
+	static_assert(SMALL_NB * 80 * 4 >= 595 * 16, "gcm_small scratch");
 	__shared__ uint32_t s_tag_ok;
 	const uint32_t i = blockIdx.x, tid = threadIdx.x;
 	if (i >= a.njobs)
@@ -269,6 +678,7 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	const uint32_t nr = cp->nr;
 	T[tid] = a.t0[tid];
 
+	const bool gcm = (j.flags & SJ_GCM) != 0;
 	const bool do_cipher = (j.flags & SJ_CIPHER) != 0;
 	const bool do_hmac = (j.flags & SJ_HMAC) != 0;
 	const bool trail = (j.flags & SJ_TRAILER) != 0;
@@ -276,21 +686,21 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	const bool roc_at_tag = !PROT && (j.flags & SJ_ROC_AT_TAG);
 	const uint32_t c_off = j.c_off;
 	const uint32_t c_end = do_cipher ? j.c_off + j.c_len : 0u;
-	const uint32_t A = do_hmac ? j.a_len : 0u;
-	const uint32_t tag_len = do_hmac ? cp->tag_len : 0u;
+	const uint32_t A = (do_hmac || gcm) ? j.a_len : 0u;
+	const uint32_t tag_len = do_hmac ? cp->tag_len : gcm ? 16u : 0u;
 	const bool store_ct = do_cipher && (PROT || cipher_if_ok || !do_hmac);
 	/* bytes read: the MAC input and cipher region, unprotect's tag;
 	 * bytes written back: those plus protect's tag and trailer */
 	uint32_t in_len = max(c_end, A);
 	uint32_t out_len = in_len;
 	if (PROT) {
-		if (do_hmac)
+		if (tag_len)
 			out_len = max(out_len, j.tag_off + tag_len);
 		if (j.flags & SJ_STORE_TRAIL)
 			out_len = max(out_len, j.t_off + 4u);
 	}
 	else {
-		if (do_hmac)
+		if (tag_len)
 			in_len = max(in_len, j.tag_off + tag_len);
 		if (roc_at_tag)
 			in_len = max(in_len, j.tag_off + 4u);
@@ -318,7 +728,10 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 
 	uint8_t vd = 0;
 	uint32_t h[5];
-	if (PROT) {
+	if (gcm) {
+		vd = gcm_small(j, cp, PROT, T, rk, buf, ksb, (uint4 *)WK, tid);
+	}
+	else if (PROT) {
 		/* the MAC covers the ciphertext: keystream first.  (Hashing
 		 * each chunk as soon as its blocks are done, the other waves
 		 * applying the keystream meanwhile, measured slower: 41.6 vs
@@ -328,9 +741,18 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 			region_ks(T, rk, nr, iv, c_off, c_end, buf, true, tid,
 				  blockDim.x);
 		__syncthreads();
+		if (do_hmac && SMALL_WK) {
+			sched_lds(buf, A, trail, j.trailer, WK, tid, blockDim.x);
+			__syncthreads();
+		}
 		if (tid == 0 && do_hmac) {
-			const ks_wait none = {nullptr, 0, 0};
-			hmac_lds(buf, cp, A, trail, j.trailer, h, none);
+			if (SMALL_WK) {
+				hmac_wk(WK, mac_blocks(A, trail), cp, h);
+			}
+			else {
+				const ks_wait none = {nullptr, 0, 0};
+				hmac_lds(buf, cp, A, trail, j.trailer, h, none);
+			}
 			uint8_t *tp = (uint8_t *)buf + j.tag_off;
 			for (uint32_t q = 0; q < tag_len; q++)
 				tp[q] = (uint8_t)(h[q >> 2] >> (24 - 8 * (q & 3)));
@@ -346,11 +768,20 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	else {
 		/* the MAC covers the received ciphertext: lane 0 hashes while
 		 * the other waves make the keystream */
+		if (do_hmac && SMALL_WK) {
+			sched_lds(buf, A, trail, j.trailer, WK, tid, blockDim.x);
+			__syncthreads();
+		}
 		if (tid == 0) {
 			uint32_t ok = 1;
-			if (do_hmac) {
+			if (do_hmac && SMALL_WK) {
+				hmac_wk(WK, mac_blocks(A, trail), cp, h);
+			}
+			else if (do_hmac) {
 				const ks_wait none = {nullptr, 0, 0};
 				hmac_lds(buf, cp, A, trail, j.trailer, h, none);
+			}
+			if (do_hmac) {
 				const uint8_t *tp = (const uint8_t *)buf + j.tag_off;
 				uint32_t diff = 0;
 				for (uint32_t q = 0; q < tag_len; q++)

@@ -1417,6 +1417,40 @@ extern "C" int sgpu_parse_prologue(const uint8_t *arena, uint64_t arena_size,
 	return herr(hipGetLastError(), "k_parse launch");
 }
 
+/* srtp_rx_index_dev: one word per parsed packet for the host's receiver
+ * walk -- seq | ok << 16 | (ssrc != ssrc0) << 17 | wide << 23 |
+ * (res & 255) << 24 (wide: res outside 0..255, sent separately) */
+__global__ void k_rx_pack(const struct sgpu_hdr *__restrict__ hd,
+			  const int32_t *__restrict__ res, uint32_t ssrc0,
+			  uint32_t *__restrict__ out, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const struct sgpu_hdr h = hd[i];
+	const int32_t r = res[i];
+	const bool ok = h.hdr_len != 0xffffffffu;
+	uint32_t v = ok ? (uint32_t)h.seq | 1u << 16 : 0u;
+	if (ok && h.ssrc != ssrc0)
+		v |= 1u << 17;
+	if (r < 0 || r > 255)
+		v |= 1u << 23;
+	else
+		v |= (uint32_t)r << 24;
+	out[i] = v;
+}
+
+extern "C" int sgpu_rx_pack(const struct sgpu_hdr *hd, const int32_t *res,
+			    uint32_t ssrc0, uint32_t *out, uint32_t n,
+			    void *stream)
+{
+	if (!n)
+		return 0;
+	hipLaunchKernelGGL(k_rx_pack, dim3((n + 255) / 256), dim3(256), 0,
+			   (hipStream_t)stream, hd, res, ssrc0, out, n);
+	return herr(hipGetLastError(), "k_rx_pack launch");
+}
+
 __global__ void k_store_words(uint8_t *__restrict__ arena,
 			      const uint32_t *__restrict__ offs,
 			      const uint32_t *__restrict__ vals, uint32_t n)

@@ -152,6 +152,12 @@ static struct {
 	int nosmall;            /* RE_SRTP_NOSMALL: the per-packet path's small
 				   CTR launches take the general kernels
 				   with copies (not sgpu_run_small) */
+	long pcrunners;         /* srtp_gpu_tune pcrunners: per-packet runners
+				   at once (default PC_RUNNERS, at most
+				   PC_SLOTS) */
+	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
+				   per-packet caller spins before it sleeps
+				   (default 1000) */
 	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
 				   shared per-packet launch run as separate
 				   launches (helper thread), not one */
@@ -204,6 +210,8 @@ static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
 /* the per-packet path's small launches and where their time goes (ns):
  * the host work of run_mbufs_, the launch call, the synchronisation */
 static uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
+/* pc_run_fused: host time before the launch and after the sync (ns) */
+static uint64_t g_ns_fused_prep, g_ns_fused_post;
 
 static uint64_t mono_ns(void)
 {
@@ -255,6 +263,10 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_ns_small_launch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "small_ns_sync"))
 		return __atomic_load_n(&g_ns_small_sync, __ATOMIC_RELAXED);
+	if (!strcmp(name, "fused_ns_prep"))
+		return __atomic_load_n(&g_ns_fused_prep, __ATOMIC_RELAXED);
+	if (!strcmp(name, "fused_ns_post"))
+		return __atomic_load_n(&g_ns_fused_post, __ATOMIC_RELAXED);
 	if (!strcmp(name, "mbufs_ns"))
 		return __atomic_load_n(&g_ns_mbufs, __ATOMIC_RELAXED);
 	if (!strcmp(name, "prof_voided"))
@@ -298,6 +310,10 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nosmall = value > 0;
 	else if (!strcmp(name, "nofuse"))
 		g_env.nofuse = value > 0;
+	else if (!strcmp(name, "pcrunners"))
+		g_env.pcrunners = value > 0 ? value : 0;
+	else if (!strcmp(name, "pcspin"))
+		g_env.pcspin = value > 0 ? value : 0;
 	else if (!strcmp(name, "trace"))
 		g_env.trace = value > 0;
 	else if (!strcmp(name, "times"))
@@ -1333,8 +1349,13 @@ static struct ws *ws_new(void)
 	return w;
 }
 
+/* a per-packet runner's slot workspace while it runs (pc_slot_ws) */
+static __thread struct ws *t_ws_use;
+
 static struct ws *ws_get(void)
 {
+	if (t_ws_use)
+		return t_ws_use;
 	if (!t_ws)
 		t_ws = ws_new();
 	return t_ws;
@@ -1539,14 +1560,6 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 		collect_rec(&E->rec[w->cls_idx[k]], v[k], sv[k]);
 }
 
-/*
- * The per-packet path's round (few packets, CTR + HMAC-SHA1 suites): the
- * staged packets and the jobs stay in pinned host memory and one fused
- * kernel reads and writes them there (sgpu_run_small, small.hip) -- no
- * copies; the verdicts land where round_collect reads them.  0 with *pm
- * jobs, errno, or -1: not eligible (a GCM job, a packet past
- * SGPU_SMALL_MAX, more than SGPU_COOP_MAX jobs) -- nothing launched.
- */
 /* #jobs of a planned round if the small kernel can take all of them,
  * else (size_t)-1 */
 static size_t small_fits(const struct engine *E)
@@ -1556,7 +1569,7 @@ static size_t small_fits(const struct engine *E)
 		const struct rec *r = &E->rec[i];
 		if (!r->need_run)
 			continue;
-		if ((r->job.flags & (SJ_GCM | SJ_UNDO)) ||
+		if ((r->job.flags & SJ_UNDO) ||
 		    r->ext_end - E->pi[i].start > SGPU_SMALL_MAX ||
 		    r->in_end - E->pi[i].start > SGPU_SMALL_MAX)
 			return (size_t)-1;
@@ -1565,6 +1578,14 @@ static size_t small_fits(const struct engine *E)
 	return need;
 }
 
+/*
+ * The per-packet path's round (few packets, every suite): the
+ * staged packets and the jobs stay in pinned host memory and one fused
+ * kernel reads and writes them there (sgpu_run_small, small.hip) -- no
+ * copies; the verdicts land where round_collect reads them.  0 with *pm
+ * jobs, errno, or -1: not eligible (an undo job, a packet past
+ * SGPU_SMALL_MAX, more than SGPU_COOP_MAX jobs) -- nothing launched.
+ */
 static int round_small(struct ws *w, struct engine *E, uint64_t asz,
 		       const uint32_t *joff, int prot, uint32_t *pm,
 		       void *stream)
@@ -1844,7 +1865,7 @@ static int mbc_round(struct mbc *c, struct ws *w)
 		return err;
 	mbc_stage(c, w->stage.h);
 	{
-		/* few packets of the CTR suites: the fused kernel over the
+		/* few packets: the fused kernel over the
 		 * pinned staging memory itself */
 		const uint64_t t0 = mono_ns();
 		rs = round_small(w, E, bytes, c->soff, c->prot, &m, w->stream);
@@ -2000,6 +2021,8 @@ struct pc_req {
 	struct mbuf *mb;
 	int err;
 	int state;              /* PC_*, atomic: the owner waits on it */
+	int slot;               /* PC_RUN: the runner slot handed over */
+	struct pc_req *list;    /* ... and the queue it runs (from this one) */
 };
 
 static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -2016,10 +2039,12 @@ static void pc_wake(int *state, int v)
 
 static int pc_wait(int *state)
 {
-	int spin, v;
+	long spin;
+	int v;
 	/* a short spin, then sleep: many callers spinning on fewer cores
 	 * would take the CPU from the runner and its helper */
-	for (spin = 0; spin < 1000; spin++) {
+	const long nspin = g_env.pcspin ? g_env.pcspin : 1000;
+	for (spin = 0; spin < nspin; spin++) {
 		v = __atomic_load_n(state, __ATOMIC_ACQUIRE);
 		if (v != PC_QUEUED)
 			return v;
@@ -2098,52 +2123,66 @@ static void pc_run_op(struct pc_req *list, int op)
 }
 
 /*
+ * Runner slots: up to pcrunners (default PC_RUNNERS) runners at once, each
+ * with its slot's workspace (HIP stream, pinned pools) and helper thread,
+ * so the next list is planned and launched while the previous one is on
+ * the GPU.  Concurrent lists hold distinct sessions too (a session's one
+ * owner thread has one call in flight).
+ *
  * A list usually mixes operations (callers alternate srtp_encrypt and
- * srtp_decrypt): each operation is its own batch, and the batches of two
- * operations run at once -- one on a persistent helper thread (its own
- * workspace and HIP stream), the rest on the runner -- instead of one
- * GPU round trip after the other.  The sessions of one list are distinct
- * (one request per calling thread, one thread per struct srtp), so the
- * operations share no stream state.
+ * srtp_decrypt).  Lists the small kernel takes run as one launch
+ * (pc_run_fused); otherwise each operation is its own batch, and the
+ * batches of two operations run at once -- one on the slot's persistent
+ * helper thread (its own workspace and HIP stream), the rest on the
+ * runner -- instead of one GPU round trip after the other.
  */
-static struct {
-	pthread_once_t once;
-	int ok;
-	int state;              /* 0 idle, 1 posted, 2 done (futex word) */
-	struct pc_req *list;
-	int op;
-} pc_h = {PTHREAD_ONCE_INIT, 0, 0, NULL, 0};
+/* runners 1..4 at 64 threads: 230, 278, 306, 326 K pairs/s
+ * (profiles/r04_percall_runners.txt) */
+enum { PC_SLOTS = 4, PC_RUNNERS = 4 };
+
+static struct pc_slot {
+	struct ws *ws;
+	int hok;                /* helper thread running */
+	int hstate;             /* 0 idle, 1 posted, 2 done (futex word) */
+	struct pc_req *hlist;
+	int hop;
+} pc_slots[PC_SLOTS];
+static unsigned pc_slot_used;   /* under pc_lock */
 
 static void *pc_helper(void *arg)
 {
-	(void)arg;
+	struct pc_slot *sl = arg;
 	for (;;) {
-		while (__atomic_load_n(&pc_h.state, __ATOMIC_ACQUIRE) != 1)
-			(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAIT_PRIVATE,
-				      __atomic_load_n(&pc_h.state,
+		while (__atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE) != 1)
+			(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAIT_PRIVATE,
+				      __atomic_load_n(&sl->hstate,
 						      __ATOMIC_RELAXED),
 				      NULL, NULL, 0);
-		pc_run_op(pc_h.list, pc_h.op);
-		__atomic_store_n(&pc_h.state, 2, __ATOMIC_RELEASE);
-		(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAKE_PRIVATE, 1,
+		pc_run_op(sl->hlist, sl->hop);
+		__atomic_store_n(&sl->hstate, 2, __ATOMIC_RELEASE);
+		(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAKE_PRIVATE, 1,
 			      NULL, NULL, 0);
 	}
 	return NULL;
 }
 
-static void pc_helper_start(void)
+/* the slot's helper, started on first use (only its runner calls this) */
+static int pc_helper_ok(struct pc_slot *sl)
 {
-	pthread_t t;
-	pthread_attr_t a;
-	pthread_attr_init(&a);
-	pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
-	pc_h.ok = pthread_create(&t, &a, pc_helper, NULL) == 0;
-	pthread_attr_destroy(&a);
+	if (!sl->hok) {
+		pthread_t t;
+		pthread_attr_t a;
+		pthread_attr_init(&a);
+		pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
+		sl->hok = pthread_create(&t, &a, pc_helper, sl) == 0 ? 1 : -1;
+		pthread_attr_destroy(&a);
+	}
+	return sl->hok > 0;
 }
 
 /*
- * A list mixing operations whose packets all fit the small kernel (the CTR
- * suites, <= SGPU_SMALL_MAX bytes): every operation plans its first round
+ * A list mixing operations whose packets all fit the small kernel (<=
+ * SGPU_SMALL_MAX bytes): every operation plans its first round
  * on the host and all of them run as ONE launch of the fused kernel (the
  * protect or unprotect body per job, by SJ_PROTECT) -- one GPU round trip
  * for the whole list instead of one per operation on two streams.  Later
@@ -2163,6 +2202,7 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 	size_t base[5], need[4], tot = 0, bytes = 0, i, k;
 	int nc = 0, opk[4], err = 0, inited = 0, redo = 0;
 	const uint64_t t0 = mono_ns();
+	uint64_t t1 = t0;
 	struct pc_req *r;
 	struct sgpu_job *jh;
 	uint8_t *vh;
@@ -2249,8 +2289,9 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 	}
 	mst[nc] = m;
 	vh = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
+	t1 = mono_ns();
+	count(&g_ns_fused_prep, t1 - t0);
 	if (m) {
-		const uint64_t t1 = mono_ns();
 		uint64_t t2;
 		err = sgpu_run_small(w->stage.h, bytes, jh, m, vh,
 				     (uint32_t *)(vh + m), 2, w->stream);
@@ -2259,7 +2300,8 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 			err = sgpu_stream_sync(w->stream);
 		count(&g_cnt_small, 1);
 		count(&g_ns_small_launch, t2 - t1);
-		count(&g_ns_small_sync, mono_ns() - t2);
+		t1 = mono_ns();
+		count(&g_ns_small_sync, t1 - t2);
 		if (err)
 			goto out;
 	}
@@ -2313,6 +2355,7 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 		}
 	}
 	inited = 0;
+	count(&g_ns_fused_post, mono_ns() - t1);
  out:
 	/* nothing ran, or the launch failed: every operation as it was */
 	for (k = 0; k < (size_t)inited; k++)
@@ -2328,7 +2371,7 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 	return err ? -1 : 0;
 }
 
-static void pc_run(struct pc_req *list)
+static void pc_run(struct pc_req *list, struct pc_slot *sl)
 {
 	unsigned ops = 0;
 	int op, first = -1;
@@ -2338,35 +2381,32 @@ static void pc_run(struct pc_req *list)
 		ops |= 1u << r->op;
 	if ((ops & (ops - 1)) && pc_run_fused(list, ops) == 0)
 		return;
-	if (ops & (ops - 1)) {
-		pthread_once(&pc_h.once, pc_helper_start);
-		if (pc_h.ok) {
-			/* the lowest operation to the helper (only the
-			 * runner posts: runners are serialised) */
-			first = __builtin_ctz(ops);
-			pc_h.list = list;
-			pc_h.op = first;
-			__atomic_store_n(&pc_h.state, 1, __ATOMIC_RELEASE);
-			(void)syscall(SYS_futex, &pc_h.state,
-				      FUTEX_WAKE_PRIVATE, 1, NULL, NULL, 0);
-		}
+	if ((ops & (ops - 1)) && pc_helper_ok(sl)) {
+		/* the lowest operation to the slot's helper */
+		first = __builtin_ctz(ops);
+		sl->hlist = list;
+		sl->hop = first;
+		__atomic_store_n(&sl->hstate, 1, __ATOMIC_RELEASE);
+		(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAKE_PRIVATE, 1,
+			      NULL, NULL, 0);
 	}
 	for (op = 0; op < 4; op++)
 		if ((ops >> op) & 1 && op != first)
 			pc_run_op(list, op);
 	if (first >= 0) {
 		int v;
-		while ((v = __atomic_load_n(&pc_h.state, __ATOMIC_ACQUIRE)) != 2)
-			(void)syscall(SYS_futex, &pc_h.state, FUTEX_WAIT_PRIVATE,
+		while ((v = __atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE)) != 2)
+			(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAIT_PRIVATE,
 				      v, NULL, NULL, 0);
-		__atomic_store_n(&pc_h.state, 0, __ATOMIC_RELAXED);
+		__atomic_store_n(&sl->hstate, 0, __ATOMIC_RELAXED);
 	}
 }
 
 static int one(int op, struct srtp *srtp, struct mbuf *mb)
 {
 	struct pc_req req;
-	int e = 0, err, run;
+	struct pc_slot *sl;
+	int e = 0, err, run, slot = 0, nrun;
 
 	if (!srtp || !mb)
 		return EINVAL;
@@ -2380,32 +2420,53 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 	req.op = op;
 	req.s = srtp;
 	req.mb = mb;
+	nrun = g_env.pcrunners > 0 ? (int)g_env.pcrunners : PC_RUNNERS;
+	if (nrun > PC_SLOTS)
+		nrun = PC_SLOTS;
 	pthread_mutex_lock(&pc_lock);
 	if (pc_tail)
 		pc_tail->next = &req;
 	else
 		pc_head = &req;
 	pc_tail = &req;
-	run = !pc_running;
-	pc_running = 1;
+	run = pc_running < nrun;
+	if (run) {
+		/* a free slot: run the queue now (taken here, in the same
+		 * critical section, so no hand-off can take this request) */
+		pc_running++;
+		slot = __builtin_ctz(~pc_slot_used);
+		pc_slot_used |= 1u << slot;
+		req.list = pc_head;
+		pc_head = pc_tail = NULL;
+	}
 	pthread_mutex_unlock(&pc_lock);
 	if (!run && pc_wait(&req.state) == PC_DONE)
 		return req.err;
-	/* the runner: everything queued so far, then the role to the first
-	 * request queued meanwhile (or none) */
+	/* the runner (PC_RUN: slot and queue handed over): its queue on the
+	 * slot's workspace, then the slot and the queue gathered meanwhile to
+	 * that queue's first request (or the slot is freed) */
+	slot = req.slot = run ? slot : req.slot;
+	sl = &pc_slots[slot];
+	if (!sl->ws)
+		sl->ws = ws_new();      /* the slot is this thread's alone */
 	{
-		struct pc_req *list, *r, *nx, *next_runner;
-		pthread_mutex_lock(&pc_lock);
-		list = pc_head;
-		pc_head = pc_tail = NULL;
-		pthread_mutex_unlock(&pc_lock);
-		pc_run(list);
+		struct pc_req *list = req.list, *r, *nx, *next_runner;
+		t_ws_use = sl->ws;      /* NULL: this thread's own */
+		pc_run(list, sl);
+		t_ws_use = NULL;
 		/* the next batch first: hand the runner role on, then
 		 * complete this one's callers */
 		pthread_mutex_lock(&pc_lock);
 		next_runner = pc_head;
-		if (!next_runner)
-			pc_running = 0;
+		if (next_runner) {
+			next_runner->slot = slot;
+			next_runner->list = pc_head;
+			pc_head = pc_tail = NULL;
+		}
+		else {
+			pc_running--;
+			pc_slot_used &= ~(1u << slot);
+		}
 		pthread_mutex_unlock(&pc_lock);
 		if (next_runner)
 			pc_wake(&next_runner->state, PC_RUN);
@@ -5259,8 +5320,10 @@ static int rx_step(struct rx_walk *x, int ok, uint32_t ssrc, uint16_t seq,
 		   int32_t res, struct srtp_rx_rec *r)
 {
 	int diff;
-	memset(r, 0, sizeof(*r));
+	r->ix = 0;
 	r->res = res;
+	r->seq = 0;
+	r->pad = 0;
 	if (!ok) {
 		r->stage = SRTP_RX_NOHDR;
 		return 0;
@@ -5320,12 +5383,12 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 		      const int32_t *res, size_t n, struct srtp_rx_rec *rec,
 		      void *stream)
 {
-	const struct sgpu_hdr *hh;
-	const int32_t *rh;
+	const uint32_t *pk;
+	const int32_t *rh = NULL;
 	struct rx_walk x;
 	struct ws *w;
 	size_t i;
-	int err;
+	int err, wide = 0;
 
 	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)) ||
 	    n > UINT32_MAX)
@@ -5338,8 +5401,8 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 	if (!w)
 		return ENOMEM;
 	/* the headers parsed where the packets lie (k_parse: rtp_hdr_decode,
-	 * rtp.c:88-137), 12 B per packet down with the results: the arena
-	 * stays on the device */
+	 * rtp.c:88-137) and packed with the results, 4 B per packet down:
+	 * the arena stays on the device */
 	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
 	if (!err)
 		err = pool_reserve(w, &w->es, n * 4);
@@ -5348,24 +5411,41 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 					 (struct sgpu_hdr *)w->hd.d, NULL,
 					 (uint32_t)n, 0, stream);
 	if (!err)
-		err = sgpu_memcpy_d2h(w->hd.h, w->hd.d,
-				      n * sizeof(struct sgpu_hdr), stream);
+		err = sgpu_rx_pack((const struct sgpu_hdr *)w->hd.d, res,
+				   st0->ssrc, (uint32_t *)w->es.d, (uint32_t)n,
+				   stream);
 	if (!err)
-		err = sgpu_memcpy_d2h(w->es.h, res, n * 4, stream);
+		err = sgpu_memcpy_d2h(w->es.h, w->es.d, n * 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)
 		return err;
-	hh = (const struct sgpu_hdr *)w->hd.h;
-	rh = (const int32_t *)w->es.h;
+	pk = (const uint32_t *)w->es.h;
+	for (i = 0; i < n; i++)
+		wide |= (pk[i] >> 23) & 1;
+	if (wide) {
+		/* a result outside 0..255 (not an errno): all of them */
+		err = pool_reserve(w, &w->hd, n * 4);
+		if (!err)
+			err = sgpu_memcpy_d2h(w->hd.h, res, n * 4, stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		if (err)
+			return err;
+		rh = (const int32_t *)w->hd.h;
+	}
 	x.ssrc = st0->ssrc;
 	x.roc = st0->roc;
 	x.s_l = st0->s_l;
 	x.set = st0->s_l_set;
-	for (i = 0; i < n; i++)
-		if (rx_step(&x, hh[i].hdr_len != UINT32_MAX, hh[i].ssrc,
-			    hh[i].seq, rh[i], &rec[i]))
+	for (i = 0; i < n; i++) {
+		const uint32_t v = pk[i];
+		const int32_t r = rh ? rh[i] : (int32_t)(v >> 24);
+		if ((v >> 17) & 1)
+			return EINVAL;  /* another SSRC */
+		if (rx_step(&x, (v >> 16) & 1, x.ssrc, (uint16_t)v, r, &rec[i]))
 			return EINVAL;
+	}
 	return 0;
 }
 

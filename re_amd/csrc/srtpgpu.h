@@ -546,6 +546,10 @@ int   sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,
 			 const uint32_t *pos, const uint32_t *end,
 			 struct sgpu_hdr *out, uint32_t *eix, uint32_t n,
 			 int rtcp, void *stream);
+/* srtp_rx_index_dev: per packet seq | ok << 16 | (ssrc != ssrc0) << 17 |
+ * (res outside 0..255) << 23 | (res & 255) << 24 */
+int   sgpu_rx_pack(const struct sgpu_hdr *hd, const int32_t *res,
+		   uint32_t ssrc0, uint32_t *out, uint32_t n, void *stream);
 
 /* sgpu_parse_headers plus the per-call prologue of a device batch in the
  * same launch: end_copy[i] = end[i] (if set), z0[0..nz0) and z1[0..nz1)

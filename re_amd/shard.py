@@ -135,17 +135,21 @@ def rx_records(st0, arena, pos, end, res):
     return rec
 
 
-def rx_records_dev(st0, arena, pos, end, res, stream=None):
+def rx_records_dev(st0, arena, pos, end, res, stream=None, out=None):
     """the rank's records from its DEVICE outputs (srtp_rx_index_dev): arena
     a torch uint8 CUDA tensor, pos/end/res int32 CUDA tensors of the rank's
-    srtp_decrypt_batch_dev call (the arena never leaves the device)"""
+    srtp_decrypt_batch_dev call (the arena never leaves the device); out: a
+    record array of that length to fill (else a new one)"""
     import ctypes
     import numpy as np
     from . import srtp as S
     n = int(pos.numel())
     if int(end.numel()) != n or int(res.numel()) != n:
         raise ValueError("rx_records_dev: pos, end and res differ in length")
-    rec = np.zeros(n, dtype=_rx_rec_dtype())
+    rec = np.zeros(n, dtype=_rx_rec_dtype()) if out is None else out
+    if rec.dtype != _rx_rec_dtype() or len(rec) != n or \
+            not rec.flags["C_CONTIGUOUS"]:
+        raise ValueError("rx_records_dev: out is not n contiguous records")
     e = S.lib().srtp_rx_index_dev(ctypes.byref(st0), arena.data_ptr(),
                                   arena.numel(), pos.data_ptr(),
                                   end.data_ptr(), res.data_ptr(), n,

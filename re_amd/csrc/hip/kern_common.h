@@ -298,6 +298,12 @@ struct KArgs {
 	struct sgpu_compact c;          /* compact path */
 	int nocipher;                   /* general path: the cipher regions are
 					   done by k_ctr_coop (small launches) */
+	/* k_ctr_small: completion word in pinned host memory (or NULL): the
+	 * last workgroup stores done_seq there after every workgroup's
+	 * writes, done_cnt (device, 0 between launches) counts them */
+	uint32_t *done_cnt;
+	uint32_t *done_flag;
+	uint32_t done_seq;
 };
 
 /*
@@ -725,7 +731,8 @@ typedef void (*kfn_t)(const KArgs);
 int small_launch(uint8_t *arena, uint64_t arena_size,
 		 const struct sgpu_job *jobs, uint32_t njobs, uint8_t *verdict,
 		 uint32_t *save, const struct sgpu_comp *comps,
-		 const uint32_t *t0, int prot, void *stream);
+		 const uint32_t *t0, int prot, uint32_t *done_cnt,
+		 uint32_t *done_flag, uint32_t done_seq, void *stream);
 
 /* kernel pickers, one per translation unit */
 unsigned sgpu_ctr_block(bool uni, int prot);

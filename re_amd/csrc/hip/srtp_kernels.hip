@@ -1249,11 +1249,12 @@ extern "C" int sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 extern "C" int sgpu_run_small(uint8_t *arena, uint64_t arena_size,
 			      const struct sgpu_job *jobs, uint32_t njobs,
 			      uint8_t *verdict, uint32_t *save, int prot,
-			      void *stream)
+			      uint32_t *done_cnt, uint32_t *done_flag,
+			      uint32_t done_seq, void *stream)
 {
 	return small_launch(arena, arena_size, jobs, njobs, verdict, save,
 			    (const struct sgpu_comp *)g_table, g_T0_dev, prot,
-			    stream);
+			    done_cnt, done_flag, done_seq, stream);
 }
 
 /* srtp_gpu_tune nocoop (A/B): small general launches fused as usual */
@@ -1521,6 +1522,15 @@ extern "C" int sgpu_memset(void *dst, int v, size_t n, void *stream)
 extern "C" int sgpu_stream_sync(void *stream)
 {
 	return herr(hipStreamSynchronize((hipStream_t)stream), "stream sync");
+}
+
+/* 0: the stream's work is done, EAGAIN: not yet, else EIO */
+extern "C" int sgpu_stream_query(void *stream)
+{
+	const hipError_t e = hipStreamQuery((hipStream_t)stream);
+	if (e == hipErrorNotReady)
+		return EAGAIN;
+	return herr(e, "stream query");
 }
 
 extern "C" int sgpu_device_sync(void)

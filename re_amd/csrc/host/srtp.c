@@ -158,6 +158,9 @@ static struct {
 	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
 				   per-packet caller spins before it sleeps
 				   (default 1000) */
+	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
+				   launch by a stream synchronisation, not
+				   its completion word */
 	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
 				   shared per-packet launch run as separate
 				   launches (helper thread), not one */
@@ -310,6 +313,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nosmall = value > 0;
 	else if (!strcmp(name, "nofuse"))
 		g_env.nofuse = value > 0;
+	else if (!strcmp(name, "smallsync"))
+		g_env.smallsync = value > 0;
 	else if (!strcmp(name, "pcrunners"))
 		g_env.pcrunners = value > 0 ? value : 0;
 	else if (!strcmp(name, "pcspin"))
@@ -1330,6 +1335,10 @@ struct ws {
 	void **ev;              /* per-chunk parse events */
 	size_t nev;
 	struct ulogv ulog[1];   /* stream-state undo log */
+	/* the small kernel's completion word (small_wait) */
+	uint32_t *sm_cnt;       /* device */
+	uint32_t *sm_flag;      /* pinned host */
+	uint32_t sm_seq;
 };
 
 
@@ -1359,6 +1368,63 @@ static struct ws *ws_get(void)
 	if (!t_ws)
 		t_ws = ws_new();
 	return t_ws;
+}
+
+/*
+ * Launch the small kernel and wait for it by its completion word: the
+ * host spins on the pinned word the last workgroup stores (system scope,
+ * after every workgroup's writes) instead of a stream synchronisation,
+ * checking the stream for an error now and then.  Without the word (its
+ * allocation failed) a plain synchronisation.
+ */
+static int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
+		     const struct sgpu_job *jobs, uint32_t m, uint8_t *vh,
+		     uint32_t *sv, int prot, uint64_t *t_launch)
+{
+	const uint64_t t0 = mono_ns();
+	unsigned long k;
+	uint32_t seq;
+	int err;
+
+	if (!w->sm_flag && !g_env.smallsync) {
+		w->sm_cnt = fi_sgpu_malloc(4);
+		w->sm_flag = fi_sgpu_host_alloc(4);
+		if (w->sm_cnt && w->sm_flag &&
+		    !sgpu_memset(w->sm_cnt, 0, 4, w->stream)) {
+			*w->sm_flag = 0;
+		}
+		else {
+			sgpu_free(w->sm_cnt);
+			sgpu_host_free(w->sm_flag);
+			w->sm_cnt = w->sm_flag = NULL;
+		}
+	}
+	seq = ++w->sm_seq ? w->sm_seq : ++w->sm_seq;   /* never 0 */
+	{
+		uint32_t *flag = g_env.smallsync ? NULL : w->sm_flag;
+		err = sgpu_run_small(arena, asz, jobs, m, vh, sv, prot,
+				     w->sm_cnt, flag, seq, w->stream);
+		*t_launch = mono_ns() - t0;
+		if (err)
+			return err;
+		if (!flag)
+			return sgpu_stream_sync(w->stream);
+	}
+	for (k = 1;; k++) {
+		int q;
+		if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
+			return 0;
+		if (k & 1023) {
+			__builtin_ia32_pause();
+			continue;
+		}
+		q = sgpu_stream_query(w->stream);
+		if (q == EAGAIN)
+			continue;
+		if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
+			return 0;
+		return q ? q : EIO;     /* done without its word: a fault */
+	}
 }
 
 static int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
@@ -1622,8 +1688,16 @@ static int round_small(struct ws *w, struct engine *E, uint64_t asz,
 		m++;
 	}
 	vh = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
-	err = sgpu_run_small(w->stage.h, asz, jh, m, vh, (uint32_t *)(vh + m),
-			     prot, stream);
+	(void)stream;
+	{
+		uint64_t tl;
+		const uint64_t t0 = mono_ns();
+		err = small_run(w, w->stage.h, asz, jh, m, vh,
+				(uint32_t *)(vh + m), prot, &tl);
+		count(&g_cnt_small, 1);
+		count(&g_ns_small_launch, tl);
+		count(&g_ns_small_sync, mono_ns() - t0 - tl);
+	}
 	if (!err)
 		*pm = m;
 	return err;
@@ -1864,25 +1938,15 @@ static int mbc_round(struct mbc *c, struct ws *w)
 	if (err)
 		return err;
 	mbc_stage(c, w->stage.h);
-	{
-		/* few packets: the fused kernel over the
-		 * pinned staging memory itself */
-		const uint64_t t0 = mono_ns();
-		rs = round_small(w, E, bytes, c->soff, c->prot, &m, w->stream);
-		if (rs >= 0) {
-			const uint64_t t1 = mono_ns();
-			err = rs ? rs : sgpu_stream_sync(w->stream);
-			if (m) {
-				count(&g_cnt_small, 1);
-				count(&g_ns_small_launch, t1 - t0);
-				count(&g_ns_small_sync, mono_ns() - t1);
-			}
-			if (err)
-				return err;
-			round_collect(w, E, m);
-			mbc_ran(c, w->stage.h);
-			return 0;
-		}
+	/* few packets: the fused kernel over the pinned staging memory
+	 * itself, launched and waited for */
+	rs = round_small(w, E, bytes, c->soff, c->prot, &m, w->stream);
+	if (rs > 0)
+		return rs;
+	if (rs == 0) {
+		round_collect(w, E, m);
+		mbc_ran(c, w->stage.h);
+		return 0;
 	}
 	err = sgpu_memcpy_h2d(w->stage.d, w->stage.h, bytes, w->stream);
 	if (!err)
@@ -2292,16 +2356,13 @@ static int pc_run_fused(struct pc_req *list, unsigned ops)
 	t1 = mono_ns();
 	count(&g_ns_fused_prep, t1 - t0);
 	if (m) {
-		uint64_t t2;
-		err = sgpu_run_small(w->stage.h, bytes, jh, m, vh,
-				     (uint32_t *)(vh + m), 2, w->stream);
-		t2 = mono_ns();
-		if (!err)
-			err = sgpu_stream_sync(w->stream);
+		uint64_t tl;
+		err = small_run(w, w->stage.h, bytes, jh, m, vh,
+				(uint32_t *)(vh + m), 2, &tl);
 		count(&g_cnt_small, 1);
-		count(&g_ns_small_launch, t2 - t1);
+		count(&g_ns_small_launch, tl);
+		count(&g_ns_small_sync, mono_ns() - t1 - tl);
 		t1 = mono_ns();
-		count(&g_ns_small_sync, t1 - t2);
 		if (err)
 			goto out;
 	}

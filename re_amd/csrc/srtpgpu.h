@@ -118,11 +118,15 @@ void  sgpu_set_coop(int on);
  * kernel, one packet per workgroup, over jobs, packets, verdicts and saved
  * words in PINNED HOST memory (sgpu_host_alloc: device-accessible), no
  * copies; packets of at most SGPU_SMALL_MAX bytes from their start.
- * prot: 0 unprotect, 1 protect, 2 per job (SJ_PROTECT) */
+ * prot: 0 unprotect, 1 protect, 2 per job (SJ_PROTECT).  done_flag (pinned
+ * host word, or NULL): done_seq is stored there once every workgroup's
+ * writes are visible; done_cnt: a device word, 0 between launches */
 #define SGPU_SMALL_MAX 2048
 int   sgpu_run_small(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,
-		     uint8_t *verdict, uint32_t *save, int prot, void *stream);
+		     uint8_t *verdict, uint32_t *save, int prot,
+		     uint32_t *done_cnt, uint32_t *done_flag,
+		     uint32_t done_seq, void *stream);
 int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,
 		     uint8_t *verdict, uint32_t *save, int mode, int nr,
@@ -606,6 +610,7 @@ int   sgpu_memcpy_d2h(void *dst, const void *src, size_t n, void *stream);
 int   sgpu_memcpy_d2d(void *dst, const void *src, size_t n, void *stream);
 int   sgpu_memset(void *dst, int v, size_t n, void *stream);
 int   sgpu_stream_sync(void *stream);
+int   sgpu_stream_query(void *stream);  /* 0 done, EAGAIN, EIO */
 int   sgpu_device_sync(void);
 void *sgpu_stream_create(void);
 void  sgpu_stream_destroy(void *s);

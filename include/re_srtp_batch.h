@@ -235,7 +235,11 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * of a device-planned batch fold on the host), "nocombine" (per-packet
  * calls of different threads do not share launches), "nosmall" (the
  * per-packet path's fused small kernel off), "nofuse" (the operations of
- * a shared per-packet launch run as one launch each), "trace", "times" (phase
+ * a shared per-packet launch run as one launch each), "smallsync" (a small
+ * launch waited for by a stream synchronisation, not its completion
+ * word), "pcrunners" (per-packet runners at once, 1-4, default 4),
+ * "pcspin" (pause loops a waiting per-packet caller spins before it
+ * sleeps, default 1000), "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores
  * a size's built-in default.  Results never depend on them.  0 or EINVAL.

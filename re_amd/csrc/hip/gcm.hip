@@ -788,6 +788,13 @@ __device__ __forceinline__ uint8_t gcma_packet(const uint8_t *smem, uint32_t lo,
 			quad_store(arena, qb, 64u * m, lane, o);
 		}
 		else {
+			/* the chunk's four 16-B stores back to back: scheduled
+			 * as each block is ready (the unprotect S = 2 body put
+			 * ~1000 instructions between them), a lane's 64-B line
+			 * was evicted half written and written back twice --
+			 * SRTCP-GCM unprotect moved 2.6 GB of writes against
+			 * 1.7 for the same bytes (TCC_NORMAL_WRITEBACK x2) */
+			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int g = 0; g < 4; g++)
 				*(uint4 *)(pkt + 64u * k + 16u * g) =

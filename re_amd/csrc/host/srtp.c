@@ -206,6 +206,7 @@ static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
 static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
 static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
+static uint64_t g_cnt_rxw_redo; /* srtp_rx_index*: parts walked again */
 static uint64_t g_cnt_pcfused;  /* ... of which several operations in one
 				   small launch (pc_run_fused) */
 static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
@@ -256,6 +257,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcpackets"))
 		return __atomic_load_n(&g_cnt_pcpkts, __ATOMIC_RELAXED);
+	if (!strcmp(name, "rxw_redos"))
+		return __atomic_load_n(&g_cnt_rxw_redo, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcfused"))
 		return __atomic_load_n(&g_cnt_pcfused, __ATOMIC_RELAXED);
 	if (!strcmp(name, "gated"))
@@ -5412,29 +5415,171 @@ static int rx_step(struct rx_walk *x, int ok, uint32_t ssrc, uint16_t seq,
 	return 0;
 }
 
+static int rx_walk_packed(const struct srtp_stream_state *st0,
+			  const uint32_t *pk, const int32_t *rh, size_t n,
+			  struct srtp_rx_rec *rec);
+
 int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
 		  const uint32_t *pos, const uint32_t *end,
 		  const int32_t *res, size_t n, struct srtp_rx_rec *rec)
 {
-	struct rx_walk x;
+	uint32_t *pk;
 	size_t i;
+	int err;
 
 	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)))
 		return EINVAL;
-	x.ssrc = st0->ssrc;
-	x.roc = st0->roc;
-	x.s_l = st0->s_l;
-	x.set = st0->s_l_set;
+	if (!n)
+		return 0;
+	/* the headers parsed here, then the walk of srtp_rx_index_dev */
+	pk = fi_malloc(n * sizeof(*pk));
+	if (!pk)
+		return ENOMEM;
 	for (i = 0; i < n; i++) {
 		struct pinfo pi;
 		memset(&pi, 0, sizeof(pi));
 		pi.start = pos[i];
 		pi.end = end[i];
 		parse_rtp(&pi, arena);
-		if (rx_step(&x, pi.hdr_len != UINT32_MAX, pi.ssrc, pi.seq,
-			    res[i], &rec[i]))
-			return EINVAL;
+		pk[i] = pi.hdr_len == UINT32_MAX ? 0u :
+			(uint32_t)pi.seq | 1u << 16 |
+			(pi.ssrc != st0->ssrc ? 1u << 17 : 0u);
 	}
+	err = rx_walk_packed(st0, pk, res, n, rec);
+	free(pk);
+	return err;
+}
+
+/*
+ * The walk over packed words (k_rx_pack: seq | ok << 16 | other SSRC << 17
+ * | res << 24, or res from rh) in parallel parts: part k > 0 guesses its
+ * start state by a cold walk over the W packets before it (the receiver's
+ * s_l is the newest accepted in-window seq, which a few hundred packets
+ * re-establish) and walks with a relative ROC; then, in order, each
+ * guess is checked against the previous part's true end state -- a part
+ * whose guess was wrong is walked again from the true state, a right one
+ * gets its ROC base added to its indices (get_index is linear in the ROC
+ * while it stays below 2^31, which the caller checks).  Same records as
+ * the sequential walk.
+ */
+enum { RXW_PARTS = 16, RXW_WARM = 512 };
+
+struct rxw {
+	const uint32_t *pk;
+	const int32_t *rh;
+	struct srtp_rx_rec *rec;
+	size_t n;
+	struct rx_walk st0;
+	struct rx_walk guess[RXW_PARTS], end[RXW_PARTS];
+	int bad[RXW_PARTS];
+	uint32_t base[RXW_PARTS];
+};
+
+static size_t rxw_lo(const struct rxw *q, size_t k)
+{
+	return q->n * k / RXW_PARTS;
+}
+
+/* packets [lo, hi) from *x; 1 if one has another SSRC */
+static int rxw_walk(const struct rxw *q, struct rx_walk *x, size_t lo,
+		    size_t hi, int store)
+{
+	size_t i;
+	for (i = lo; i < hi; i++) {
+		const uint32_t v = q->pk[i];
+		const int32_t r = q->rh ? q->rh[i] : (int32_t)(v >> 24);
+		struct srtp_rx_rec tmp;
+		if ((v >> 17) & 1)
+			return 1;
+		(void)rx_step(x, (v >> 16) & 1, x->ssrc, (uint16_t)v, r,
+			      store ? &q->rec[i] : &tmp);
+	}
+	return 0;
+}
+
+static void rxw_part(void *arg, size_t k0, size_t k1)
+{
+	struct rxw *q = arg;
+	size_t k;
+	for (k = k0; k < k1; k++) {
+		const size_t lo = rxw_lo(q, k), hi = rxw_lo(q, k + 1);
+		struct rx_walk x = q->st0;
+		if (k) {
+			x.roc = 0;
+			x.set = 0;
+			x.s_l = 0;
+			q->bad[k] = rxw_walk(q, &x, lo > RXW_WARM ? lo - RXW_WARM : 0,
+					     lo, 0);
+			x.roc = 0;      /* relative from here */
+			q->guess[k] = x;
+		}
+		q->bad[k] |= rxw_walk(q, &x, lo, hi, 1);
+		q->end[k] = x;
+	}
+}
+
+static void rxw_fix(void *arg, size_t k0, size_t k1)
+{
+	struct rxw *q = arg;
+	size_t k, i;
+	for (k = k0; k < k1; k++) {
+		const uint64_t add = (uint64_t)q->base[k] << 16;
+		if (!add)
+			continue;
+		for (i = rxw_lo(q, k); i < rxw_lo(q, k + 1); i++)
+			if (q->rec[i].stage == SRTP_RX_IX)
+				q->rec[i].ix += add;
+	}
+}
+
+static int rx_walk_packed(const struct srtp_stream_state *st0,
+			  const uint32_t *pk, const int32_t *rh, size_t n,
+			  struct srtp_rx_rec *rec)
+{
+	struct rxw *q;
+	struct rx_walk x;
+	size_t k;
+	int fix = 0;
+
+	x.ssrc = st0->ssrc;
+	x.roc = st0->roc;
+	x.s_l = st0->s_l;
+	x.set = st0->s_l_set;
+	if (n < 65536 || (uint64_t)st0->roc + n + 2 >= 0x7fffffffull) {
+		struct rxw one = {.pk = pk, .rh = rh, .rec = rec, .n = n};
+		return rxw_walk(&one, &x, 0, n, 1) ? EINVAL : 0;
+	}
+	q = fi_calloc(1, sizeof(*q));
+	if (!q)
+		return ENOMEM;
+	q->pk = pk;
+	q->rh = rh;
+	q->rec = rec;
+	q->n = n;
+	q->st0 = x;
+	par_for(RXW_PARTS, 1, rxw_part, q);
+	for (k = 0; k < RXW_PARTS; k++)
+		if (q->bad[k]) {
+			free(q);
+			return EINVAL;
+		}
+	for (k = 1; k < RXW_PARTS; k++) {
+		struct rx_walk t = q->end[k - 1];       /* the true start */
+		if (t.set != q->guess[k].set ||
+		    (t.set && t.s_l != q->guess[k].s_l)) {
+			/* a wrong guess: this part again, exactly */
+			count(&g_cnt_rxw_redo, 1);
+			(void)rxw_walk(q, &t, rxw_lo(q, k), rxw_lo(q, k + 1), 1);
+			q->end[k] = t;
+			continue;
+		}
+		q->base[k] = t.roc;
+		fix |= t.roc != 0;
+		q->end[k].roc += t.roc;
+	}
+	if (fix)
+		par_for(RXW_PARTS, 1, rxw_fix, q);
+	free(q);
 	return 0;
 }
 
@@ -5446,7 +5591,6 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 {
 	const uint32_t *pk;
 	const int32_t *rh = NULL;
-	struct rx_walk x;
 	struct ws *w;
 	size_t i;
 	int err, wide = 0;
@@ -5495,19 +5639,7 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 			return err;
 		rh = (const int32_t *)w->hd.h;
 	}
-	x.ssrc = st0->ssrc;
-	x.roc = st0->roc;
-	x.s_l = st0->s_l;
-	x.set = st0->s_l_set;
-	for (i = 0; i < n; i++) {
-		const uint32_t v = pk[i];
-		const int32_t r = rh ? rh[i] : (int32_t)(v >> 24);
-		if ((v >> 17) & 1)
-			return EINVAL;  /* another SSRC */
-		if (rx_step(&x, (v >> 16) & 1, x.ssrc, (uint16_t)v, r, &rec[i]))
-			return EINVAL;
-	}
-	return 0;
+	return rx_walk_packed(st0, pk, rh, n, rec);
 }
 
 int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,

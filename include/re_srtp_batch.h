@@ -211,7 +211,7 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
  * packet's position and *st = the exact state before it -- re-run packets
  * ndone.. from *st (srtp_stream_import) on their received bytes.
  * *ndone == n when every verdict stands; *st is then the final state.
- * 0 or EINVAL.
+ * err[i] for i >= *ndone is unspecified.  0, EINVAL or ENOMEM.
  */
 int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
 		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
@@ -239,7 +239,8 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * launch waited for by a stream synchronisation, not its completion
  * word), "pcrunners" (per-packet runners at once, 1-4, default 4),
  * "pcspin" (pause loops a waiting per-packet caller spins before it
- * sleeps, default 1000), "trace", "times" (phase
+ * sleeps, default 1000), "rxseq" (srtp_rx_index* and srtp_rx_fold walk
+ * in one sequential pass, not in parallel parts), "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores
  * a size's built-in default.  Results never depend on them.  0 or EINVAL.

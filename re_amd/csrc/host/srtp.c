@@ -158,6 +158,8 @@ static struct {
 	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
 				   per-packet caller spins before it sleeps
 				   (default 1000) */
+	int rxseq;              /* srtp_gpu_tune rxseq: srtp_rx_index* and
+				   srtp_rx_fold walk sequentially (A/B) */
 	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
 				   launch by a stream synchronisation, not
 				   its completion word */
@@ -318,6 +320,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nofuse = value > 0;
 	else if (!strcmp(name, "smallsync"))
 		g_env.smallsync = value > 0;
+	else if (!strcmp(name, "rxseq"))
+		g_env.rxseq = value > 0;
 	else if (!strcmp(name, "pcrunners"))
 		g_env.pcrunners = value > 0 ? value : 0;
 	else if (!strcmp(name, "pcspin"))
@@ -5545,7 +5549,8 @@ static int rx_walk_packed(const struct srtp_stream_state *st0,
 	x.roc = st0->roc;
 	x.s_l = st0->s_l;
 	x.set = st0->s_l_set;
-	if (n < 65536 || (uint64_t)st0->roc + n + 2 >= 0x7fffffffull) {
+	if (n < 65536 || g_env.rxseq ||
+	    (uint64_t)st0->roc + n + 2 >= 0x7fffffffull) {
 		struct rxw one = {.pk = pk, .rh = rh, .rec = rec, .n = n};
 		return rxw_walk(&one, &x, 0, n, 1) ? EINVAL : 0;
 	}
@@ -5642,58 +5647,81 @@ int srtp_rx_index_dev(const struct srtp_stream_state *st0,
 	return rx_walk_packed(st0, pk, rh, n, rec);
 }
 
-int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
-		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
-		 size_t *ndone)
-{
+/*
+ * The fold's walk (the reference receiver from the true state, srtp.c
+ * :310-321 index step, :355-368 / :413-429 replay verdicts; the rank's
+ * verdict void where the index or the replay verdict differs) over
+ * records [lo, hi) from *x.  Returns the first void position (hi: none);
+ * the state is then the one before it.  RXF_REL: the ROC is relative to
+ * an unknown base -- instead of comparing indices, rec.ix - ix must be
+ * one constant *D over the part (a different one is a void); *vmin is
+ * the least ROC value get_index used.  RXF_WARM: state only (a guess of
+ * a part's start), no verdicts, nothing stops it.
+ */
+enum { RXF_EXACT, RXF_REL, RXF_WARM, RXF_PARTS = 16, RXF_WARMN = 512,
+       RXF_R0 = 2 };
+
+struct rxf_state {
 	struct replay rp;
 	uint32_t roc;
 	uint16_t s_l;
 	uint8_t set;
-	size_t i;
+};
 
-	/* every suite checks the replay window after its tag (srtp.c:362-368
-	 * HMAC, 414-421 GCM), so suite is only validated */
-	if (!st || !ndone || (n && (!rec || !err)) ||
-	    (unsigned)suite > SRTP_AES_256_GCM)
-		return EINVAL;
-	rp.bitmap = st->replay_rtp_bitmap;
-	rp.lix = st->replay_rtp_lix;
-	roc = st->roc;
-	s_l = st->s_l;
-	set = st->s_l_set;
-	for (i = 0; i < n; i++) {
+static size_t rxf_walk(struct rxf_state *x, const struct srtp_rx_rec *rec,
+		       int32_t *err, size_t lo, size_t hi, int mode,
+		       uint64_t *D, int *hasD, int64_t *vmin)
+{
+	size_t i;
+	for (i = lo; i < hi; i++) {
 		const struct srtp_rx_rec *r = &rec[i];
-		const uint32_t roc0 = roc;
-		const uint16_t s_l0 = s_l;
-		const uint8_t set0 = set;
+		const uint32_t roc0 = x->roc;
+		const uint16_t s_l0 = x->s_l;
+		const uint8_t set0 = x->set;
 		uint64_t ix;
 		int diff;
 
 		if (r->stage == SRTP_RX_NOHDR) {
-			err[i] = r->res;
+			if (err)
+				err[i] = r->res;
 			continue;
 		}
-		if (!set) {
-			s_l = r->seq;
-			set = 1;
+		if (!x->set) {
+			x->s_l = r->seq;
+			x->set = 1;
 		}
-		diff = (int)r->seq - (int)s_l;
+		diff = (int)r->seq - (int)x->s_l;
 		if (diff > 32768) {
-			err[i] = ETIMEDOUT;
+			if (err)
+				err[i] = ETIMEDOUT;
 			continue;
 		}
 		if (r->stage != SRTP_RX_IX)
 			goto void_verdict;
 		if (diff <= -32768) {
-			roc++;
-			s_l = 0;
+			x->roc++;
+			x->s_l = 0;
 		}
-		ix = get_index(roc, s_l, r->seq);
-		if (ix != r->ix)
-			goto void_verdict;
+		ix = get_index(x->roc, x->s_l, r->seq);
+		if (mode == RXF_EXACT) {
+			if (ix != r->ix)
+				goto void_verdict;
+		}
+		else if (mode == RXF_REL) {
+			const int64_t v = (int64_t)x->roc - 1;
+			if (v < *vmin)
+				*vmin = v;
+			if (!*hasD) {
+				*D = r->ix - ix;
+				*hasD = 1;
+			}
+			else if (r->ix - ix != *D) {
+				goto void_verdict;
+			}
+		}
 		if (r->res != 0 && r->res != EALREADY) {
-			err[i] = r->res;        /* tag verdict: ROC bump stays */
+			if (err)
+				err[i] = r->res;        /* tag verdict: ROC bump stays */
 			continue;
 		}
 		/* a replay verdict the fold changes voids the packet's side
@@ -5702,32 +5730,172 @@ int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
 		 * pos there (:413-422), success restores it (:429).  Check
 		 * the window on a copy so the state stays the one before it */
 		{
-			struct replay tmp = rp;
+			struct replay tmp = x->rp;
 			const int ok = replay_check(&tmp, ix);
 			if (ok != (r->res == 0))
 				goto void_verdict;
-			rp = tmp;
+			x->rp = tmp;
 			if (!ok) {
-				err[i] = EALREADY;
+				if (err)
+					err[i] = EALREADY;
 				continue;
 			}
 		}
-		err[i] = 0;
-		if (r->seq > s_l)
-			s_l = r->seq;
+		if (err)
+			err[i] = 0;
+		if (r->seq > x->s_l)
+			x->s_l = r->seq;
 		continue;
 	void_verdict:
-		roc = roc0;
-		s_l = s_l0;
-		set = set0;
-		break;
+		x->roc = roc0;
+		x->s_l = s_l0;
+		x->set = set0;
+		if (mode != RXF_WARM)
+			return i;
 	}
-	st->replay_rtp_bitmap = rp.bitmap;
-	st->replay_rtp_lix = rp.lix;
-	st->roc = roc;
-	st->s_l = s_l;
-	st->s_l_set = set;
-	*ndone = i;
+	return hi;
+}
+
+/*
+ * The fold in parallel parts, as rx_walk_packed: part k > 0 guesses its
+ * start state by a cold walk over the RXF_WARMN records before it (the
+ * 64-packet window and s_l are re-established by a few hundred packets)
+ * and folds with a relative ROC (RXF_R0: its indices never go below 0);
+ * then, in order, each part's guess, index offset and lowest ROC are
+ * checked against the previous part's true end state -- a right guess
+ * makes its verdicts, its void position and its end state (shifted by
+ * the ROC base) exact, because the window compares indices only by
+ * difference while none wraps; a wrong one is folded again exactly.
+ */
+struct rxf {
+	const struct srtp_rx_rec *rec;
+	int32_t *err;
+	size_t n;
+	struct rxf_state st0;
+	struct rxf_state guess[RXF_PARTS], end[RXF_PARTS];
+	size_t stop[RXF_PARTS];
+	uint64_t D[RXF_PARTS];
+	int hasD[RXF_PARTS];
+	int64_t vmin[RXF_PARTS];
+};
+
+static size_t rxf_lo(const struct rxf *q, size_t k)
+{
+	return q->n * k / RXF_PARTS;
+}
+
+static void rxf_part(void *arg, size_t k0, size_t k1)
+{
+	struct rxf *q = arg;
+	size_t k;
+	for (k = k0; k < k1; k++) {
+		const size_t lo = rxf_lo(q, k), hi = rxf_lo(q, k + 1);
+		struct rxf_state x = q->st0;
+		if (!k) {
+			q->stop[k] = rxf_walk(&x, q->rec, q->err, lo, hi,
+					      RXF_EXACT, NULL, NULL, NULL);
+			q->end[k] = x;
+			continue;
+		}
+		memset(&x, 0, sizeof(x));
+		x.roc = RXF_R0;
+		(void)rxf_walk(&x, q->rec, NULL,
+			       lo > RXF_WARMN ? lo - RXF_WARMN : 0, lo, RXF_WARM,
+			       NULL, NULL, NULL);
+		/* the part's relative ROC starts at RXF_R0 again */
+		x.rp.lix -= (uint64_t)(x.roc - RXF_R0) << 16;
+		x.roc = RXF_R0;
+		q->guess[k] = x;
+		q->vmin[k] = INT64_MAX;
+		q->stop[k] = rxf_walk(&x, q->rec, q->err, lo, hi, RXF_REL,
+				      &q->D[k], &q->hasD[k], &q->vmin[k]);
+		q->end[k] = x;
+	}
+}
+
+static int rxf_parallel(struct rxf_state *st, const struct srtp_rx_rec *rec,
+			size_t n, int32_t *err, size_t *ndone)
+{
+	struct rxf *q = fi_calloc(1, sizeof(*q));
+	size_t k;
+	if (!q)
+		return ENOMEM;
+	q->rec = rec;
+	q->err = err;
+	q->n = n;
+	q->st0 = *st;
+	par_for(RXF_PARTS, 1, rxf_part, q);
+	for (k = 0; k < RXF_PARTS; k++) {
+		const size_t lo = rxf_lo(q, k), hi = rxf_lo(q, k + 1);
+		if (k) {
+			const struct rxf_state t = q->end[k - 1];
+			const struct rxf_state *g = &q->guess[k];
+			const int64_t base = (int64_t)t.roc - RXF_R0;
+			const uint64_t B = (uint64_t)base << 16;
+			const int right = t.set == g->set &&
+				(!t.set || t.s_l == g->s_l) &&
+				t.rp.bitmap == g->rp.bitmap &&
+				t.rp.lix == g->rp.lix + B &&
+				g->rp.lix < (1ull << 62) &&
+				t.rp.lix < (1ull << 62) &&
+				(!q->hasD[k] || q->D[k] == B) &&
+				q->vmin[k] + base >= 0;
+			if (right) {
+				q->end[k].roc += (uint32_t)base;
+				q->end[k].rp.lix += B;
+			}
+			else {
+				struct rxf_state x = t;
+				count(&g_cnt_rxw_redo, 1);
+				q->stop[k] = rxf_walk(&x, rec, err, lo, hi,
+						      RXF_EXACT, NULL, NULL, NULL);
+				q->end[k] = x;
+			}
+		}
+		if (q->stop[k] < hi) {
+			*st = q->end[k];
+			*ndone = q->stop[k];
+			free(q);
+			return 0;
+		}
+	}
+	*st = q->end[RXF_PARTS - 1];
+	*ndone = n;
+	free(q);
+	return 0;
+}
+
+int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
+		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
+		 size_t *ndone)
+{
+	struct rxf_state x;
+	int e = 0;
+
+	/* every suite checks the replay window after its tag (srtp.c:362-368
+	 * HMAC, 414-421 GCM), so suite is only validated */
+	if (!st || !ndone || (n && (!rec || !err)) ||
+	    (unsigned)suite > SRTP_AES_256_GCM)
+		return EINVAL;
+	x.rp.bitmap = st->replay_rtp_bitmap;
+	x.rp.lix = st->replay_rtp_lix;
+	x.roc = st->roc;
+	x.s_l = st->s_l;
+	x.set = st->s_l_set;
+	if (n >= 65536 && !g_env.rxseq &&
+	    (uint64_t)st->roc + n + RXF_R0 + 2 < 0x7fffffffull &&
+	    st->replay_rtp_lix < (1ull << 62))
+		e = rxf_parallel(&x, rec, n, err, ndone);
+	else
+		*ndone = rxf_walk(&x, rec, err, 0, n, RXF_EXACT, NULL, NULL,
+				  NULL);
+	if (e)
+		return e;
+	st->replay_rtp_bitmap = x.rp.bitmap;
+	st->replay_rtp_lix = x.rp.lix;
+	st->roc = x.roc;
+	st->s_l = x.s_l;
+	st->s_l_set = x.set;
 	return 0;
 }
 

@@ -132,3 +132,91 @@ def test_parallel_walk_other_ssrc_is_einval():
     st0.ssrc = SSRC
     with pytest.raises(OSError):
         S.rx_records(st0, arena, pos, end, np.zeros(len(seqs), np.int32))
+
+
+EALREADY, ETIMEDOUT, EAUTH = 114, 110, 80
+
+
+def receiver(st, oks, seqs, forged):
+    """the reference receiver's results (srtp.c:310-368 with the 64-packet
+    window of replay.c:32-62) for a packet sequence: what every rank of a
+    correct split would report"""
+    roc, s_l, sset = st
+    lix, bm = 0, 0
+    out = []
+    for ok, seq, bad in zip(oks, seqs, forged):
+        if not ok:
+            out.append(74)                                   # EBADMSG
+            continue
+        if not sset:
+            s_l, sset = seq, 1
+        diff = seq - s_l
+        if diff > 32768:
+            out.append(ETIMEDOUT)
+            continue
+        if diff <= -32768:
+            roc = (roc + 1) & 0xffffffff
+            s_l = 0
+        ix = get_index(roc, s_l, seq)
+        if bad:
+            out.append(EAUTH)
+            continue
+        if ix > lix:
+            d = ix - lix
+            bm = ((bm << d) | 1) & (2**64 - 1) if d < 64 else 1
+            lix = ix
+        else:
+            d = lix - ix
+            if d >= 64 or (bm >> d) & 1:
+                out.append(EALREADY)
+                continue
+            bm |= 1 << d
+        out.append(0)
+        if seq > s_l:
+            s_l = seq
+    return np.array(out, dtype=np.int32)
+
+
+def fold_both(st, rec):
+    """srtp_rx_fold in one pass (rxseq) and in parallel parts"""
+    outs = []
+    for seq in (1, 0):
+        s = P.StreamState()
+        s.ssrc = SSRC
+        s.roc, s.s_l, s.s_l_set = st
+        with P.tune(rxseq=seq):
+            e, nd = S.rx_fold(s, 1, rec)
+        outs.append((e.tolist(), nd, s.roc, s.s_l, s.s_l_set,
+                     s.replay_rtp_lix, s.replay_rtp_bitmap))
+    return outs
+
+
+@pytest.mark.parametrize("seed,st", [(11, (0, 0, 0)), (12, (3, 40000, 1))])
+def test_parallel_fold_equals_sequential(seed, st):
+    P.load()
+    seqs, rng = stream(300000, seed)
+    arena, pos, end, ok = arena_of(seqs, rng)
+    forged = rng.random(len(seqs)) < 0.02
+    res = receiver(st, ok.tolist(), seqs.tolist(), forged.tolist())
+    st0 = P.StreamState()
+    st0.ssrc = SSRC
+    st0.roc, st0.s_l, st0.s_l_set = st
+    rec = S.rx_records(st0, arena, pos, end, res)
+    r0 = P.counter("rxw_redos")
+    a, b = fold_both(st, rec)
+    assert a == b
+    assert a[1] == len(rec) and a[0] == res.tolist()       # every verdict
+    m = len(rec)
+    # a replay verdict the window contradicts, and an index the rank got
+    # wrong, late in the stream: the fold stops there, in both forms
+    for p0, how in ((int(m * 0.71), "res"), (int(m * 0.83), "ix")):
+        r = rec.copy()
+        p = p0 + int(np.flatnonzero((r["stage"][p0:] == P.RX_IX) &
+                                    (r["res"][p0:] == 0))[0])
+        if how == "res":
+            r["res"][p] = EALREADY
+        else:
+            r["ix"][p] += 65536
+        a, b = fold_both(st, r)
+        assert a == b and a[1] == p, (how, p, a[1], b[1])
+    assert P.counter("rxw_redos") >= r0                     # (diagnostic)

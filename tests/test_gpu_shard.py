@@ -286,3 +286,114 @@ def test_split_stream_fold_on_device_results(torch_cuda):
     assert (st.roc, st.s_l, st.replay_rtp_lix, st.replay_rtp_bitmap) == fin
     assert (end2 == end1).all() and (pos2 == pos1).all()
     assert torch.equal(two, one)
+
+
+def test_split_stream_fold_full_size(torch_cuda):
+    """the split-stream fold at shard size: a 512K-packet config-2-shape
+    stream (1200-B packets, the ROC wraps) with 1 % loss, local swaps, late
+    packets across the shard boundary, replays and forged packets,
+    unprotected on the GPU as two shards (rank 1 from the header-only
+    boundary guess), records from the device outputs, the parallel fold
+    (srtp_rx_fold in parts), voided tails re-run from the fold's state:
+    arena, ends, errnos and final state equal to the same stream
+    unprotected in one call"""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import test_rxfold_cpu as X
+    torch = torch_cuda
+    suite = 1                                   # AES_CM_128_HMAC_SHA1_80
+    N = 1 << 19
+    key = W.make_keys(1, 30)[0].tobytes()
+    arena, pos, end, cap = W.make_arena(N, 1200, s0=S0)
+    slot = int(cap[0] - pos[0])
+    dev = torch.from_numpy(arena).cuda()
+    tx = P.Srtp(suite, key)
+    e = run(torch, "srtp_encrypt", tx, dev, pos, end, cap, 0, N)
+    assert not e.any()
+    tx.close()
+    prot = dev.cpu().numpy().reshape(N, slot)
+    plen = int(end[0] - pos[0])                 # protected length
+    # arrival order
+    rng = np.random.default_rng(7)
+    g = np.arange(N)
+    g = g[rng.random(N) > 0.01]
+    sw = rng.integers(0, len(g) - 1, len(g) // 100)
+    g[sw], g[sw + 1] = g[sw + 1].copy(), g[sw].copy()
+    m0 = len(g) // 2
+    late = g[m0 - 5:m0 - 2].copy()              # three arrive in rank 1
+    g = np.concatenate([g[:m0 - 5], g[m0 - 2:m0 + 7], late, g[m0 + 7:]])
+    dup = np.sort(rng.integers(0, len(g), 200))
+    g = np.insert(g, dup, g[dup])               # replays
+    m = len(g)
+    arr = prot[g].copy()
+    forged = rng.integers(0, m, 40)
+    arr[forged, 40] ^= 1
+    buf = arr.reshape(-1)
+    apos = np.arange(m, dtype=np.uint32) * slot
+    aend = apos + plen
+    acap = apos + slot
+    del prot, arr
+
+    # one call
+    one = torch.from_numpy(buf).cuda()
+    rx = P.Srtp(suite, key)
+    end1, pos1 = aend.copy(), apos.copy()
+    e1 = run(torch, "srtp_decrypt", rx, one, apos, end1, acap, 0, m, pos1)
+    st_one = state(rx)
+    rx.close()
+    assert (e1 != 0).sum() >= 40
+
+    # two shards, device records, the fold, voided tails re-run
+    b = m // 2
+    hdrs = [buf[int(apos[i]):int(apos[i]) + 12].tobytes() for i in range(b)]
+    guess = X.assumed_boundary(hdrs)
+    two = torch.from_numpy(buf).cuda()
+    end2, pos2 = aend.copy(), apos.copy()
+    dv = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(
+        np.int32)).cuda()
+    recs = []
+    for r, (a, z) in enumerate(((0, b), (b, m))):
+        c = P.Srtp(suite, key)
+        st0 = X.state(*guess) if r else X.state()
+        st0.ssrc = W.SSRC_BASE
+        if r:
+            assert c.import_(st0) == 0
+        res = run(torch, "srtp_decrypt", c, two, apos, end2, acap, a, z, pos2)
+        recs.append(S.rx_records_dev(st0, two, dv(apos[a:z]), dv(aend[a:z]),
+                                     dv(res)))
+        c.close()
+    rec = np.concatenate(recs)
+    st = X.state()
+    st.ssrc = W.SSRC_BASE
+    done, reruns, errs = 0, 0, []
+    while True:
+        err, nd = S.rx_fold(st, suite, rec[done:])
+        errs.append(err)
+        done += nd
+        if done == m:
+            break
+        reruns += 1
+        assert reruns <= 8
+        lo, hi = int(apos[done]), int(acap[m - 1])
+        two[lo:hi] = torch.from_numpy(buf[lo:hi]).cuda()
+        end2[done:] = aend[done:]
+        st0 = X.state(st.roc, st.s_l, st.s_l_set, st.replay_rtp_lix,
+                      st.replay_rtp_bitmap)
+        st0.ssrc = W.SSRC_BASE
+        c = P.Srtp(suite, key)
+        assert c.import_(st0) == 0
+        res = run(torch, "srtp_decrypt", c, two, apos, end2, acap, done, m,
+                  pos2)
+        c.close()
+        rec = np.concatenate([rec[:done],
+                              S.rx_records_dev(st0, two, dv(apos[done:]),
+                                               dv(aend[done:]), dv(res))])
+    # the late packets rank 1 took for replays are accepted by the one
+    # receiver: voided and re-run
+    assert reruns >= 1
+    assert (np.concatenate(errs) == e1).all()
+    assert (st.roc, st.s_l, st.s_l_set, st.replay_rtp_lix,
+            st.replay_rtp_bitmap) == st_one
+    assert (end2 == end1).all() and (pos2 == pos1).all()
+    assert torch.equal(two, one)

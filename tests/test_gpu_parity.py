@@ -26,14 +26,17 @@ def torch_cuda():
     return torch
 
 
-@pytest.mark.parametrize("coop", [1, 0])
-def test_per_call_golden(golden, coop, torch_cuda):
+@pytest.mark.parametrize("path", ["small", "coop", "general"])
+def test_per_call_golden(golden, path, torch_cuda):
     """Every recorded reference call, replayed one srtp_* call at a time --
-    with the small-launch split (the cipher regions by k_ctr_coop /
-    k_gcm_coop, the general kernel MAC-only: the default) and with the
-    cipher fused into the one-packet-per-lane kernel (nocoop)."""
+    through the fused small kernel over pinned memory (small.hip, the
+    default for packets up to SGPU_SMALL_MAX), through the copy path with
+    the small-launch split (nosmall: the cipher regions by k_ctr_coop /
+    k_gcm_coop, the general kernel MAC-only), and with the cipher fused
+    into the one-packet-per-lane general kernel (nosmall + nocoop)."""
     be = ProductBackend()
-    with P.tune(nocoop=1 - coop):
+    with P.tune(nosmall=0 if path == "small" else 1,
+                nocoop=1 if path == "general" else 0):
         bad = [m for m in (replay_scenario(be, s)
                            for s in golden["scenarios"]) if m]
     assert not bad, bad[:5]

@@ -38,6 +38,13 @@
 #ifndef CTRF_COAL_MK        /* ... per-lane-key (multi-session) kernel */
 #define CTRF_COAL_MK 1
 #endif
+#ifndef CTRF_SB_ST          /* per-lane steady chunks: stores together --
+			       off: unlike GCM's, config 4 moved the same
+			       bytes either way (3.28 GB, 1.05 ms per launch,
+			       same-box A/B) and the unprotect body spilled
+			       147 VGPRs instead of 110 */
+#define CTRF_SB_ST 0
+#endif
 #ifndef CTRF_SHAFIRST_U     /* unprotect steady chunk: MAC, then decrypt */
 #define CTRF_SHAFIRST_U 1
 #endif
@@ -362,6 +369,10 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 						   x[g][3]);
 		}
 		else {
+			/* CTRF_SB_ST: a lane's four 16-B stores of its 64-B
+			 * line back to back (gcm.hip gcma_packet) */
+			if (CTRF_SB_ST)
+				__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int g = 0; g < 4; g++)
 				*(uint4 *)(pkt + c0 + 16u * g) =

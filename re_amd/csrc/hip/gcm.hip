@@ -63,6 +63,8 @@ k_gcm(const KArgs a)
 	uint8_t *ht = smem + TT_BYTES;
 	uint32_t *rem4 = (uint32_t *)(smem + TT_BYTES +
 				      (UNI ? 1u : KBLOCK / 64u) * HT_BYTES);
+	if (COMPACT)
+		prof_guard(a);
 	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
 		return;
 	tt_fill(smem, a.t0);
@@ -910,6 +912,7 @@ k_gcmu(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT_BYTES + GH8_BYTES];
 	__shared__ uint32_t blk_comp;
+	prof_guard(a);
 	if (a.c.guard && *a.c.guard)          /* rejected plan */
 		return;
 	tt_fill(smem, a.t0);

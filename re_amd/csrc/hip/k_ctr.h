@@ -72,6 +72,8 @@ __host__ __device__ constexpr int ctr_waves(bool prot, bool uni)
 template <int NR, int SHIFT, bool PROT, bool COMPACT, bool UNI>
 __device__ __forceinline__ void ctr_hmac_body(const KArgs &a, uint8_t *smem)
 {
+	if (COMPACT)
+		prof_guard(a);
 	if (COMPACT && a.c.guard && *a.c.guard)  /* rejected plan / class */
 		return;
 	if (COMPACT || !a.nocipher)     /* MAC only: no AES */
@@ -559,6 +561,7 @@ __attribute__((amdgpu_waves_per_eu(ctr_waves(PROT, UNI), 8)))
 k_ctr_hmac_any(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	prof_guard(a);
 	const uint32_t *g = a.c.guard;
 	const uint32_t q = !g[3] ? 3u : !g[0] ? 0u : !g[1] ? 1u : !g[2] ? 2u
 								    : 4u;

@@ -612,6 +612,7 @@ __device__ __forceinline__ void ctr_refix_body(const KArgs &a, uint8_t *smem)
  * plan's skip[0..3] names it (k_plan_final), as for k_ctr_hmac_any */
 __device__ __forceinline__ int fast_class(const KArgs &a)
 {
+	prof_guard(a);
 	const uint32_t *g = a.c.guard;
 	return !g[3] ? 3 : !g[0] ? 0 : !g[1] ? 1 : !g[2] ? 2 : -1;
 }
@@ -670,6 +671,7 @@ __attribute__((amdgpu_waves_per_eu(CTRF_BLK(PROT) / 256, 8)))
 k_ctr_fast_rtcp(const KArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
+	prof_guard(a);
 	if (*a.c.guard)
 		return;                 /* rejected plan */
 	ctr_fast_body<NR, 2, PROT, false, true>(a, smem);

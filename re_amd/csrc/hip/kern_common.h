@@ -304,7 +304,22 @@ struct KArgs {
 	uint32_t *done_cnt;
 	uint32_t *done_flag;
 	uint32_t done_seq;
+	/* srtp_gpu_prof: where the kernel stores the pguard_n guard words it
+	 * saw (pinned ring slot, or NULL) -- prof_guard */
+	uint32_t *pguard;
+	uint32_t pguard_n;
 };
+
+/* srtp_gpu_prof: the plan guard words this launch saw, stored by its
+ * first thread into the launch's pinned ring slot, so the host can tell a
+ * launch that did work from one its rejected plan voided without a copy
+ * behind every launch */
+__device__ __forceinline__ void prof_guard(const KArgs &a)
+{
+	if (a.pguard && a.c.guard && blockIdx.x == 0 && threadIdx.x == 0)
+		for (uint32_t q = 0; q < a.pguard_n; q++)
+			a.pguard[q] = a.c.guard[q];
+}
 
 /*
  * SRTCP job of a device-planned packet, exactly as plan_rtcp_enc /

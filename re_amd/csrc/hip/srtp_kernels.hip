@@ -1030,16 +1030,18 @@ extern "C" int sgpu_setup_sessions(const struct sgpu_keyreq *req,
 #include <pthread.h>
 static pthread_mutex_t g_prof_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_prof_on;
-struct prof_ev { hipEvent_t a, b, c; int slot; uint32_t jobs;
-		  const char *name; int nr, prot; int gw; };
+struct prof_ev { hipEvent_t a, b; int slot; uint32_t jobs;
+		  const char *name; int nr, prot; int gw; int gslot; };
 static struct prof_ev *g_pev;
 static size_t g_npev, g_pev_cap;
 /* a launch behind a device plan does nothing when the plan was rejected
  * (its guard words, k_ctr_fast.h fast_class, k_ctr.h k_ctr_hmac_any, the
- * single-word guards): the words are copied to pinned memory right behind
- * the launch and such a launch is not counted as work (sgpu_prof_voided) */
+ * single-word guards): the kernel itself stores the words it saw into a
+ * pinned ring slot (KArgs.pguard, kern_common.h prof_guard) and such a
+ * launch is not counted as work (sgpu_prof_voided) */
 #define PROF_GRING 65536
-static uint32_t *g_pguard;              /* pinned, 4 words per event */
+static uint32_t *g_pguard;              /* pinned, 4 words per slot */
+static size_t g_ngslot;                 /* ring slots handed out */
 static uint64_t g_prof_voided;
 static double g_prof_ms[32];
 static uint64_t g_prof_launch[32], g_prof_jobs[32];
@@ -1059,13 +1061,13 @@ static void prof_drain_locked(void)
 {
 	for (size_t k = 0; k < g_npev; k++) {
 		float ms = 0;
-		(void)hipEventSynchronize(g_pev[k].gw ? g_pev[k].c : g_pev[k].b);
+		(void)hipEventSynchronize(g_pev[k].b);
 		(void)hipEventElapsedTime(&ms, g_pev[k].a, g_pev[k].b);
 		if (g_pev[k].gw) {
-			const uint32_t *w = g_pguard + 4 * k;
+			const volatile uint32_t *w = g_pguard +
+						     4 * g_pev[k].gslot;
 			const bool work = g_pev[k].gw == 4 ?
 				(!w[0] || !w[1] || !w[2] || !w[3]) : !w[0];
-			(void)hipEventDestroy(g_pev[k].c);
 			if (!work) {
 				g_prof_voided++;
 				(void)hipEventDestroy(g_pev[k].a);
@@ -1088,6 +1090,7 @@ static void prof_drain_locked(void)
 		(void)hipEventDestroy(g_pev[k].b);
 	}
 	g_npev = 0;
+	g_ngslot = 0;
 }
 
 /* slot = prot*16 + mode*8 + (nr==14)*4 + shift; reading resets */
@@ -1127,15 +1130,35 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		  int nr, int prot, int gw = 1)
 {
 	struct prof_ev pe;
-	int prof = 0;
+	KArgs b = a;
+	int prof = 0, gslot = -1;
 	if (g_prof_on && slot >= 0) {
 		prof = hipEventCreate(&pe.a) == hipSuccess &&
 		       hipEventCreate(&pe.b) == hipSuccess;
+		if (prof && a.c.guard) {
+			/* a ring slot for the guard words the kernel sees */
+			pthread_mutex_lock(&g_prof_lock);
+			if (!g_pguard &&
+			    hipHostMalloc((void **)&g_pguard, PROF_GRING * 16,
+					  hipHostMallocDefault) != hipSuccess)
+				g_pguard = NULL;
+			if (g_pguard && g_ngslot < PROF_GRING)
+				gslot = (int)g_ngslot++;
+			pthread_mutex_unlock(&g_prof_lock);
+		}
+		if (gslot >= 0) {
+			/* 0 = work, for a kernel that does not store its
+			 * guard; the launch below orders these writes */
+			for (int q = 0; q < 4; q++)
+				g_pguard[4 * gslot + q] = 0;
+			b.pguard = g_pguard + 4 * gslot;
+			b.pguard_n = gw == 4 ? 4u : 1u;
+		}
 		if (prof)
 			(void)hipEventRecord(pe.a, stream);
 	}
 	hipLaunchKernelGGL(f, dim3((n + block - 1) / block), dim3(block), 0,
-			   stream, a);
+			   stream, b);
 	int e = herr(hipGetLastError(), "kernel launch");
 	if (prof) {
 		(void)hipEventRecord(pe.b, stream);
@@ -1144,7 +1167,8 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 		pe.name = name;
 		pe.nr = nr;
 		pe.prot = prot;
-		pe.gw = 0;
+		pe.gw = gslot >= 0 ? (int)b.pguard_n : 0;
+		pe.gslot = gslot;
 		pthread_mutex_lock(&g_prof_lock);
 		if (g_npev == g_pev_cap) {
 			size_t nc = g_pev_cap ? 2 * g_pev_cap : 64;
@@ -1154,19 +1178,6 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 				g_pev = np;
 				g_pev_cap = nc;
 			}
-		}
-		if (!g_pguard &&
-		    hipHostMalloc((void **)&g_pguard, PROF_GRING * 16,
-				  hipHostMallocDefault) != hipSuccess)
-			g_pguard = NULL;
-		if (a.c.guard && g_pguard && g_npev < PROF_GRING &&
-		    g_npev < g_pev_cap &&
-		    hipEventCreate(&pe.c) == hipSuccess) {
-			pe.gw = gw == 4 ? 4 : 1;
-			(void)hipMemcpyAsync(g_pguard + 4 * g_npev, a.c.guard,
-					     4u * pe.gw, hipMemcpyDeviceToHost,
-					     stream);
-			(void)hipEventRecord(pe.c, stream);
 		}
 		if (g_npev < g_pev_cap)
 			g_pev[g_npev++] = pe;

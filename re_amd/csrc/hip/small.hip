@@ -4,7 +4,7 @@
  *
  * Every unchanged libre caller protects one mbuf per srtp_encrypt() call
  * (reference src/srtp/srtp.c:183-285; unprotect :288-432).  Concurrent
- * calls share a launch (host srtp.c one/pc_run) but a launch still carries
+ * calls share a launch (host percall.c one/pc_run) but a launch still carries
  * only a handful of packets, so its cost is latency, not bandwidth.  The
  * general path pays four copies (packets and jobs up, verdicts and packets
  * down), two kernels (k_ctr_coop + the MAC-only k_ctr_hmac) and a sync.

@@ -35,59 +35,8 @@
 #include "../srtpgpu.h"
 #include "fault.h"
 #include "pool.h"
+#include "srtp_int.h"
 
-#ifndef EAUTH
-#define EAUTH 217               /* include/re_types.h:215-217 */
-#endif
-
-#define SRTP_MAX_STREAMS 8      /* src/srtp/stream.c:16-17 */
-
-enum { OP_RTP_ENC = 0, OP_RTP_DEC = 1, OP_RTCP_ENC = 2, OP_RTCP_DEC = 3 };
-
-struct replay {
-	uint64_t bitmap;
-	uint64_t lix;
-};
-
-struct srtp_stream {
-	struct replay replay_rtp;
-	struct replay replay_rtcp;
-	uint32_t ssrc;
-	uint32_t roc;
-	uint16_t s_l;
-	uint8_t s_l_set;
-	uint32_t rtcp_index;
-	uint32_t epoch;         /* fast path: call that last logged it */
-};
-
-struct comp {
-	int has_aes;
-	int mode;               /* SGPU_MODE_* */
-	int has_hmac;
-	int encrypted;
-	uint32_t tag_len;
-	uint32_t nr;
-	uint32_t dev;           /* sgpu_comp index in the device table */
-};
-
-struct srtp {
-	/* hot fields first: one cache line with stream 0 covers what the
-	 * batch paths read per session (count, device slot, suite) */
-	unsigned nstreams;
-	uint32_t slot;          /* device session table slot */
-	int suite;              /* enum srtp_suite */
-	struct srtp_stream streams[SRTP_MAX_STREAMS];
-	struct comp rtp, rtcp;
-	int dev;
-	uint32_t mp_epoch;      /* multi-session plan: call that gathered it
-				   (detects sessv entries aliasing one
-				   context) */
-	int dres;               /* where stream 0's RTP state lives: DRES_* */
-	uint64_t pend_p;        /* async: last pending single-stream call on
-				   it (issuing thread's sequence number) */
-	uint64_t pend_m;        /* ... last pending multi-session call */
-	const struct tk_owner *pend_own; /* the thread that issued them */
-};
 
 /*
  * Completion counter of one thread's asynchronous calls, readable by every
@@ -97,9 +46,6 @@ struct srtp {
  * Allocated on a thread's first asynchronous call and never freed
  * (sessions may name it after the thread has exited).
  */
-struct tk_owner {
-	uint64_t done;          /* sequence number of the last completed call */
-};
 
 static __thread struct tk_owner *t_own;
 
@@ -111,7 +57,7 @@ static struct tk_owner *tk_me(void)
 }
 
 /* another thread's asynchronous call on s is still pending */
-static int sess_busy(const struct srtp *s)
+int sess_busy(const struct srtp *s)
 {
 	const struct tk_owner *o = s->pend_own;
 	uint64_t p;
@@ -133,44 +79,7 @@ enum { DRES_HOST = 0, DRES_BOTH = 1, DRES_DEV = 2, DRES_LISTED = 3 };
 /* ------------------------------------------------------------------ */
 /* tuning / diagnostics switches, read once (not per batch)             */
 
-static struct {
-	int noplan;             /* RE_SRTP_NOPLAN: no device planners */
-	int general;            /* RE_SRTP_GENERAL: general engine only */
-	int perclass;           /* RE_SRTP_PERCLASS: one launch per class */
-	int nolean;             /* RE_SRTP_NOLEAN: general CTR kernels for
-				   device-planned single-key batches */
-	int nocombine;          /* srtp_gpu_tune nocombine: per-packet calls
-				   of different threads do not share launches */
-	int nomk;               /* srtp_gpu_tune nomk: multi-session plans on
-				   the general per-lane-key kernel */
-	int splan;              /* srtp_gpu_tune splan: single-session RTP
-				   batches through the per-stream planner */
-	int mpradix;            /* srtp_gpu_tune mpradix: multi-session plans
-				   group by the radix sort (not counting) */
-	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
-				   device-planned batch fold on the host */
-	int nosmall;            /* RE_SRTP_NOSMALL: the per-packet path's small
-				   CTR launches take the general kernels
-				   with copies (not sgpu_run_small) */
-	long pcrunners;         /* srtp_gpu_tune pcrunners: per-packet runners
-				   at once (default PC_RUNNERS, at most
-				   PC_SLOTS) */
-	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
-				   per-packet caller spins before it sleeps
-				   (default 1000) */
-	int rxseq;              /* srtp_gpu_tune rxseq: srtp_rx_index* and
-				   srtp_rx_fold walk sequentially (A/B) */
-	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
-				   launch by a stream synchronisation, not
-				   its completion word */
-	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
-				   shared per-packet launch run as separate
-				   launches (helper thread), not one */
-	int trace;              /* RE_SRTP_TRACE: per-call phase times */
-	int times;              /* RE_SRTP_TIMES: multi-session phases */
-	size_t chunk;           /* RE_SRTP_CHUNK: host-scan chunk */
-	size_t par_min;         /* RE_SRTP_PAR_MIN: sessions per pool part */
-} g_env;
+struct srtp_env g_env;
 static pthread_once_t g_env_once = PTHREAD_ONCE_INIT;
 
 static void env_read(void)
@@ -206,25 +115,19 @@ static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
-static uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
-static uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
-static uint64_t g_cnt_rxw_redo; /* srtp_rx_index*: parts walked again */
-static uint64_t g_cnt_pcfused;  /* ... of which several operations in one
+uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
+uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
+uint64_t g_cnt_rxw_redo; /* srtp_rx_index*: parts walked again */
+uint64_t g_cnt_pcfused;  /* ... of which several operations in one
 				   small launch (pc_run_fused) */
 static uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
 				   host completed, re-run when waited for */
 /* the per-packet path's small launches and where their time goes (ns):
  * the host work of run_mbufs_, the launch call, the synchronisation */
-static uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
+uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
 /* pc_run_fused: host time before the launch and after the sync (ns) */
-static uint64_t g_ns_fused_prep, g_ns_fused_post;
+uint64_t g_ns_fused_prep, g_ns_fused_post;
 
-static uint64_t mono_ns(void)
-{
-	struct timespec ts;
-	clock_gettime(CLOCK_MONOTONIC, &ts);
-	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-}
 /* fault injection (srtp_gpu_tune "fail_grow", like the reference's
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
  * now fails with ENOMEM */
@@ -236,10 +139,6 @@ long re_amd_fail_alloc;
 extern size_t re_amd_mem_live(void) __attribute__((weak));
 static uint32_t slots_live(void);
 
-static void count(uint64_t *c, uint64_t v)
-{
-	__atomic_add_fetch(c, v, __ATOMIC_RELAXED);
-}
 
 uint64_t srtp_gpu_counter(const char *name)
 {
@@ -361,7 +260,7 @@ static uint32_t *g_free;
 static uint32_t g_nfree, g_free_cap, g_next_slot;
 static int g_gpu_state;         /* 0 unknown, 1 ok, -1 unavailable */
 
-static int gpu_ready(void)
+int gpu_ready(void)
 {
 	int r;
 	pthread_mutex_lock(&g_lock);
@@ -431,13 +330,13 @@ static int slots_get(uint32_t *slots, size_t n)
 	return err;
 }
 
-static void table_rdlock(void)
+void table_rdlock(void)
 {
 	env_init();
 	pthread_rwlock_rdlock(&g_table_rw);
 }
 
-static void table_unlock(void)
+void table_unlock(void)
 {
 	pthread_rwlock_unlock(&g_table_rw);
 }
@@ -464,7 +363,7 @@ static void slot_put(uint32_t s)
 /* srtp_alloc (srtp.c:88-180)                                          */
 
 static void tk_drain(void);
-static int tk_pending(void);
+int tk_pending(void);
 
 static void destructor(void *arg)
 {
@@ -644,7 +543,7 @@ static int stream_get_seq(struct srtp_stream **sp, struct srtp *s,
 }
 
 /* replay.c:32-62 (64-packet window) */
-static int replay_check(struct replay *r, uint64_t ix)
+int replay_check(struct replay *r, uint64_t ix)
 {
 	uint64_t diff;
 	if (ix > r->lix) {
@@ -668,7 +567,7 @@ static int replay_check(struct replay *r, uint64_t ix)
 }
 
 /* misc.c:22-41, including the `int v` sign extension of roc+-1 */
-static uint64_t get_index(uint32_t roc, uint16_t s_l, uint16_t seq)
+uint64_t get_index(uint32_t roc, uint16_t s_l, uint16_t seq)
 {
 	int32_t v;
 	if (s_l < 32768) {
@@ -689,30 +588,7 @@ static uint64_t get_index(uint32_t roc, uint16_t s_l, uint16_t seq)
 /* ------------------------------------------------------------------ */
 /* per-packet planning                                                  */
 
-struct pinfo {
-	uint32_t start, end, size;
-	uint32_t hdr_len;       /* UINT32_MAX on EBADMSG */
-	uint32_t err_pos;       /* bytes consumed before EBADMSG */
-	uint32_t ssrc;
-	uint16_t seq;
-	uint32_t eix[3];        /* RTCP: BE word at end-4-tl, tl = 0, 4, 10 */
-	uint8_t fixed;          /* device arena: size is a hard cap */
-};
 
-struct rec {
-	int32_t err;
-	uint32_t pos_o, end_o, size_o;
-	uint8_t has_job;
-	uint8_t need_run;
-	uint8_t ran;
-	uint8_t vd;             /* verdict bits of the last run */
-	uint8_t need_undo;
-	uint32_t in_end;        /* stage bytes [start, in_end) */
-	uint32_t ext_end;       /* GPU may write up to here */
-	struct sgpu_job job;
-	struct sgpu_job ran_job;
-	uint32_t save;          /* original tag word (device path undo) */
-};
 
 static uint32_t grow(uint32_t size, uint32_t need)
 {
@@ -725,7 +601,7 @@ static uint32_t grow(uint32_t size, uint32_t need)
 }
 
 /* RTP header parse over host bytes (rtp.c:88-137) */
-static void parse_rtp(struct pinfo *pi, const uint8_t *buf)
+void parse_rtp(struct pinfo *pi, const uint8_t *buf)
 {
 	const uint32_t left = pi->end > pi->start ? pi->end - pi->start : 0;
 	const uint8_t *b = buf + pi->start;
@@ -1211,17 +1087,6 @@ static void plan_rtcp_dec(struct srtp *s, const struct pinfo *pi,
 /* ------------------------------------------------------------------ */
 /* the batch engine                                                     */
 
-struct engine {
-	int op;
-	size_t n;
-	struct srtp **sess;        /* per packet session */
-	struct pinfo *pi;
-	struct rec *rec;
-	/* snapshot of every distinct session's stream state */
-	struct srtp **uniq;
-	size_t nuniq;
-	struct srtp *snap;
-};
 
 static void snap_take(struct engine *E)
 {
@@ -1303,56 +1168,15 @@ static void engine_free(struct engine *E)
 
 /* ---- GPU rounds ----------------------------------------------------- */
 
-struct pool {
-	uint8_t *h;             /* pinned host */
-	uint8_t *d;             /* device */
-	size_t cap;
-};
 
-struct ulog {
-	struct srtp *s;                 /* session entry: old nstreams */
-	struct srtp_stream *st;         /* stream entry: old state */
-	unsigned nstreams;
-	struct srtp_stream old;
-};
 
-struct ulogv {
-	struct ulog *v;
-	size_t n, cap;
-};
 
-struct ws {
-	void *stream;
-	struct pool ctl;        /* jobs | verdict | save */
-	struct pool stage;      /* host path: packet bytes */
-	struct pool hdr;        /* device path: pos/end, parsed headers */
-	uint32_t *cls_idx;
-	size_t cls_cap;
-	/* compact fast path */
-	void *pstream;          /* header parse + D2H stream */
-	struct pool up;         /* pos | end | sess (original values) */
-	struct pool hd;         /* parsed headers */
-	struct pool dsc;        /* descriptors | class lists */
-	struct pool vs;         /* verdict | save | nfail */
-	struct pool cm;         /* session -> comp index */
-	struct pool pl;         /* device planner: out | scratch */
-	struct pool es;         /* device API: original ends */
-	struct pool ms;         /* multi-session plan: states in | out */
-	struct pool mscr;       /* multi-session plan: device scratch */
-	void **ev;              /* per-chunk parse events */
-	size_t nev;
-	struct ulogv ulog[1];   /* stream-state undo log */
-	/* the small kernel's completion word (small_wait) */
-	uint32_t *sm_cnt;       /* device */
-	uint32_t *sm_flag;      /* pinned host */
-	uint32_t sm_seq;
-};
 
 
 
 static __thread struct ws *t_ws;
 
-static struct ws *ws_new(void)
+struct ws *ws_new(void)
 {
 	struct ws *w = fi_calloc(1, sizeof(*w));
 	if (!w)
@@ -1366,9 +1190,9 @@ static struct ws *ws_new(void)
 }
 
 /* a per-packet runner's slot workspace while it runs (pc_slot_ws) */
-static __thread struct ws *t_ws_use;
+__thread struct ws *t_ws_use;
 
-static struct ws *ws_get(void)
+struct ws *ws_get(void)
 {
 	if (t_ws_use)
 		return t_ws_use;
@@ -1384,7 +1208,7 @@ static struct ws *ws_get(void)
  * checking the stream for an error now and then.  Without the word (its
  * allocation failed) a plain synchronisation.
  */
-static int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
+int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 		     const struct sgpu_job *jobs, uint32_t m, uint8_t *vh,
 		     uint32_t *sv, int prot, uint64_t *t_launch)
 {
@@ -1434,7 +1258,7 @@ static int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 	}
 }
 
-static int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
+int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
 {
 	size_t c;
 	if (bytes <= p->cap)
@@ -1459,7 +1283,7 @@ static int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
 	return 0;
 }
 
-static int idx_reserve(struct ws *w, size_t n)
+int idx_reserve(struct ws *w, size_t n)
 {
 	if (n > w->cls_cap) {
 		size_t c = n + n / 2 + 64;
@@ -1615,7 +1439,7 @@ static int round_fetch(struct ws *w, uint32_t m, void *stream)
 			       stream);
 }
 
-static void collect_rec(struct rec *r, uint8_t v, uint32_t save)
+void collect_rec(struct rec *r, uint8_t v, uint32_t save)
 {
 	r->ran = 1;
 	r->ran_job = r->job;
@@ -1635,7 +1459,7 @@ static void round_collect(struct ws *w, struct engine *E, uint32_t m)
 
 /* #jobs of a planned round if the small kernel can take all of them,
  * else (size_t)-1 */
-static size_t small_fits(const struct engine *E)
+size_t small_fits(const struct engine *E)
 {
 	size_t i, need = 0;
 	for (i = 0; i < E->n; i++) {
@@ -1718,7 +1542,7 @@ static int round_small(struct ws *w, struct engine *E, uint64_t asz,
  * (DRES_DEV) are read back in one transfer; all end up DRES_HOST (the
  * path may change them).  Needs the table read lock.
  */
-static int sess_host(struct srtp **sessv, size_t nsess)
+int sess_host(struct srtp **sessv, size_t nsess)
 {
 	struct srtp **lst = NULL;
 	uint32_t *slots = NULL;
@@ -1793,19 +1617,8 @@ static int sess_host(struct srtp **sessv, size_t nsess)
  * run_mbufs_core drives one operation; pc_run_fused drives the first round
  * of several operations as one launch.
  */
-struct mbc {
-	int op, prot, snapped, done;
-	struct engine E;
-	struct mbuf **mbv;
-	int *errv;
-	size_t n, round;
-	uint8_t **outp;         /* where packet i's GPU output lives */
-	uint8_t *keep;          /* per-packet copies across rounds */
-	uint32_t *soff;         /* staging offsets */
-	size_t *koff;
-};
 
-static int mbc_init(struct mbc *c, int op, struct srtp **sessv, size_t nsess,
+int mbc_init(struct mbc *c, int op, struct srtp **sessv, size_t nsess,
 		    const uint32_t *sidx, struct mbuf **mbv, int *errv,
 		    size_t n)
 {
@@ -1848,7 +1661,7 @@ static int mbc_init(struct mbc *c, int op, struct srtp **sessv, size_t nsess,
 }
 
 /* the plan of the next round from the snapshot: #packets to run */
-static size_t mbc_plan(struct mbc *c)
+size_t mbc_plan(struct mbc *c)
 {
 	snap_restore(&c->E);
 	return plan_all(&c->E);
@@ -1856,7 +1669,7 @@ static size_t mbc_plan(struct mbc *c)
 
 /* staging is about to be reused: move the outputs of earlier rounds aside
  * (from round 1 on; idempotent) */
-static int mbc_aside(struct mbc *c)
+int mbc_aside(struct mbc *c)
 {
 	const struct engine *E = &c->E;
 	size_t i;
@@ -1884,7 +1697,7 @@ static int mbc_aside(struct mbc *c)
 }
 
 /* stage the packets that need a run at 16-B aligned offsets from base */
-static size_t mbc_offsets(struct mbc *c, size_t base)
+size_t mbc_offsets(struct mbc *c, size_t base)
 {
 	const struct engine *E = &c->E;
 	size_t i, bytes = base;
@@ -1898,7 +1711,7 @@ static size_t mbc_offsets(struct mbc *c, size_t base)
 	return bytes;
 }
 
-static void mbc_stage(struct mbc *c, uint8_t *stage)
+void mbc_stage(struct mbc *c, uint8_t *stage)
 {
 	struct engine *E = &c->E;
 	size_t i;
@@ -1913,7 +1726,7 @@ static void mbc_stage(struct mbc *c, uint8_t *stage)
 	}
 }
 
-static void mbc_ran(struct mbc *c, uint8_t *stage)
+void mbc_ran(struct mbc *c, uint8_t *stage)
 {
 	size_t i;
 	for (i = 0; i < c->n; i++)
@@ -1923,7 +1736,7 @@ static void mbc_ran(struct mbc *c, uint8_t *stage)
 }
 
 /* one round of one operation; c->done once nothing is left to run */
-static int mbc_round(struct mbc *c, struct ws *w)
+int mbc_round(struct mbc *c, struct ws *w)
 {
 	struct engine *E = &c->E;
 	size_t need, bytes;
@@ -1973,7 +1786,7 @@ static int mbc_round(struct mbc *c, struct ws *w)
 }
 
 /* the results into the caller's mbufs */
-static int mbc_finish(struct mbc *c)
+int mbc_finish(struct mbc *c)
 {
 	const struct engine *E = &c->E;
 	size_t i;
@@ -2003,7 +1816,7 @@ static int mbc_finish(struct mbc *c)
 	return 0;
 }
 
-static void mbc_free(struct mbc *c, int err)
+void mbc_free(struct mbc *c, int err)
 {
 	/* a failed call leaves the stream states as it found them */
 	if (err && c->snapped)
@@ -2036,7 +1849,7 @@ static int run_mbufs_core(int op, struct srtp **sessv, size_t nsess,
 	return err;
 }
 
-static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
+int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 		      const uint32_t *sidx, struct mbuf **mbv, int *errv,
 		      size_t n)
 {
@@ -2046,7 +1859,7 @@ static int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 	return err;
 }
 
-static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
+int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 		     size_t n)
 {
 	int err;
@@ -2059,537 +1872,6 @@ static int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 		err = run_mbufs_(op, &srtp, 1, NULL, mbv, errv, n);
 	table_unlock();
 	return err;
-}
-
-/*
- * Per-packet calls from many threads (the unchanged re_srtp.h API: every
- * libre caller protects one mbuf per call, src/srtp/srtp.c:183-432)
- * share GPU launches: a calling thread queues its packet; if no thread is
- * running a batch it becomes the runner, takes everything queued (the
- * packets of other threads that arrived meanwhile) and runs it as one
- * multi-session batch per operation.  No timer and no waiting at low
- * load: a lone caller runs its packet at once.  A struct srtp is used by
- * one thread at a time (the reference's contract), so the packets of one
- * batch belong to distinct sessions, and each thread's calls stay in its
- * own order.
- *
- * Completion is per request: the runner marks each request done and wakes
- * only its owner (a futex on the request's state word; owners spin
- * briefly first), then hands the runner role to the owner of the first
- * request queued meanwhile -- no broadcast, so 64 callers do not convoy
- * through one mutex on every batch.
- */
-#include <linux/futex.h>
-#include <sys/syscall.h>
-#include <unistd.h>
-
-enum { PC_QUEUED = 0, PC_DONE = 1, PC_RUN = 2, PC_SLEEP = 3 };
-
-struct pc_req {
-	struct pc_req *next;
-	int op;
-	struct srtp *s;
-	struct mbuf *mb;
-	int err;
-	int state;              /* PC_*, atomic: the owner waits on it */
-	int slot;               /* PC_RUN: the runner slot handed over */
-	struct pc_req *list;    /* ... and the queue it runs (from this one) */
-};
-
-static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
-static struct pc_req *pc_head, *pc_tail;
-static int pc_running;
-
-/* the owner learns v; a futex wake only if it went to sleep (PC_SLEEP) */
-static void pc_wake(int *state, int v)
-{
-	if (__atomic_exchange_n(state, v, __ATOMIC_ACQ_REL) == PC_SLEEP)
-		(void)syscall(SYS_futex, state, FUTEX_WAKE_PRIVATE, 1, NULL,
-			      NULL, 0);
-}
-
-static int pc_wait(int *state)
-{
-	long spin;
-	int v;
-	/* a short spin, then sleep: many callers spinning on fewer cores
-	 * would take the CPU from the runner and its helper */
-	const long nspin = g_env.pcspin ? g_env.pcspin : 1000;
-	for (spin = 0; spin < nspin; spin++) {
-		v = __atomic_load_n(state, __ATOMIC_ACQUIRE);
-		if (v != PC_QUEUED)
-			return v;
-		__builtin_ia32_pause();
-	}
-	for (;;) {
-		int q = PC_QUEUED;
-		if (!__atomic_compare_exchange_n(state, &q, PC_SLEEP, 0,
-						 __ATOMIC_ACQ_REL,
-						 __ATOMIC_ACQUIRE))
-			return q;       /* DONE or RUN arrived */
-		while ((v = __atomic_load_n(state, __ATOMIC_ACQUIRE)) ==
-		       PC_SLEEP)
-			(void)syscall(SYS_futex, state, FUTEX_WAIT_PRIVATE,
-				      PC_SLEEP, NULL, NULL, 0);
-		return v;
-	}
-}
-
-/* one operation's requests of a list, as multi-session batches */
-static void pc_run_op(struct pc_req *list, int op)
-{
-	enum { MAXB = 1024 };
-	struct srtp *sv[MAXB];
-	struct mbuf *mv[MAXB];
-	struct pc_req *rq[MAXB];
-	int ev[MAXB];
-	struct pc_req *r = list;
-
-	while (r) {
-		size_t n = 0, i;
-		int err;
-		for (; r && n < MAXB; r = r->next) {
-			if (r->op != op)
-				continue;
-			rq[n] = r;
-			sv[n] = r->s;
-			mv[n++] = r->mb;
-		}
-		if (!n)
-			break;
-		count(&g_cnt_pcbatch, 1);
-		count(&g_cnt_pcpkts, n);
-		table_rdlock();
-		err = sess_host(sv, n);
-		if (!err) {
-			uint32_t *idx = fi_malloc(n * sizeof(*idx));
-			if (!idx)
-				err = ENOMEM;
-			for (i = 0; !err && i < n; i++)
-				idx[i] = (uint32_t)i;
-			if (!err)
-				err = run_mbufs_(op, sv, n, idx, mv, ev, n);
-			free(idx);
-		}
-		if (err && n > 1) {
-			/* a batch-level error (one session busy with another
-			 * thread's asynchronous calls, an allocation): the
-			 * failed batch changed nothing, so each request runs on
-			 * its own and gets the result its own call would */
-			for (i = 0; i < n; i++) {
-				uint32_t zero = 0;
-				int e = sess_host(&sv[i], 1);
-				if (!e)
-					e = run_mbufs_(op, &sv[i], 1, &zero, &mv[i],
-						       &ev[i], 1);
-				rq[i]->err = e ? e : ev[i];
-			}
-			table_unlock();
-			continue;
-		}
-		table_unlock();
-		for (i = 0; i < n; i++)
-			rq[i]->err = err ? err : ev[i];
-	}
-}
-
-/*
- * Runner slots: up to pcrunners (default PC_RUNNERS) runners at once, each
- * with its slot's workspace (HIP stream, pinned pools) and helper thread,
- * so the next list is planned and launched while the previous one is on
- * the GPU.  Concurrent lists hold distinct sessions too (a session's one
- * owner thread has one call in flight).
- *
- * A list usually mixes operations (callers alternate srtp_encrypt and
- * srtp_decrypt).  Lists the small kernel takes run as one launch
- * (pc_run_fused); otherwise each operation is its own batch, and the
- * batches of two operations run at once -- one on the slot's persistent
- * helper thread (its own workspace and HIP stream), the rest on the
- * runner -- instead of one GPU round trip after the other.
- */
-/* runners 1..4 at 64 threads: 230, 278, 306, 326 K pairs/s
- * (profiles/r04_percall_runners.txt) */
-enum { PC_SLOTS = 4, PC_RUNNERS = 4 };
-
-static struct pc_slot {
-	struct ws *ws;
-	int hok;                /* helper thread running */
-	int hstate;             /* 0 idle, 1 posted, 2 done (futex word) */
-	struct pc_req *hlist;
-	int hop;
-} pc_slots[PC_SLOTS];
-static unsigned pc_slot_used;   /* under pc_lock */
-
-static void *pc_helper(void *arg)
-{
-	struct pc_slot *sl = arg;
-	for (;;) {
-		while (__atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE) != 1)
-			(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAIT_PRIVATE,
-				      __atomic_load_n(&sl->hstate,
-						      __ATOMIC_RELAXED),
-				      NULL, NULL, 0);
-		pc_run_op(sl->hlist, sl->hop);
-		__atomic_store_n(&sl->hstate, 2, __ATOMIC_RELEASE);
-		(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAKE_PRIVATE, 1,
-			      NULL, NULL, 0);
-	}
-	return NULL;
-}
-
-/* the slot's helper, started on first use (only its runner calls this) */
-static int pc_helper_ok(struct pc_slot *sl)
-{
-	if (!sl->hok) {
-		pthread_t t;
-		pthread_attr_t a;
-		pthread_attr_init(&a);
-		pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
-		sl->hok = pthread_create(&t, &a, pc_helper, sl) == 0 ? 1 : -1;
-		pthread_attr_destroy(&a);
-	}
-	return sl->hok > 0;
-}
-
-/*
- * A list mixing operations whose packets all fit the small kernel (<=
- * SGPU_SMALL_MAX bytes): every operation plans its first round
- * on the host and all of them run as ONE launch of the fused kernel (the
- * protect or unprotect body per job, by SJ_PROTECT) -- one GPU round trip
- * for the whole list instead of one per operation on two streams.  Later
- * rounds (a verdict that changes a plan) run per operation as usual.
- * Returns -1, with nothing changed, when the list does not qualify or a
- * batch-level error stopped it before any result (the caller then runs
- * the operations its usual way); else 0 with every request's result set.
- */
-static int pc_run_fused(struct pc_req *list, unsigned ops)
-{
-	struct mbc cv[4];
-	struct srtp **sv = NULL;
-	struct mbuf **mv = NULL;
-	struct pc_req **rq = NULL;
-	int *ev = NULL;
-	uint32_t *idx = NULL, mst[5], m = 0;
-	size_t base[5], need[4], tot = 0, bytes = 0, i, k;
-	int nc = 0, opk[4], err = 0, inited = 0, redo = 0;
-	const uint64_t t0 = mono_ns();
-	uint64_t t1 = t0;
-	struct pc_req *r;
-	struct sgpu_job *jh;
-	uint8_t *vh;
-	struct ws *w;
-
-	if (g_env.nosmall || g_env.nofuse)
-		return -1;
-	/* per operation, in list order */
-	base[0] = 0;
-	for (k = 0; k < 4; k++) {
-		size_t n = 0;
-		if (!((ops >> k) & 1))
-			continue;
-		for (r = list; r; r = r->next)
-			n += r->op == (int)k;
-		opk[nc] = (int)k;
-		base[nc + 1] = base[nc] + n;
-		nc++;
-	}
-	tot = base[nc];
-	if (!tot || tot > SGPU_COOP_MAX)
-		return -1;
-	sv = fi_malloc(tot * sizeof(*sv));
-	mv = fi_malloc(tot * sizeof(*mv));
-	rq = fi_malloc(tot * sizeof(*rq));
-	ev = fi_malloc(tot * sizeof(*ev));
-	idx = fi_malloc(tot * sizeof(*idx));
-	if (!sv || !mv || !rq || !ev || !idx) {
-		err = -1;
-		goto out_free;
-	}
-	for (k = 0; k < (size_t)nc; k++) {
-		i = base[k];
-		for (r = list; r; r = r->next)
-			if (r->op == opk[k]) {
-				rq[i] = r;
-				sv[i] = r->s;
-				mv[i] = r->mb;
-				idx[i] = (uint32_t)(i - base[k]);
-				i++;
-			}
-	}
-
-	table_rdlock();
-	w = ws_get();
-	err = w ? 0 : ENOMEM;
-	for (k = 0; !err && k < (size_t)nc; k++)
-		err = sess_host(sv + base[k], base[k + 1] - base[k]);
-	for (k = 0; !err && k < (size_t)nc; k++) {
-		const size_t b = base[k], n = base[k + 1] - b;
-		inited = (int)k + 1;
-		err = mbc_init(&cv[k], opk[k], sv + b, n, idx + b, mv + b,
-			       ev + b, n);
-	}
-	/* round 0: every operation planned; the small kernel takes all? */
-	for (k = 0; !err && k < (size_t)nc; k++) {
-		need[k] = mbc_plan(&cv[k]);
-		if (small_fits(&cv[k].E) == (size_t)-1)
-			err = -1;
-	}
-	for (k = 0; !err && k < (size_t)nc; k++)
-		bytes = mbc_offsets(&cv[k], bytes);
-	if (!err)
-		err = pool_reserve(w, &w->stage, bytes);
-	if (!err)
-		err = pool_reserve(w, &w->ctl, tot * (sizeof(struct sgpu_job) + 5));
-	if (!err)
-		err = idx_reserve(w, tot);
-	if (err)
-		goto out;
-	jh = (struct sgpu_job *)w->ctl.h;
-	for (k = 0; k < (size_t)nc; k++) {
-		struct mbc *c = &cv[k];
-		mbc_stage(c, w->stage.h);
-		mst[k] = m;
-		for (i = 0; i < c->n; i++) {
-			const struct rec *rc = &c->E.rec[i];
-			if (!rc->need_run)
-				continue;
-			jh[m] = rc->job;
-			jh[m].off = c->soff[i];
-			w->cls_idx[m++] = (uint32_t)i;
-		}
-	}
-	mst[nc] = m;
-	vh = w->ctl.h + (size_t)m * sizeof(struct sgpu_job);
-	t1 = mono_ns();
-	count(&g_ns_fused_prep, t1 - t0);
-	if (m) {
-		uint64_t tl;
-		err = small_run(w, w->stage.h, bytes, jh, m, vh,
-				(uint32_t *)(vh + m), 2, &tl);
-		count(&g_cnt_small, 1);
-		count(&g_ns_small_launch, tl);
-		count(&g_ns_small_sync, mono_ns() - t1 - tl);
-		t1 = mono_ns();
-		if (err)
-			goto out;
-	}
-	count(&g_cnt_pcbatch, 1);
-	count(&g_cnt_pcpkts, tot);
-	count(&g_cnt_pcfused, 1);
-	for (k = 0; k < (size_t)nc; k++) {
-		struct mbc *c = &cv[k];
-		uint32_t q;
-		if (!need[k]) {
-			c->done = 1;
-			continue;
-		}
-		for (q = mst[k]; q < mst[k + 1]; q++)
-			collect_rec(&c->E.rec[w->cls_idx[q]], vh[q],
-				    ((const uint32_t *)(vh + m))[q]);
-		mbc_ran(c, w->stage.h);
-	}
-	/* later rounds reuse the staging memory: every operation's outputs
-	 * aside first if any operation needs one */
-	for (k = 0; k < (size_t)nc; k++)
-		if (!cv[k].done && mbc_plan(&cv[k]))
-			break;
-	if (k < (size_t)nc)
-		for (k = 0; k < (size_t)nc; k++)
-			if (mbc_aside(&cv[k]))
-				redo = 1;
-	for (k = 0; k < (size_t)nc; k++) {
-		struct mbc *c = &cv[k];
-		const size_t b = base[k], n = base[k + 1] - b;
-		int e = redo ? ENOMEM : 0;
-		while (!e && !c->done)
-			e = mbc_round(c, w);
-		if (!e)
-			e = mbc_finish(c);
-		mbc_free(c, e);
-		if (!e) {
-			for (i = b; i < b + n; i++)
-				rq[i]->err = ev[i];
-			continue;
-		}
-		/* this operation as it found it: each request on its own,
-		 * with the result its own call would get */
-		for (i = b; i < b + n; i++) {
-			uint32_t zero = 0;
-			int e1 = sess_host(&sv[i], 1);
-			if (!e1)
-				e1 = run_mbufs_(opk[k], &sv[i], 1, &zero, &mv[i],
-						&ev[i], 1);
-			rq[i]->err = e1 ? e1 : ev[i];
-		}
-	}
-	inited = 0;
-	count(&g_ns_fused_post, mono_ns() - t1);
- out:
-	/* nothing ran, or the launch failed: every operation as it was */
-	for (k = 0; k < (size_t)inited; k++)
-		mbc_free(&cv[k], 1);
-	table_unlock();
-	count(&g_ns_mbufs, mono_ns() - t0);
- out_free:
-	free(sv);
-	free(mv);
-	free(rq);
-	free(ev);
-	free(idx);
-	return err ? -1 : 0;
-}
-
-static void pc_run(struct pc_req *list, struct pc_slot *sl)
-{
-	unsigned ops = 0;
-	int op, first = -1;
-	struct pc_req *r;
-
-	for (r = list; r; r = r->next)
-		ops |= 1u << r->op;
-	if ((ops & (ops - 1)) && pc_run_fused(list, ops) == 0)
-		return;
-	if ((ops & (ops - 1)) && pc_helper_ok(sl)) {
-		/* the lowest operation to the slot's helper */
-		first = __builtin_ctz(ops);
-		sl->hlist = list;
-		sl->hop = first;
-		__atomic_store_n(&sl->hstate, 1, __ATOMIC_RELEASE);
-		(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAKE_PRIVATE, 1,
-			      NULL, NULL, 0);
-	}
-	for (op = 0; op < 4; op++)
-		if ((ops >> op) & 1 && op != first)
-			pc_run_op(list, op);
-	if (first >= 0) {
-		int v;
-		while ((v = __atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE)) != 2)
-			(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAIT_PRIVATE,
-				      v, NULL, NULL, 0);
-		__atomic_store_n(&sl->hstate, 0, __ATOMIC_RELAXED);
-	}
-}
-
-static int one(int op, struct srtp *srtp, struct mbuf *mb)
-{
-	struct pc_req req;
-	struct pc_slot *sl;
-	int e = 0, err, run, slot = 0, nrun;
-
-	if (!srtp || !mb)
-		return EINVAL;
-	if (sess_busy(srtp))
-		return EBUSY;   /* another thread's asynchronous call on it */
-	if (g_env.nocombine || tk_pending()) {
-		err = run_mbufs(op, srtp, &mb, &e, 1);
-		return err ? err : e;
-	}
-	memset(&req, 0, sizeof(req));
-	req.op = op;
-	req.s = srtp;
-	req.mb = mb;
-	nrun = g_env.pcrunners > 0 ? (int)g_env.pcrunners : PC_RUNNERS;
-	if (nrun > PC_SLOTS)
-		nrun = PC_SLOTS;
-	pthread_mutex_lock(&pc_lock);
-	if (pc_tail)
-		pc_tail->next = &req;
-	else
-		pc_head = &req;
-	pc_tail = &req;
-	run = pc_running < nrun;
-	if (run) {
-		/* a free slot: run the queue now (taken here, in the same
-		 * critical section, so no hand-off can take this request) */
-		pc_running++;
-		slot = __builtin_ctz(~pc_slot_used);
-		pc_slot_used |= 1u << slot;
-		req.list = pc_head;
-		pc_head = pc_tail = NULL;
-	}
-	pthread_mutex_unlock(&pc_lock);
-	if (!run && pc_wait(&req.state) == PC_DONE)
-		return req.err;
-	/* the runner (PC_RUN: slot and queue handed over): its queue on the
-	 * slot's workspace, then the slot and the queue gathered meanwhile to
-	 * that queue's first request (or the slot is freed) */
-	slot = req.slot = run ? slot : req.slot;
-	sl = &pc_slots[slot];
-	if (!sl->ws)
-		sl->ws = ws_new();      /* the slot is this thread's alone */
-	{
-		struct pc_req *list = req.list, *r, *nx, *next_runner;
-		t_ws_use = sl->ws;      /* NULL: this thread's own */
-		pc_run(list, sl);
-		t_ws_use = NULL;
-		/* the next batch first: hand the runner role on, then
-		 * complete this one's callers */
-		pthread_mutex_lock(&pc_lock);
-		next_runner = pc_head;
-		if (next_runner) {
-			next_runner->slot = slot;
-			next_runner->list = pc_head;
-			pc_head = pc_tail = NULL;
-		}
-		else {
-			pc_running--;
-			pc_slot_used &= ~(1u << slot);
-		}
-		pthread_mutex_unlock(&pc_lock);
-		if (next_runner)
-			pc_wake(&next_runner->state, PC_RUN);
-		for (r = list; r; r = nx) {
-			nx = r->next;   /* r may be gone once woken */
-			if (r != &req)
-				pc_wake(&r->state, PC_DONE);
-		}
-	}
-	return req.err;
-}
-
-int srtp_encrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
-		       size_t n)
-{
-	return run_mbufs(OP_RTP_ENC, srtp, mbv, errv, n);
-}
-
-int srtp_decrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
-		       size_t n)
-{
-	return run_mbufs(OP_RTP_DEC, srtp, mbv, errv, n);
-}
-
-int srtcp_encrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
-			size_t n)
-{
-	return run_mbufs(OP_RTCP_ENC, srtp, mbv, errv, n);
-}
-
-int srtcp_decrypt_mbufs(struct srtp *srtp, struct mbuf **mbv, int *errv,
-			size_t n)
-{
-	return run_mbufs(OP_RTCP_DEC, srtp, mbv, errv, n);
-}
-
-
-int srtp_encrypt(struct srtp *srtp, struct mbuf *mb)
-{
-	return one(OP_RTP_ENC, srtp, mb);
-}
-
-int srtp_decrypt(struct srtp *srtp, struct mbuf *mb)
-{
-	return one(OP_RTP_DEC, srtp, mb);
-}
-
-int srtcp_encrypt(struct srtp *srtp, struct mbuf *mb)
-{
-	return one(OP_RTCP_ENC, srtp, mb);
-}
-
-int srtcp_decrypt(struct srtp *srtp, struct mbuf *mb)
-{
-	return one(OP_RTCP_DEC, srtp, mb);
 }
 
 /* ---- device-resident front-end ---------------------------------------- */
@@ -4955,7 +4237,7 @@ static void tk_finish_one(void)
 
 /* this thread has asynchronous calls pending (their sessions must not
  * be handed to another thread's shared launch) */
-static int tk_pending(void)
+int tk_pending(void)
 {
 	return t_tk_head != NULL;
 }
@@ -5370,532 +4652,6 @@ int srtp_stream_import(struct srtp *srtp, const struct srtp_stream_state *st)
 	s->s_l = st->s_l;
 	s->s_l_set = st->s_l_set;
 	s->rtcp_index = st->rtcp_index;
-	return 0;
-}
-
-/* ---- cross-rank replay fold (include/re_srtp_batch.h) ----------------- */
-
-/* the rank's own receiver over one packet (srtp.c:310-321 + the s_l
- * update of :426-427); ok: rtp_hdr_decode succeeded.  0 or EINVAL (another
- * SSRC) */
-struct rx_walk {
-	uint32_t ssrc, roc;
-	uint16_t s_l;
-	uint8_t set;
-};
-
-static int rx_step(struct rx_walk *x, int ok, uint32_t ssrc, uint16_t seq,
-		   int32_t res, struct srtp_rx_rec *r)
-{
-	int diff;
-	r->ix = 0;
-	r->res = res;
-	r->seq = 0;
-	r->pad = 0;
-	if (!ok) {
-		r->stage = SRTP_RX_NOHDR;
-		return 0;
-	}
-	if (ssrc != x->ssrc)
-		return EINVAL;
-	r->seq = seq;
-	if (!x->set) {
-		x->s_l = seq;
-		x->set = 1;
-	}
-	diff = (int)seq - (int)x->s_l;
-	if (diff > 32768) {
-		r->stage = SRTP_RX_NOIX;
-		return 0;
-	}
-	if (diff <= -32768) {
-		x->roc++;
-		x->s_l = 0;
-	}
-	r->stage = SRTP_RX_IX;
-	r->ix = get_index(x->roc, x->s_l, seq);
-	if (res == 0 && seq > x->s_l)
-		x->s_l = seq;
-	return 0;
-}
-
-static int rx_walk_packed(const struct srtp_stream_state *st0,
-			  const uint32_t *pk, const int32_t *rh, size_t n,
-			  struct srtp_rx_rec *rec);
-
-int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
-		  const uint32_t *pos, const uint32_t *end,
-		  const int32_t *res, size_t n, struct srtp_rx_rec *rec)
-{
-	uint32_t *pk;
-	size_t i;
-	int err;
-
-	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)))
-		return EINVAL;
-	if (!n)
-		return 0;
-	/* the headers parsed here, then the walk of srtp_rx_index_dev */
-	pk = fi_malloc(n * sizeof(*pk));
-	if (!pk)
-		return ENOMEM;
-	for (i = 0; i < n; i++) {
-		struct pinfo pi;
-		memset(&pi, 0, sizeof(pi));
-		pi.start = pos[i];
-		pi.end = end[i];
-		parse_rtp(&pi, arena);
-		pk[i] = pi.hdr_len == UINT32_MAX ? 0u :
-			(uint32_t)pi.seq | 1u << 16 |
-			(pi.ssrc != st0->ssrc ? 1u << 17 : 0u);
-	}
-	err = rx_walk_packed(st0, pk, res, n, rec);
-	free(pk);
-	return err;
-}
-
-/*
- * The walk over packed words (k_rx_pack: seq | ok << 16 | other SSRC << 17
- * | res << 24, or res from rh) in parallel parts: part k > 0 guesses its
- * start state by a cold walk over the W packets before it (the receiver's
- * s_l is the newest accepted in-window seq, which a few hundred packets
- * re-establish) and walks with a relative ROC; then, in order, each
- * guess is checked against the previous part's true end state -- a part
- * whose guess was wrong is walked again from the true state, a right one
- * gets its ROC base added to its indices (get_index is linear in the ROC
- * while it stays below 2^31, which the caller checks).  Same records as
- * the sequential walk.
- */
-enum { RXW_PARTS = 16, RXW_WARM = 512 };
-
-struct rxw {
-	const uint32_t *pk;
-	const int32_t *rh;
-	struct srtp_rx_rec *rec;
-	size_t n;
-	struct rx_walk st0;
-	struct rx_walk guess[RXW_PARTS], end[RXW_PARTS];
-	int bad[RXW_PARTS];
-	uint32_t base[RXW_PARTS];
-};
-
-static size_t rxw_lo(const struct rxw *q, size_t k)
-{
-	return q->n * k / RXW_PARTS;
-}
-
-/* packets [lo, hi) from *x; 1 if one has another SSRC */
-static int rxw_walk(const struct rxw *q, struct rx_walk *x, size_t lo,
-		    size_t hi, int store)
-{
-	size_t i;
-	for (i = lo; i < hi; i++) {
-		const uint32_t v = q->pk[i];
-		const int32_t r = q->rh ? q->rh[i] : (int32_t)(v >> 24);
-		struct srtp_rx_rec tmp;
-		if ((v >> 17) & 1)
-			return 1;
-		(void)rx_step(x, (v >> 16) & 1, x->ssrc, (uint16_t)v, r,
-			      store ? &q->rec[i] : &tmp);
-	}
-	return 0;
-}
-
-static void rxw_part(void *arg, size_t k0, size_t k1)
-{
-	struct rxw *q = arg;
-	size_t k;
-	for (k = k0; k < k1; k++) {
-		const size_t lo = rxw_lo(q, k), hi = rxw_lo(q, k + 1);
-		struct rx_walk x = q->st0;
-		if (k) {
-			x.roc = 0;
-			x.set = 0;
-			x.s_l = 0;
-			q->bad[k] = rxw_walk(q, &x, lo > RXW_WARM ? lo - RXW_WARM : 0,
-					     lo, 0);
-			x.roc = 0;      /* relative from here */
-			q->guess[k] = x;
-		}
-		q->bad[k] |= rxw_walk(q, &x, lo, hi, 1);
-		q->end[k] = x;
-	}
-}
-
-static void rxw_fix(void *arg, size_t k0, size_t k1)
-{
-	struct rxw *q = arg;
-	size_t k, i;
-	for (k = k0; k < k1; k++) {
-		const uint64_t add = (uint64_t)q->base[k] << 16;
-		if (!add)
-			continue;
-		for (i = rxw_lo(q, k); i < rxw_lo(q, k + 1); i++)
-			if (q->rec[i].stage == SRTP_RX_IX)
-				q->rec[i].ix += add;
-	}
-}
-
-static int rx_walk_packed(const struct srtp_stream_state *st0,
-			  const uint32_t *pk, const int32_t *rh, size_t n,
-			  struct srtp_rx_rec *rec)
-{
-	struct rxw *q;
-	struct rx_walk x;
-	size_t k;
-	int fix = 0;
-
-	x.ssrc = st0->ssrc;
-	x.roc = st0->roc;
-	x.s_l = st0->s_l;
-	x.set = st0->s_l_set;
-	if (n < 65536 || g_env.rxseq ||
-	    (uint64_t)st0->roc + n + 2 >= 0x7fffffffull) {
-		struct rxw one = {.pk = pk, .rh = rh, .rec = rec, .n = n};
-		return rxw_walk(&one, &x, 0, n, 1) ? EINVAL : 0;
-	}
-	q = fi_calloc(1, sizeof(*q));
-	if (!q)
-		return ENOMEM;
-	q->pk = pk;
-	q->rh = rh;
-	q->rec = rec;
-	q->n = n;
-	q->st0 = x;
-	par_for(RXW_PARTS, 1, rxw_part, q);
-	for (k = 0; k < RXW_PARTS; k++)
-		if (q->bad[k]) {
-			free(q);
-			return EINVAL;
-		}
-	for (k = 1; k < RXW_PARTS; k++) {
-		struct rx_walk t = q->end[k - 1];       /* the true start */
-		if (t.set != q->guess[k].set ||
-		    (t.set && t.s_l != q->guess[k].s_l)) {
-			/* a wrong guess: this part again, exactly */
-			count(&g_cnt_rxw_redo, 1);
-			(void)rxw_walk(q, &t, rxw_lo(q, k), rxw_lo(q, k + 1), 1);
-			q->end[k] = t;
-			continue;
-		}
-		q->base[k] = t.roc;
-		fix |= t.roc != 0;
-		q->end[k].roc += t.roc;
-	}
-	if (fix)
-		par_for(RXW_PARTS, 1, rxw_fix, q);
-	free(q);
-	return 0;
-}
-
-int srtp_rx_index_dev(const struct srtp_stream_state *st0,
-		      const uint8_t *arena, size_t arena_size,
-		      const uint32_t *pos, const uint32_t *end,
-		      const int32_t *res, size_t n, struct srtp_rx_rec *rec,
-		      void *stream)
-{
-	const uint32_t *pk;
-	const int32_t *rh = NULL;
-	struct ws *w;
-	size_t i;
-	int err, wide = 0;
-
-	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)) ||
-	    n > UINT32_MAX)
-		return EINVAL;
-	if (!n)
-		return 0;
-	if (!gpu_ready())
-		return ENOSYS;
-	w = ws_get();
-	if (!w)
-		return ENOMEM;
-	/* the headers parsed where the packets lie (k_parse: rtp_hdr_decode,
-	 * rtp.c:88-137) and packed with the results, 4 B per packet down:
-	 * the arena stays on the device */
-	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
-	if (!err)
-		err = pool_reserve(w, &w->es, n * 4);
-	if (!err)
-		err = sgpu_parse_headers(arena, arena_size, pos, end,
-					 (struct sgpu_hdr *)w->hd.d, NULL,
-					 (uint32_t)n, 0, stream);
-	if (!err)
-		err = sgpu_rx_pack((const struct sgpu_hdr *)w->hd.d, res,
-				   st0->ssrc, (uint32_t *)w->es.d, (uint32_t)n,
-				   stream);
-	if (!err)
-		err = sgpu_memcpy_d2h(w->es.h, w->es.d, n * 4, stream);
-	if (!err)
-		err = sgpu_stream_sync(stream);
-	if (err)
-		return err;
-	pk = (const uint32_t *)w->es.h;
-	for (i = 0; i < n; i++)
-		wide |= (pk[i] >> 23) & 1;
-	if (wide) {
-		/* a result outside 0..255 (not an errno): all of them */
-		err = pool_reserve(w, &w->hd, n * 4);
-		if (!err)
-			err = sgpu_memcpy_d2h(w->hd.h, res, n * 4, stream);
-		if (!err)
-			err = sgpu_stream_sync(stream);
-		if (err)
-			return err;
-		rh = (const int32_t *)w->hd.h;
-	}
-	return rx_walk_packed(st0, pk, rh, n, rec);
-}
-
-/*
- * The fold's walk (the reference receiver from the true state, srtp.c
- * :310-321 index step, :355-368 / :413-429 replay verdicts; the rank's
- * verdict void where the index or the replay verdict differs) over
- * records [lo, hi) from *x.  Returns the first void position (hi: none);
- * the state is then the one before it.  RXF_REL: the ROC is relative to
- * an unknown base -- instead of comparing indices, rec.ix - ix must be
- * one constant *D over the part (a different one is a void); *vmin is
- * the least ROC value get_index used.  RXF_WARM: state only (a guess of
- * a part's start), no verdicts, nothing stops it.
- */
-enum { RXF_EXACT, RXF_REL, RXF_WARM, RXF_PARTS = 16, RXF_WARMN = 512,
-       RXF_R0 = 2 };
-
-struct rxf_state {
-	struct replay rp;
-	uint32_t roc;
-	uint16_t s_l;
-	uint8_t set;
-};
-
-static size_t rxf_walk(struct rxf_state *x, const struct srtp_rx_rec *rec,
-		       int32_t *err, size_t lo, size_t hi, int mode,
-		       uint64_t *D, int *hasD, int64_t *vmin)
-{
-	size_t i;
-	for (i = lo; i < hi; i++) {
-		const struct srtp_rx_rec *r = &rec[i];
-		const uint32_t roc0 = x->roc;
-		const uint16_t s_l0 = x->s_l;
-		const uint8_t set0 = x->set;
-		uint64_t ix;
-		int diff;
-
-		if (r->stage == SRTP_RX_NOHDR) {
-			if (err)
-				err[i] = r->res;
-			continue;
-		}
-		if (!x->set) {
-			x->s_l = r->seq;
-			x->set = 1;
-		}
-		diff = (int)r->seq - (int)x->s_l;
-		if (diff > 32768) {
-			if (err)
-				err[i] = ETIMEDOUT;
-			continue;
-		}
-		if (r->stage != SRTP_RX_IX)
-			goto void_verdict;
-		if (diff <= -32768) {
-			x->roc++;
-			x->s_l = 0;
-		}
-		ix = get_index(x->roc, x->s_l, r->seq);
-		if (mode == RXF_EXACT) {
-			if (ix != r->ix)
-				goto void_verdict;
-		}
-		else if (mode == RXF_REL) {
-			const int64_t v = (int64_t)x->roc - 1;
-			if (v < *vmin)
-				*vmin = v;
-			if (!*hasD) {
-				*D = r->ix - ix;
-				*hasD = 1;
-			}
-			else if (r->ix - ix != *D) {
-				goto void_verdict;
-			}
-		}
-		if (r->res != 0 && r->res != EALREADY) {
-			if (err)
-				err[i] = r->res;        /* tag verdict: ROC bump stays */
-			continue;
-		}
-		/* a replay verdict the fold changes voids the packet's side
-		 * effects as well: HMAC suites return EALREADY before the
-		 * decrypt with pos at the payload (srtp.c:355-368), GCM leaves
-		 * pos there (:413-422), success restores it (:429).  Check
-		 * the window on a copy so the state stays the one before it */
-		{
-			struct replay tmp = x->rp;
-			const int ok = replay_check(&tmp, ix);
-			if (ok != (r->res == 0))
-				goto void_verdict;
-			x->rp = tmp;
-			if (!ok) {
-				if (err)
-					err[i] = EALREADY;
-				continue;
-			}
-		}
-		if (err)
-			err[i] = 0;
-		if (r->seq > x->s_l)
-			x->s_l = r->seq;
-		continue;
-	void_verdict:
-		x->roc = roc0;
-		x->s_l = s_l0;
-		x->set = set0;
-		if (mode != RXF_WARM)
-			return i;
-	}
-	return hi;
-}
-
-/*
- * The fold in parallel parts, as rx_walk_packed: part k > 0 guesses its
- * start state by a cold walk over the RXF_WARMN records before it (the
- * 64-packet window and s_l are re-established by a few hundred packets)
- * and folds with a relative ROC (RXF_R0: its indices never go below 0);
- * then, in order, each part's guess, index offset and lowest ROC are
- * checked against the previous part's true end state -- a right guess
- * makes its verdicts, its void position and its end state (shifted by
- * the ROC base) exact, because the window compares indices only by
- * difference while none wraps; a wrong one is folded again exactly.
- */
-struct rxf {
-	const struct srtp_rx_rec *rec;
-	int32_t *err;
-	size_t n;
-	struct rxf_state st0;
-	struct rxf_state guess[RXF_PARTS], end[RXF_PARTS];
-	size_t stop[RXF_PARTS];
-	uint64_t D[RXF_PARTS];
-	int hasD[RXF_PARTS];
-	int64_t vmin[RXF_PARTS];
-};
-
-static size_t rxf_lo(const struct rxf *q, size_t k)
-{
-	return q->n * k / RXF_PARTS;
-}
-
-static void rxf_part(void *arg, size_t k0, size_t k1)
-{
-	struct rxf *q = arg;
-	size_t k;
-	for (k = k0; k < k1; k++) {
-		const size_t lo = rxf_lo(q, k), hi = rxf_lo(q, k + 1);
-		struct rxf_state x = q->st0;
-		if (!k) {
-			q->stop[k] = rxf_walk(&x, q->rec, q->err, lo, hi,
-					      RXF_EXACT, NULL, NULL, NULL);
-			q->end[k] = x;
-			continue;
-		}
-		memset(&x, 0, sizeof(x));
-		x.roc = RXF_R0;
-		(void)rxf_walk(&x, q->rec, NULL,
-			       lo > RXF_WARMN ? lo - RXF_WARMN : 0, lo, RXF_WARM,
-			       NULL, NULL, NULL);
-		/* the part's relative ROC starts at RXF_R0 again */
-		x.rp.lix -= (uint64_t)(x.roc - RXF_R0) << 16;
-		x.roc = RXF_R0;
-		q->guess[k] = x;
-		q->vmin[k] = INT64_MAX;
-		q->stop[k] = rxf_walk(&x, q->rec, q->err, lo, hi, RXF_REL,
-				      &q->D[k], &q->hasD[k], &q->vmin[k]);
-		q->end[k] = x;
-	}
-}
-
-static int rxf_parallel(struct rxf_state *st, const struct srtp_rx_rec *rec,
-			size_t n, int32_t *err, size_t *ndone)
-{
-	struct rxf *q = fi_calloc(1, sizeof(*q));
-	size_t k;
-	if (!q)
-		return ENOMEM;
-	q->rec = rec;
-	q->err = err;
-	q->n = n;
-	q->st0 = *st;
-	par_for(RXF_PARTS, 1, rxf_part, q);
-	for (k = 0; k < RXF_PARTS; k++) {
-		const size_t lo = rxf_lo(q, k), hi = rxf_lo(q, k + 1);
-		if (k) {
-			const struct rxf_state t = q->end[k - 1];
-			const struct rxf_state *g = &q->guess[k];
-			const int64_t base = (int64_t)t.roc - RXF_R0;
-			const uint64_t B = (uint64_t)base << 16;
-			const int right = t.set == g->set &&
-				(!t.set || t.s_l == g->s_l) &&
-				t.rp.bitmap == g->rp.bitmap &&
-				t.rp.lix == g->rp.lix + B &&
-				g->rp.lix < (1ull << 62) &&
-				t.rp.lix < (1ull << 62) &&
-				(!q->hasD[k] || q->D[k] == B) &&
-				q->vmin[k] + base >= 0;
-			if (right) {
-				q->end[k].roc += (uint32_t)base;
-				q->end[k].rp.lix += B;
-			}
-			else {
-				struct rxf_state x = t;
-				count(&g_cnt_rxw_redo, 1);
-				q->stop[k] = rxf_walk(&x, rec, err, lo, hi,
-						      RXF_EXACT, NULL, NULL, NULL);
-				q->end[k] = x;
-			}
-		}
-		if (q->stop[k] < hi) {
-			*st = q->end[k];
-			*ndone = q->stop[k];
-			free(q);
-			return 0;
-		}
-	}
-	*st = q->end[RXF_PARTS - 1];
-	*ndone = n;
-	free(q);
-	return 0;
-}
-
-int srtp_rx_fold(struct srtp_stream_state *st, enum srtp_suite suite,
-		 const struct srtp_rx_rec *rec, size_t n, int32_t *err,
-		 size_t *ndone)
-{
-	struct rxf_state x;
-	int e = 0;
-
-	/* every suite checks the replay window after its tag (srtp.c:362-368
-	 * HMAC, 414-421 GCM), so suite is only validated */
-	if (!st || !ndone || (n && (!rec || !err)) ||
-	    (unsigned)suite > SRTP_AES_256_GCM)
-		return EINVAL;
-	x.rp.bitmap = st->replay_rtp_bitmap;
-	x.rp.lix = st->replay_rtp_lix;
-	x.roc = st->roc;
-	x.s_l = st->s_l;
-	x.set = st->s_l_set;
-	if (n >= 65536 && !g_env.rxseq &&
-	    (uint64_t)st->roc + n + RXF_R0 + 2 < 0x7fffffffull &&
-	    st->replay_rtp_lix < (1ull << 62))
-		e = rxf_parallel(&x, rec, n, err, ndone);
-	else
-		*ndone = rxf_walk(&x, rec, err, 0, n, RXF_EXACT, NULL, NULL,
-				  NULL);
-	if (e)
-		return e;
-	st->replay_rtp_bitmap = x.rp.bitmap;
-	st->replay_rtp_lix = x.rp.lix;
-	st->roc = x.roc;
-	st->s_l = x.s_l;
-	st->s_l_set = x.set;
 	return 0;
 }
 

@@ -1,5 +1,5 @@
 """srtp_rx_index's receiver walk runs in parallel parts on long streams
-(re_amd/csrc/host/srtp.c rx_walk_packed: each part guesses its start
+(re_amd/csrc/host/rxfold.c rx_walk_packed: each part guesses its start
 state from a cold walk over the packets before it, the guesses are checked
 in order against the previous part's true end state, a wrong one is walked
 again, a right one gets its ROC base added).  The records must be those of

@@ -279,6 +279,12 @@ def main():
                          "asynchronous srtp_*_batch_dev_async + "
                          "srtp_batch_wait pair (protect and unprotect "
                          "queued back to back on the stream)")
+    ap.add_argument("--async", dest="async_", action="store_true",
+                    help="the asynchronous pair with two steps in flight "
+                         "for every config (default: for multi-session "
+                         "configs and sharded runs; one-session configs on "
+                         "one GPU default to the synchronous calls, 1.5-2 "
+                         "%% faster there: profiles/r04_sync_async_ab.txt)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="asynchronous pairs: wait for each step before "
                          "issuing the next (default: two steps in flight)")
@@ -458,7 +464,14 @@ def main():
     # the packets; --host-arrays: srtp_*_batch with host windows.
     use_dev = not args.host_arrays
     # asynchronous pair (srtp_*_batch_dev_async) for the RTP device path
-    use_async = use_dev and not args.sync and not args.e2e and not args.rtcp
+    # one session: the synchronous pair measured faster (the crypto
+    # kernel itself: config 3 unprotect 1.570 vs 1.617 ms); many sessions:
+    # the pipelined asynchronous pair (its host planning overlaps the
+    # previous step on the GPU: config 4 292-295 vs 217-269 GiB/s)
+    # (sharded runs keep the pipelined pair: on the shared-GPU rehearsal the
+    # synchronous one lost 9 %)
+    sync = args.sync or (nsess == 1 and world == 1 and not args.async_)
+    use_async = use_dev and not sync and not args.e2e and not args.rtcp
     pipelined = use_async and not args.no_pipeline
     sess_d = None
     if use_dev:
@@ -468,10 +481,16 @@ def main():
         if sess is not None:
             sess_d = i32(sess)
         p_d, e_d = torch.empty_like(pos_d), torch.empty_like(end_d)
-        # two steps in flight: each in-flight call keeps its own windows
-        # until it is waited for (re_srtp_batch.h: the device arrays of an
-        # asynchronous call stay untouched by other calls until then)
-        win2 = [(p_d, e_d), (torch.empty_like(pos_d), torch.empty_like(end_d))]
+        # every step its own input windows (the API moves pos/end in place;
+        # an asynchronous call keeps its arrays until it is waited for,
+        # re_srtp_batch.h), written before the timed region like the arena
+        nwin = max(1, args.steps, args.warmup)
+        winp = pos_d.repeat(nwin, 1)
+        wine = end_d.repeat(nwin, 1)
+
+        def reset_windows():
+            winp.copy_(pos_d.expand(nwin, -1))
+            wine.copy_(end_d.expand(nwin, -1))
         # per-step result arrays: the API fills them inside the timed
         # region; the bench tallies them after it (verification, not path)
         errbuf = torch.zeros((2, max(1, args.steps, args.warmup), n), dtype=torch.int32,
@@ -538,9 +557,7 @@ def main():
             e2e_pass(OPS[1], rx, err_dd)
             return 0
         if use_dev:
-            pw, ew = win2[k & 1] if inflight is not None else (p_d, e_d)
-            pw.copy_(pos_d)
-            ew.copy_(end_d)
+            pw, ew = winp[k], wine[k]
             pend = []
             for opname, ss, er in ((OPS[0], tx, err_ed),
                                    (OPS[1], rx, err_dd)):
@@ -608,6 +625,8 @@ def main():
     # the library's per-call workspaces exist before timing) ----
     if args.warmup:
         warm = [make_sessions() for _ in range(args.warmup)]
+        if use_dev:
+            reset_windows()
         run_steps([(P.session_array(tx), P.session_array(rx))
                    for tx, rx in warm])
         torch.cuda.synchronize()
@@ -625,6 +644,7 @@ def main():
     P.prof_read()
     if use_dev:
         errbuf.fill_(-1)        # every call must write every result
+        reset_windows()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

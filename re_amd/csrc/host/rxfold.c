@@ -56,31 +56,50 @@ static int rx_walk_packed(const struct srtp_stream_state *st0,
 			  const uint32_t *pk, const int32_t *rh, size_t n,
 			  struct srtp_rx_rec *rec);
 
+/* srtp_rx_index: packets [lo, hi) parsed into the packed words of
+ * k_rx_pack (seq | ok << 16 | other SSRC << 17) */
+struct rxp {
+	const struct srtp_stream_state *st0;
+	const uint8_t *arena;
+	const uint32_t *pos, *end;
+	uint32_t *pk;
+};
+
+static void rxp_part(void *arg, size_t lo, size_t hi)
+{
+	const struct rxp *q = arg;
+	size_t i;
+	for (i = lo; i < hi; i++) {
+		struct pinfo pi;
+		memset(&pi, 0, sizeof(pi));
+		pi.start = q->pos[i];
+		pi.end = q->end[i];
+		parse_rtp(&pi, q->arena);
+		q->pk[i] = pi.hdr_len == UINT32_MAX ? 0u :
+			   (uint32_t)pi.seq | 1u << 16 |
+			   (pi.ssrc != q->st0->ssrc ? 1u << 17 : 0u);
+	}
+}
+
 int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
 		  const uint32_t *pos, const uint32_t *end,
 		  const int32_t *res, size_t n, struct srtp_rx_rec *rec)
 {
 	uint32_t *pk;
-	size_t i;
 	int err;
 
 	if (!st0 || (n && (!arena || !pos || !end || !res || !rec)))
 		return EINVAL;
 	if (!n)
 		return 0;
-	/* the headers parsed here, then the walk of srtp_rx_index_dev */
+	/* the headers parsed here (in parts: one cold line per packet of
+	 * the arena), then the walk of srtp_rx_index_dev */
 	pk = fi_malloc(n * sizeof(*pk));
 	if (!pk)
 		return ENOMEM;
-	for (i = 0; i < n; i++) {
-		struct pinfo pi;
-		memset(&pi, 0, sizeof(pi));
-		pi.start = pos[i];
-		pi.end = end[i];
-		parse_rtp(&pi, arena);
-		pk[i] = pi.hdr_len == UINT32_MAX ? 0u :
-			(uint32_t)pi.seq | 1u << 16 |
-			(pi.ssrc != st0->ssrc ? 1u << 17 : 0u);
+	{
+		struct rxp q = {st0, arena, pos, end, pk};
+		par_for(n, 16384, rxp_part, &q);
 	}
 	err = rx_walk_packed(st0, pk, res, n, rec);
 	free(pk);

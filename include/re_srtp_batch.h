@@ -240,7 +240,11 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * word), "pcrunners" (per-packet runners at once, 1-4, default 4),
  * "pcspin" (pause loops a waiting per-packet caller spins before it
  * sleeps, default 1000), "rxseq" (srtp_rx_index* and srtp_rx_fold walk
- * in one sequential pass, not in parallel parts), "trace", "times" (phase
+ * in one sequential pass, not in parallel parts), "freshmulti" (the
+ * planner's first-batch hint: 1 sends a session's first batch to the
+ * per-stream planner, 0 to the one-stream plan; the library sets it when a
+ * first batch showed several SSRCs and clears it when one showed one),
+ * "trace", "times" (phase
  * timings on stderr), "chunk" (host-scan chunk, packets), "par_min"
  * (sessions per host-pool part); value 0 turns a switch off and restores
  * a size's built-in default.  Results never depend on them.  0 or EINVAL.
@@ -256,7 +260,8 @@ int srtp_gpu_tune(const char *name, long value);
  * "pcbatches" / "pcpackets" (shared launches of per-packet calls and the
  * packets they carried), "pcfused" (those of them that ran several
  * operations as one launch), "gated" (asynchronous calls queued behind one
- * the host completed, re-run when waited for).  0 for an unknown name.
+ * the host completed, re-run when waited for), "freshmulti" (the
+ * first-batch hint, 0/1).  0 for an unknown name.
  */
 uint64_t srtp_gpu_counter(const char *name);
 

@@ -115,6 +115,13 @@ static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
+/* a session's first batch (no stream yet) goes to the per-stream planner
+ * while the last first batch planned showed several SSRCs: a one-stream
+ * plan for it is rejected at completion and the batch planned again, a
+ * second parse, plan and launch behind a host synchronisation.  Set by
+ * that rejection, cleared by a first batch of one SSRC (the per-stream
+ * plan is right for either, the one-stream plan only for one). */
+static int g_fresh_multi;
 uint64_t g_cnt_pcbatch;  /* shared launches of per-packet calls */
 uint64_t g_cnt_pcpkts;   /* ... and the packets they carried */
 uint64_t g_cnt_rxw_redo; /* srtp_rx_index*: parts walked again */
@@ -176,6 +183,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_ns_fused_post, __ATOMIC_RELAXED);
 	if (!strcmp(name, "mbufs_ns"))
 		return __atomic_load_n(&g_ns_mbufs, __ATOMIC_RELAXED);
+	if (!strcmp(name, "freshmulti"))
+		return (uint64_t)__atomic_load_n(&g_fresh_multi, __ATOMIC_RELAXED);
 	if (!strcmp(name, "prof_voided"))
 		return sgpu_prof_voided();
 	if (!strcmp(name, "fail_alloc"))
@@ -221,6 +230,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.smallsync = value > 0;
 	else if (!strcmp(name, "rxseq"))
 		g_env.rxseq = value > 0;
+	else if (!strcmp(name, "freshmulti"))
+		__atomic_store_n(&g_fresh_multi, value > 0, __ATOMIC_RELAXED);
 	else if (!strcmp(name, "pcrunners"))
 		g_env.pcrunners = value > 0 ? value : 0;
 	else if (!strcmp(name, "pcspin"))
@@ -3413,6 +3424,8 @@ static int dev_planned_finish(struct dcall *k)
 	if (po->fail) {
 		if (po->fail & SPF_PRED)
 			return -2;
+		if ((po->fail & SPF_SSRC) && !ns0)
+			__atomic_store_n(&g_fresh_multi, 1, __ATOMIC_RELAXED);
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
@@ -3640,6 +3653,8 @@ static int dev_splanned_finish(struct dcall *k)
 		return -1;
 	}
 	count(&g_cnt_splans, 1);
+	if (!s->nstreams && po->nst <= 1)
+		__atomic_store_n(&g_fresh_multi, 0, __ATOMIC_RELAXED);
 	if (!nfail) {
 		splan_apply(s, po, prot);
 		return 0;
@@ -4318,7 +4333,9 @@ static int batch_async(int op, struct srtp **sessv, size_t nsess,
 		table_unlock();
 		if (err)
 			kind = 0;
-		else if (s->nstreams > 1 || g_env.splan)
+		else if (s->nstreams > 1 || g_env.splan ||
+			 (!s->nstreams &&
+			  __atomic_load_n(&g_fresh_multi, __ATOMIC_RELAXED)))
 			kind = TK_SPLANNED;
 	}
 	if (!kind) {
@@ -4508,7 +4525,9 @@ static int run_dev(int op, struct srtp **sessv, size_t nsess,
 		 * the per-stream planner */
 		uint32_t pf = SPF_SSRC;
 		int r = -1;
-		if (sessv[0]->nstreams <= 1 && !g_env.splan)
+		if (sessv[0]->nstreams <= 1 && !g_env.splan &&
+		    (sessv[0]->nstreams ||
+		     !__atomic_load_n(&g_fresh_multi, __ATOMIC_RELAXED)))
 			r = dev_planned(op, sessv[0], d, &pf);
 		if (r == -1 && (pf & SPF_SSRC))
 			r = dev_splanned(op, sessv[0], d);

@@ -17,3 +17,16 @@ def pytest_configure(config):
 def golden():
     from tests.golden_util import load_golden
     return load_golden()
+
+
+@pytest.fixture(autouse=True)
+def _fresh_planner_hint(request):
+    """every GPU test starts with the planner's first-batch hint cleared
+    (srtp_gpu_tune "freshmulti"): a test that plans fresh multi-SSRC
+    sessions must not change which planner the next test's first batch
+    takes"""
+    if request.node.get_closest_marker("gpu"):
+        S = sys.modules.get("re_amd.srtp")
+        if S is not None:
+            S.lib().srtp_gpu_tune(b"freshmulti", 0)
+    yield

@@ -171,6 +171,38 @@ def test_streams_forced_single_stream(suite, torch_cuda):
     same(A, B, "forced splan vs single-stream plan")
 
 
+def test_fresh_sessions_learn_the_per_stream_planner(torch_cuda):
+    """a session's first batch (no stream yet) with several SSRCs: the
+    one-stream plan is rejected once (g_fresh_multi set), later fresh
+    sessions go to the per-stream planner directly (no reject, same bytes
+    and states as the general engine); a fresh one-SSRC session clears the
+    hint again"""
+    torch = torch_cuda
+    rng = np.random.default_rng(808)
+    key = keys_for(1, 1)[0]
+    b2, _ = interleaved(rng, rng.integers(0, 2, 3000), {0: 65300, 1: 900})
+    b1, _ = interleaved(rng, np.zeros(3000, dtype=int), {0: 65300})
+    ss2, ss1 = [SSRC0, SSRC0 + 1], [SSRC0]
+    assert P.counter("freshmulti") == 0
+    r0, s0 = P.counter("rejects"), P.counter("splans")
+    A = run_mode(torch, "plan", 1, key, [b2], ss2)
+    assert P.counter("rejects") - r0 == 1          # tx: rejected once
+    assert P.counter("splans") - s0 == 2
+    assert P.counter("freshmulti") == 1
+    r1 = P.counter("rejects")
+    B = run_mode(torch, "plan", 1, key, [b2], ss2)
+    assert P.counter("rejects") == r1              # planned directly
+    G = run_mode(torch, "general", 1, key, [b2], ss2)
+    same(A, G, "first fresh session vs general")
+    same(B, G, "hinted fresh session vs general")
+    C = run_mode(torch, "plan", 1, key, [b1], ss1)
+    assert P.counter("freshmulti") == 0
+    D = run_mode(torch, "plan", 1, key, [b1], ss1)
+    same(C, D, "one SSRC: per-stream vs single-stream plan")
+    for r in A[0] + B[0] + C[0]:
+        assert (r[3] == 0).all()
+
+
 @pytest.mark.parametrize("suite", [1, 4])
 @pytest.mark.parametrize("case", ["reorder", "replay", "ninth", "forged",
                                   "timeout"])

@@ -156,9 +156,10 @@ def test_tune_knobs_and_counters():
     (no GPU needed: neither touches the device)"""
     L = P.load()
     for k in ("noplan", "general", "perclass", "nolean", "nodevfold",
-              "splan", "nomk", "trace", "times"):
+              "splan", "nomk", "freshmulti", "trace", "times"):
         assert L.srtp_gpu_tune(k.encode(), 1) == 0, k
         assert L.srtp_gpu_tune(k.encode(), 0) == 0, k
     assert L.srtp_gpu_tune(b"no-such-knob", 1) != 0
-    for c in ("misses", "folds", "rejects", "devfolds", "splans"):
+    for c in ("misses", "folds", "rejects", "devfolds", "splans",
+              "freshmulti"):
         assert P.counter(c) >= 0, c

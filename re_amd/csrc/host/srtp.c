@@ -4002,11 +4002,31 @@ static int dev_mplanned_issue(struct dcall *k)
 		return err ? err : -1;
 	}
 	k->t[1] = times ? now_ms() : 0;
-	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, stream);
+	/* the slot map and the states the device lacks (64K fresh sessions:
+	 * 2 MB) go up on the workspace's own stream, so the copy overlaps
+	 * the kernels queued before it on the call's stream (the sort above,
+	 * or the previous call's crypto launch) instead of following them;
+	 * the call's stream waits for it before k_sst_load.  Nothing queued
+	 * before reads cm or the uploads, and the workspace is not reused
+	 * before the call completes. */
+	if (!w->upev)
+		w->upev = sgpu_event_create();
+	if (!w->upev)
+		return ENOMEM;
+	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->stream);
 	if (!err && k->nup)
 		err = sgpu_memcpy_h2d(up_d, up_h,
 				      nsess * (sizeof(struct sgpu_sstate) + 1),
-				      stream);
+				      w->stream);
+	if (!err)
+		err = sgpu_event_record(w->upev, w->stream);
+	if (!err)
+		err = sgpu_stream_wait(stream, w->upev);
+	if (err) {
+		/* no copy may still read the host buffers */
+		sgpu_stream_sync(w->stream);
+		return err;
+	}
 	if (!err)
 		err = sgpu_sst_load((const uint32_t *)w->cm.d,
 				    k->nup ? need_d : NULL, up_d,

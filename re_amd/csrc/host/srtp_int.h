@@ -192,6 +192,8 @@ struct ws {
 	struct pool ms;         /* multi-session plan: states in | out */
 	struct pool mscr;       /* multi-session plan: device scratch */
 	void **ev;              /* per-chunk parse events */
+	void *upev;             /* multi-session plan: its state uploads done
+				   (on the side stream w->stream) */
 	size_t nev;
 	struct ulogv ulog[1];   /* stream-state undo log */
 	/* the small kernel's completion word (small_wait) */

@@ -190,8 +190,10 @@ int srtp_rx_index(const struct srtp_stream_state *st0, const uint8_t *arena,
 /**
  * The same for a rank whose arena, windows and results (the
  * srtp_decrypt_batch_dev outputs) are DEVICE memory: the headers are
- * parsed on the device and 16 bytes per packet come down, the arena does
- * not; rec is host memory.  Queued on stream (hipStream_t, NULL: default)
+ * parsed on the device, which packs seq, header verdict and result into
+ * one 4-byte word per packet; those words come down (plus the 4-byte
+ * results of a batch whose results fall outside 0..255, a second copy),
+ * the arena does not; rec is host memory.  Queued on stream (hipStream_t, NULL: default)
  * and synchronised.  0 or EINVAL / ENOMEM / EIO / ENOSYS.
  */
 int srtp_rx_index_dev(const struct srtp_stream_state *st0,

@@ -27,6 +27,11 @@
  *  10  config 4 (64K sessions, mixed lengths) with the same forgeries
  *
  *   ref_digest <config> [npkts]
+ *
+ * `ref_digest shards 8 1048576` (shards() below) pins config 5 whole: the
+ * 8M-packet stream cut into the 8 ranks' shards, per-shard digests and the
+ * reference's stream states at every boundary
+ * (tests/golden/config5_shards.json).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -188,9 +193,136 @@ static void emit(const char *name, const uint8_t *arena, size_t n,
 	printf("}");
 }
 
+/* one stream state of the reference, as srtp_stream_import takes it */
+static void emit_state(const char *name, struct srtp *ctx)
+{
+	struct le *le;
+	const struct srtp_stream *st = NULL;
+	for (le = ctx->streaml.head; le; le = le->next)
+		if (((struct srtp_stream *)le->data)->ssrc == SSRC_BASE)
+			st = le->data;
+	printf("\"%s\":", name);
+	if (!st) {
+		printf("null");
+		return;
+	}
+	printf("{\"roc\":%u,\"s_l\":%u,\"s_l_set\":%d,\"lix\":%llu,"
+	       "\"bitmap\":%llu}", st->roc, (unsigned)st->s_l, st->s_l_set ? 1 : 0,
+	       (unsigned long long)st->replay_rtp.lix,
+	       (unsigned long long)st->replay_rtp.bitmap);
+}
+
+/*
+ * BASELINE config 5 whole: one stream of world x per packets (seq from
+ * 65000, 1200 B, AES_CM_128_HMAC_SHA1_80), cut into `world` contiguous
+ * shards of `per` packets as bench.py --gpus N cuts it.  One reference
+ * sender and one receiver run over the whole stream in order (shard by
+ * shard: the sender's and the receiver's sequences are each the sequential
+ * reference's; only one shard's arena is held at a time).  Per shard: the
+ * sender's and receiver's stream states at its start (what rank r must
+ * import), and the arena / end / errno digests and final states after its
+ * protect and its unprotect, with the arena laid out as rank r holds it
+ * (workload.make_arena(per, 1200, s0=shard_seq0(r), first=r*per)).
+ *
+ *   ref_digest shards <world> <per>
+ */
+static int shards(size_t world, size_t per)
+{
+	const size_t length = 1200, slot = (length + 16 + 15) & ~(size_t)15;
+	const unsigned s0 = 65000;
+	const size_t klen = keylen[1] + saltlen[1];
+	uint8_t key[64], *arena = calloc(per, slot);
+	uint32_t *pos = calloc(per, 4), *end = calloc(per, 4);
+	int32_t *err = calloc(per, 4);
+	struct srtp *tx, *rx;
+	size_t r, i;
+
+	if (!arena || !pos || !end || !err) {
+		fprintf(stderr, "out of memory\n");
+		return 1;
+	}
+	xs_fill(key, klen, SEED_KEYS, 0);
+	if (srtp_alloc(&tx, 1, key, klen, 0) || srtp_alloc(&rx, 1, key, klen, 0)) {
+		fprintf(stderr, "srtp_alloc failed\n");
+		return 1;
+	}
+	printf("{\"generator\":\"oracle/ref_digest.c shards (reference src/srtp"
+	       " + OpenSSL)\",\"config\":5,\"suite\":1,\"world\":%zu,\"per\":%zu,"
+	       "\"s0\":%u,\"length\":%zu,\"slot\":%zu,\"shards\":[",
+	       world, per, s0, length, slot);
+	for (r = 0; r < world; r++) {
+		const uint64_t first = (uint64_t)r * per;
+		for (i = 0; i < per; i++) {
+			const uint64_t g = first + i;
+			uint8_t *p = arena + i * slot;
+			const uint32_t ts = (uint32_t)(160u * g);
+			const uint16_t seq = (uint16_t)(s0 + g);
+			memset(p, 0, slot);
+			p[0] = 0x80;
+			p[2] = (uint8_t)(seq >> 8);
+			p[3] = (uint8_t)seq;
+			p[4] = (uint8_t)(ts >> 24); p[5] = (uint8_t)(ts >> 16);
+			p[6] = (uint8_t)(ts >> 8);  p[7] = (uint8_t)ts;
+			p[8] = (uint8_t)(SSRC_BASE >> 24);
+			p[9] = (uint8_t)(SSRC_BASE >> 16);
+			p[10] = (uint8_t)(SSRC_BASE >> 8);
+			p[11] = (uint8_t)SSRC_BASE;
+			xs_fill(p + 12, length - 12, SEED_PAYLOAD, g);
+			pos[i] = (uint32_t)(i * slot);
+			end[i] = pos[i] + (uint32_t)length;
+		}
+		printf("%s{\"rank\":%zu,\"first\":%llu,\"seq0\":%u,", r ? "," : "",
+		       r, (unsigned long long)first, (unsigned)(uint16_t)(s0 + first));
+		emit_state("tx_in", tx);
+		putchar(',');
+		emit_state("rx_in", rx);
+		printf(",\"plain\":");
+		sha(arena, per * slot);
+		for (int dir = 0; dir < 2; dir++) {
+			size_t nerr = 0;
+			for (i = 0; i < per; i++) {
+				struct mbuf mb;
+				mb.buf = arena;
+				mb.size = pos[i] + slot;
+				mb.pos = pos[i];
+				mb.end = end[i];
+				err[i] = dir ? srtp_decrypt(rx, &mb)
+					     : srtp_encrypt(tx, &mb);
+				end[i] = (uint32_t)mb.end;
+				nerr += err[i] != 0;
+			}
+			printf(",\"%s\":{\"arena\":", dir ? "unprotect" : "protect");
+			sha(arena, per * slot);
+			printf(",\"end\":");
+			sha(end, per * 4);
+			printf(",\"err\":");
+			sha(err, per * 4);
+			printf(",\"nerr\":%zu,\"pkt0\":", nerr);
+			hex(arena, end[0]);
+			printf(",");
+			emit_state("state", dir ? rx : tx);
+			printf("}");
+		}
+		printf("}");
+		fflush(stdout);
+	}
+	printf("]}\n");
+	mem_deref(tx);
+	mem_deref(rx);
+	free(arena);
+	free(pos);
+	free(end);
+	free(err);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
-	int c = argc > 1 ? atoi(argv[1]) : 0;
+	int c;
+	if (argc > 1 && !strcmp(argv[1], "shards"))
+		return shards(argc > 2 ? (size_t)atol(argv[2]) : 8,
+			      argc > 3 ? (size_t)atol(argv[3]) : (size_t)1 << 20);
+	c = argc > 1 ? atoi(argv[1]) : 0;
 	struct cfg cf;
 	size_t n, slot, maxlen, i, klen, nrows;
 	uint8_t *arena, *keys, *stbuf;

@@ -689,8 +689,12 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 	static_assert(SMALL_NB * 80 * 4 >= 595 * 16, "gcm_small scratch");
 	__shared__ uint32_t s_tag_ok;
 	const uint32_t i = blockIdx.x, tid = threadIdx.x;
-	if (i >= a.njobs)
+	/* every return below runs small_done first: the last workgroup's
+	 * count is what publishes the launch's completion word */
+	if (i >= a.njobs) {
+		small_done(a);
 		return;
+	}
 	const struct sgpu_job j = a.jobs[i];
 	const bool PROT = MODE == 2 ? (j.flags & SJ_PROTECT) != 0 : MODE == 1;
 	if (j.flags & SJ_SKIP) {

@@ -169,11 +169,13 @@ static void *pc_helper(void *arg)
 {
 	struct pc_slot *sl = arg;
 	for (;;) {
-		while (__atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE) != 1)
+		/* one read gives both the check and the futex's expected
+		 * value: a post (store 1 + wake) between two reads would
+		 * otherwise leave the helper asleep on a word already 1 */
+		int v;
+		while ((v = __atomic_load_n(&sl->hstate, __ATOMIC_ACQUIRE)) != 1)
 			(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAIT_PRIVATE,
-				      __atomic_load_n(&sl->hstate,
-						      __ATOMIC_RELAXED),
-				      NULL, NULL, 0);
+				      v, NULL, NULL, 0);
 		pc_run_op(sl->hlist, sl->hop);
 		__atomic_store_n(&sl->hstate, 2, __ATOMIC_RELEASE);
 		(void)syscall(SYS_futex, &sl->hstate, FUTEX_WAKE_PRIVATE, 1,

@@ -1219,6 +1219,16 @@ struct ws *ws_get(void)
  * checking the stream for an error now and then.  Without the word (its
  * allocation failed) a plain synchronisation.
  */
+/* after a failed small launch: the workgroup count (0 between launches)
+ * may be left part-way, so it is zeroed again on the idle stream before the
+ * workspace's next launch counts on it */
+static int small_reset(struct ws *w, int err)
+{
+	if (w->sm_cnt && !sgpu_stream_sync(w->stream))
+		(void)sgpu_memset(w->sm_cnt, 0, 4, w->stream);
+	return err;
+}
+
 int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 		     const struct sgpu_job *jobs, uint32_t m, uint8_t *vh,
 		     uint32_t *sv, int prot, uint64_t *t_launch)
@@ -1248,7 +1258,7 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 				     w->sm_cnt, flag, seq, w->stream);
 		*t_launch = mono_ns() - t0;
 		if (err)
-			return err;
+			return small_reset(w, err);
 		if (!flag)
 			return sgpu_stream_sync(w->stream);
 	}
@@ -1265,7 +1275,8 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 			continue;
 		if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
 			return 0;
-		return q ? q : EIO;     /* done without its word: a fault */
+		/* done without its word: a fault */
+		return small_reset(w, q ? q : EIO);
 	}
 }
 

@@ -23,3 +23,7 @@ make -s -C oracle ref
 	echo ']}'
 } > tests/golden/fullsize_digests.json
 python -c "import json; json.load(open('tests/golden/fullsize_digests.json'))"
+# config 5 whole: 8 shards of 1M of the one 8M-packet stream, per-shard
+# digests and the reference's boundary states (~2 min)
+oracle/_ref/ref_digest shards 8 1048576 > tests/golden/config5_shards.json
+python -c "import json; json.load(open('tests/golden/config5_shards.json'))"

@@ -143,3 +143,49 @@ def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners):
     elif suites[2] == 3 and runners == 1:
         # 16 threads alternating protect and unprotect: some lists mix them
         assert fused > 0
+
+
+def test_helper_thread_handoff_stress(torch_cuda):
+    """The runners' helper threads (lists pc_run_fused rejects: nofuse=1)
+    under many short alternating calls: a post of the runner between the
+    helper's check and its futex wait once left the helper asleep on a word
+    already posted, hanging every caller queued behind the slot.
+    32 threads x 300 protect/unprotect pairs must all finish, every packet
+    back to its plaintext."""
+    T, N = 32, 300
+    done, bad = [], []
+
+    def worker(t):
+        rng = np.random.default_rng(900 + t)
+        key = bytes((7 * t + i) & 0xff for i in range(30))
+        tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+        try:
+            for k in range(N):
+                pkt = rtp_packet(rng, (1000 + k) & 0xffff, 0x500 + t,
+                                 plen=int(rng.integers(0, 200)))
+                mb = P.new_mbuf(pkt, len(pkt) + 64)
+                e1 = tx._op("srtp_encrypt", mb)
+                m = mb.contents
+                m.pos = 0
+                e2 = rx._op("srtp_decrypt", mb)
+                m = mb.contents
+                out = P.mbuf_bytes(mb, m.end)
+                P.free_mbuf(mb)
+                if e1 or e2 or out != pkt:
+                    bad.append((t, k, e1, e2))
+                    return
+            done.append(t)
+        finally:
+            tx.close()
+            rx.close()
+
+    ths = [threading.Thread(target=worker, args=(t,), daemon=True)
+           for t in range(T)]
+    with P.tune(nofuse=1, pcspin=1, pcrunners=4):
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(90)
+    assert not bad, bad[:4]
+    assert sorted(done) == list(range(T)), "threads hung: %d of %d done" % (
+        len(done), T)

@@ -136,6 +136,70 @@ def test_two_shards_equal_one_stream(torch_cuda):
     rx.close()
 
 
+def test_config5_all_eight_shards_match_reference(torch_cuda):
+    """BASELINE config 5 whole: the 8M-packet stream as the 8 ranks of
+    bench.py --gpus 8 hold it, run shard after shard on one GPU.  Rank r's
+    fresh contexts import shard_state(r) (the closed-form boundary state
+    bench.py hands each rank), protect its 1M packets, and unprotect them;
+    every shard's arena, end, errno digests and exported final states must
+    equal the reference src/srtp's over the same stream
+    (tests/golden/config5_shards.json: one reference sender and receiver over
+    all 8M packets in order, `oracle/_ref/ref_digest shards 8 1048576`)."""
+    import hashlib
+    import json
+    import os
+    import sys
+    torch = torch_cuda
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                        "config5_shards.json")
+    with open(path) as f:
+        ref = json.load(f)
+    per, s0 = ref["per"], ref["s0"]
+    assert (ref["world"], per) == (8, PER)
+    key = W.make_keys(1, W.KEY_LEN[1])[0].tobytes()
+
+    def sha(a):
+        return hashlib.sha256(memoryview(np.ascontiguousarray(a)).cast("B")
+                              ).hexdigest()
+
+    def want_state(row):
+        return (row["roc"], row["s_l"], row["s_l_set"], row["lix"],
+                row["bitmap"])
+
+    for sh in ref["shards"]:
+        r = sh["rank"]
+        arena, pos, end, cap = W.make_arena(per, 1200,
+                                            s0=S.shard_seq0(r, per, s0),
+                                            first=r * per)
+        assert sha(arena) == sh["plain"], r
+        dev = torch.from_numpy(arena).cuda()
+        del arena
+        tx, rx = P.Srtp(1, key), P.Srtp(1, key)
+        if r:
+            for c, recv in ((tx, False), (rx, True)):
+                assert c.import_(S.shard_state(r, per, s0, W.SSRC_BASE, recv,
+                                               P.StreamState)) == 0
+        for op, ctx, direction in (("srtp_encrypt", tx, "protect"),
+                                   ("srtp_decrypt", rx, "unprotect")):
+            err = run(torch, op, ctx, dev, pos, end, cap, 0, per)
+            want = sh[direction]
+            bad = []
+            if sha(dev.cpu().numpy()) != want["arena"]:
+                bad.append("arena")
+            if sha(end.astype("<u4")) != want["end"]:
+                bad.append("end")
+            if sha(err.astype("<i4")) != want["err"]:
+                bad.append(("err", int(np.count_nonzero(err))))
+            if state(ctx) != want_state(want["state"]):
+                bad.append(("state", state(ctx), want["state"]))
+            assert not bad, (r, direction, bad)
+        tx.close()
+        rx.close()
+        del dev
+        print("config 5 shard %d/8: protect + unprotect equal to the "
+              "reference" % (r + 1), file=sys.stderr, flush=True)
+
+
 def test_bench_spawns_two_gpu_ranks():
     """`bench.py --gpus 2` without a launcher runs two real ranks (here both
     on cuda:0 with gloo counters, --same-device): config 5 shards, the

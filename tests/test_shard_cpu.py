@@ -83,6 +83,50 @@ def test_shard_state_matches_sequential_model(s0, per_rank):
         check_rank(rank, per_rank, s0)
 
 
+def _config5_shards():
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                        "config5_shards.json")
+    with open(path) as f:
+        return json.load(f)
+
+
+def _ref_state(row, receiver):
+    """a reference stream state of config5_shards.json as shard_state
+    returns it (None: no stream yet, the fresh context rank 0 starts from)"""
+    if row is None:
+        return {"roc": 0, "s_l": 0, "s_l_set": 0, "replay_rtp_lix": 0,
+                "replay_rtp_bitmap": 0}
+    st = {"roc": row["roc"], "s_l": row["s_l"], "s_l_set": row["s_l_set"],
+          "replay_rtp_lix": row["lix"], "replay_rtp_bitmap": row["bitmap"]}
+    if not receiver:
+        # the sender never touches its replay window (srtp.c:183-285)
+        assert row["lix"] == 0 and row["bitmap"] == 0
+    return st
+
+
+def test_shard_state_matches_reference_every_rank():
+    """shard_state(r) for every rank of the 8 x 1M config-5 stream equals
+    the stream state the reference src/srtp itself holds at that boundary
+    (tests/golden/config5_shards.json, `oracle/_ref/ref_digest shards 8
+    1048576`), sender and receiver; rank 8 = the state after the stream"""
+    d = _config5_shards()
+    assert (d["world"], d["per"], d["s0"]) == (8, 1 << 20, 65000)
+    per, s0 = d["per"], d["s0"]
+    for sh in d["shards"]:
+        r = sh["rank"]
+        assert sh["seq0"] == S.shard_seq0(r, per, s0)
+        for key, recv in (("tx_in", False), ("rx_in", True)):
+            got = S.shard_state(r, per, s0, 0x01020304, recv)
+            got.pop("ssrc")
+            assert got == _ref_state(sh[key], recv), (r, key)
+    last = d["shards"][-1]
+    for key, recv in (("protect", False), ("unprotect", True)):
+        got = S.shard_state(d["world"], per, s0, 0x01020304, recv)
+        got.pop("ssrc")
+        assert got == _ref_state(last[key]["state"], recv), key
+
+
 def _worker(rank, world, port, per_rank, s0, q):
     try:
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" %

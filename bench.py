@@ -20,6 +20,7 @@ Packets are independent once their index is known, so there is no data
 collective; RCCL all-reduces the per-rank counters and the max time.
 """
 import argparse
+import ctypes
 import json
 import os
 import subprocess
@@ -547,7 +548,37 @@ def main():
         forge_idx = torch.from_numpy(pos[forge_pk].astype(np.int64) +
                                      12 + 20).to(dev)
 
+    # synchronous device calls: each step's two calls prepared before the
+    # timed region (their argument structs, the C entry points), so the
+    # timed loop is the library's calls and not Python argument marshalling
+    prepared = {}
+
+    def prepare(sets, k0=0):
+        prepared.clear()
+        if not (use_dev and not use_async and not args.e2e and
+                forge_idx is None):
+            return
+        for k, (tx, rx) in enumerate(sets):
+            calls = []
+            for d, (opname, ss) in enumerate(((OPS[0], tx), (OPS[1], rx))):
+                b = P.SrtpBatchDev()
+                b.arena, b.arena_size = arena.data_ptr(), arena.numel()
+                b.pos, b.end = winp[k0 + k].data_ptr(), wine[k0 + k].data_ptr()
+                b.cap, b.err = cap_d.data_ptr(), errbuf[d, k0 + k].data_ptr()
+                b.sess = sess_d.data_ptr() if sess_d is not None else None
+                b.n, b.stream = n, sptr
+                sv = P.session_array(ss)
+                calls.append((getattr(P.lib(), opname + "_batch_dev"), sv,
+                              len(sv), ctypes.byref(b), b))
+            prepared[(id(tx), k0 + k)] = calls
+
     def step(tx, rx, k=0, inflight=None):
+        pc = prepared.get((id(tx), k))
+        if pc is not None:
+            for fn, sv, ns, bref, _ in pc:
+                rc = fn(sv, ns, bref)
+                assert rc == 0, (rc, P.lib().srtp_gpu_error())
+            return 0
         if use_dev:
             err_ed, err_dd = errbuf[0, k], errbuf[1, k]
         if args.e2e:
@@ -640,11 +671,13 @@ def main():
     log("warmup done, timed steps")
     sess_sets = [(P.session_array(tx), P.session_array(rx))
                  for tx, rx in sess_objs]
-    P.prof_enable(True)
+    # RE_SRTP_BENCH_NOPROF: no in-run kernel events (A/B of their cost)
+    P.prof_enable(not os.environ.get("RE_SRTP_BENCH_NOPROF"))
     P.prof_read()
     if use_dev:
         errbuf.fill_(-1)        # every call must write every result
         reset_windows()
+    prepare(sess_sets)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -130,12 +130,11 @@ __device__ __forceinline__ bool fast_pkt(const struct sgpu_compact &c,
 	return true;
 }
 
-/* round keys of the launch's one context in SGPRs, plain (T4 rounds) */
+/* round keys of context ci (uniform) in SGPRs, plain (T4 rounds) */
 template <int NR>
 __device__ __forceinline__ const struct sgpu_comp *
-fast_keys(const KArgs &a, uint32_t rk[4 * (NR + 1)])
+fast_keys_at(const KArgs &a, uint32_t ci, uint32_t rk[4 * (NR + 1)])
 {
-	const uint32_t ci = __builtin_amdgcn_readfirstlane(a.c.compmap[0]);
 	const struct sgpu_comp *cp = a.comps + ci;
 #pragma unroll
 	for (int k = 0; k < NR + 1; k++) {
@@ -150,6 +149,15 @@ fast_keys(const KArgs &a, uint32_t rk[4 * (NR + 1)])
 	for (int k = 0; k < 4 * (NR + 1); k++)
 		rk[k] = __builtin_amdgcn_readfirstlane(rk[k]);
 	return cp;
+}
+
+/* ... of the launch's one context (c.compmap[0]) */
+template <int NR>
+__device__ __forceinline__ const struct sgpu_comp *
+fast_keys(const KArgs &a, uint32_t rk[4 * (NR + 1)])
+{
+	return fast_keys_at<NR>(
+		a, __builtin_amdgcn_readfirstlane(a.c.compmap[0]), rk);
 }
 
 /* round keys of packet f's own context in VGPRs (multi-session batches:
@@ -220,19 +228,17 @@ __device__ __forceinline__ void tail_xor_store(const uint8_t *smem,
  * of the tag; unprotect: the 4 bytes in front of the tag, so A = L - T -
  * 4), no ROC written over the tag, E = 0: no cipher region.
  */
+/* one planned packet f (T4 image already in smem); ci: the launch's one
+ * context (uniform), unused with MK */
 template <int NR, int SHIFT, bool PROT, bool MK = false, bool RTCP = false>
-__device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
+__device__ __forceinline__ void ctr_fast_pkt(const KArgs &a, uint8_t *smem,
+					     const FastPkt &f, uint32_t ci)
 {
-	tt4_fill(smem, a.t0);
-	__syncthreads();
-	FastPkt f;
-	if (!fast_pkt<RTCP>(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
-		return;
 	uint32_t rk[4 * (NR + 1)];
 	/* MK: every lane its own session context (keys in VGPRs); all of
 	 * them one suite, so the tag length stays uniform */
 	const struct sgpu_comp *cp = MK ? lane_keys<NR>(a, f, rk)
-					: fast_keys<NR>(a, rk);
+					: fast_keys_at<NR>(a, ci, rk);
 	const uint32_t lo = (threadIdx.x & 31u) * 4u;
 	const uint32_t lane = threadIdx.x & 63u;
 	uint8_t *const arena = a.arena;
@@ -458,6 +464,19 @@ __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 	}
 	if (a.verdict)
 		a.verdict[f.p] = vd;
+}
+
+template <int NR, int SHIFT, bool PROT, bool MK = false, bool RTCP = false>
+__device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
+{
+	tt4_fill(smem, a.t0);
+	__syncthreads();
+	FastPkt f;
+	if (!fast_pkt<RTCP>(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))
+		return;
+	ctr_fast_pkt<NR, SHIFT, PROT, MK, RTCP>(
+		a, smem, f,
+		MK ? 0u : __builtin_amdgcn_readfirstlane(a.c.compmap[0]));
 }
 
 /*

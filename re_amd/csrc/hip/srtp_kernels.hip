@@ -32,6 +32,8 @@
 #include <string.h>
 #include "../srtpgpu.h"
 #include "kern_common.h"
+#include "plan_common.h"
+#include "k_ctr_fused.h"
 
 #ifndef EAUTH
 #define EAUTH 217               /* include/re_types.h:215-217 */
@@ -240,54 +242,6 @@ __global__ void k_setup(const struct sgpu_keyreq *__restrict__ req,
 /* rtp_hdr_decode (src/rtp/rtp.c:88-137), including the position at
  * which each EBADMSG is raised.  get_rtcp_ssrc (srtcp.c:19-28).        */
 
-/* one RTP header (rtp_hdr_decode, rtp.c:88-137) from a window of `left`
- * bytes at b (p: its arena offset, for the aligned fast load) */
-__device__ __forceinline__ struct sgpu_hdr parse_rtp_hdr(const uint8_t *b,
-							 uint32_t p,
-							 uint32_t left)
-{
-	struct sgpu_hdr h;
-	h.ssrc = 0; h.seq = 0; h.err_pos = 0; h.hdr_len = 0xffffffffu;
-	if (left < 12)
-		return h;
-	uint32_t b0;
-	if (!(p & 3u)) {
-		const uint32_t w0 = *(const uint32_t *)b;
-		const uint32_t w2 = *(const uint32_t *)(b + 8);
-		b0 = w0 & 0xffu;
-		h.seq = (uint16_t)((w0 >> 8 & 0xff00u) | (w0 >> 24));
-		h.ssrc = __builtin_bswap32(w2);
-	}
-	else {
-		b0 = b[0];
-		h.seq = (uint16_t)(b[2] << 8 | b[3]);
-		h.ssrc = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 |
-			 (uint32_t)b[10] << 8 | b[11];
-	}
-	const uint32_t cc = b0 & 0x0fu, x = (b0 >> 4) & 1u;
-	uint32_t hl = 12;
-	if (left - hl < 4 * cc) {
-		h.err_pos = (uint16_t)hl;
-		return h;
-	}
-	hl += 4 * cc;
-	if (x) {
-		if (left - hl < 4) {
-			h.err_pos = (uint16_t)hl;
-			return h;
-		}
-		const uint32_t xl = (uint32_t)b[hl + 2] << 8 | b[hl + 3];
-		hl += 4;
-		if (left - hl < 4 * xl) {
-			h.err_pos = (uint16_t)hl;
-			return h;
-		}
-		hl += 4 * xl;
-	}
-	h.hdr_len = hl;
-	return h;
-}
-
 /*
  * k_parse for an RTP batch of a device planner, with the planner's
  * per-packet window checks (k_plan_count / k_mp_count) made here, where
@@ -442,24 +396,6 @@ __global__ void k_parse(const uint8_t *__restrict__ arena, uint64_t asz,
 
 #define PLAN_BLOCK 256
 
-/* sgpu_desc() (srtpgpu.h) on the device */
-__device__ __forceinline__ uint64_t d_desc(uint64_t ix, uint32_t flags)
-{
-	return (ix & 0xffffull) | ((uint64_t)(uint32_t)(ix >> 16) << 16) |
-	       ((uint64_t)flags << 48);
-}
-
-/* srtp_get_index (misc.c:22-41), including the int wrap of roc +- 1 */
-__device__ __forceinline__ int32_t plan_v(uint32_t roc, uint32_t s_l,
-					  uint32_t seq)
-{
-	if (s_l < 32768)
-		return ((int)seq - (int)s_l > 32768) ? (int32_t)(roc - 1)
-						     : (int32_t)roc;
-	return ((int)s_l - 32768 > (int)seq) ? (int32_t)(roc + 1)
-					     : (int32_t)roc;
-}
-
 /* speculated s_l seen by packet i: the previous packet's seq */
 __device__ __forceinline__ uint32_t plan_sb(const struct sgpu_plan_in &in,
 					    const struct sgpu_hdr *hdr,
@@ -468,12 +404,6 @@ __device__ __forceinline__ uint32_t plan_sb(const struct sgpu_plan_in &in,
 	if (i == 0)
 		return in.fresh ? hdr[0].seq : in.s_l;
 	return hdr[i - 1].seq;
-}
-
-/* ROC rollover seen by a packet (srtp.c:208-213, 318-321) */
-__device__ __forceinline__ bool plan_wrap(uint32_t seq, uint32_t sb)
-{
-	return (int)seq - (int)sb <= -32768;
 }
 
 __global__ void __launch_bounds__(PLAN_BLOCK)
@@ -1186,6 +1116,53 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 	return e;
 }
 
+/* the same profiling bracket around a fused plan + crypto launch
+ * (k_ctr_fused.h): never voided as a whole (each workgroup plans itself) */
+typedef void (*kfn_f)(const FArgs);
+kfn_f sgpu_pick_fused(int nr, int prot, int undo);      /* fused.hip */
+
+/* grid = n / block; jobs: the packets it processes (srtp_gpu_prof) */
+static int launch_fused(kfn_f f, const FArgs &a, uint32_t n, uint32_t jobs,
+			int slot, hipStream_t stream, uint32_t block,
+			const char *name, int nr, int prot)
+{
+	struct prof_ev pe;
+	int prof = 0;
+	if (g_prof_on && slot >= 0) {
+		prof = hipEventCreate(&pe.a) == hipSuccess &&
+		       hipEventCreate(&pe.b) == hipSuccess;
+		if (prof)
+			(void)hipEventRecord(pe.a, stream);
+	}
+	hipLaunchKernelGGL(f, dim3((n + block - 1) / block), dim3(block), 0,
+			   stream, a);
+	int e = herr(hipGetLastError(), "fused launch");
+	if (prof) {
+		(void)hipEventRecord(pe.b, stream);
+		pe.slot = slot;
+		pe.jobs = jobs;
+		pe.name = name;
+		pe.nr = nr;
+		pe.prot = prot;
+		pe.gw = 0;
+		pe.gslot = -1;
+		pthread_mutex_lock(&g_prof_lock);
+		if (g_npev == g_pev_cap) {
+			size_t nc = g_pev_cap ? 2 * g_pev_cap : 64;
+			struct prof_ev *np = (struct prof_ev *)realloc(
+				g_pev, nc * sizeof(*np));
+			if (np) {
+				g_pev = np;
+				g_pev_cap = nc;
+			}
+		}
+		if (g_npev < g_pev_cap)
+			g_pev[g_npev++] = pe;
+		pthread_mutex_unlock(&g_prof_lock);
+	}
+	return e;
+}
+
 static int prof_slot(int mode, int nr, int shift, int prot)
 {
 	return (prot ? 16 : 0) + (mode ? 8 : 0) + (nr == 14 ? 4 : 0) +
@@ -1399,6 +1376,87 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 				  (c->uniform ? "k_ctr_hmac_uni"
 					      : "k_ctr_hmac_compact"),
 		      nr, prot, mode == SGPU_MODE_CTR && shift < 0 ? 4 : 1);
+}
+
+/* ---- single-stream batches planned inside the crypto launch ---------- */
+
+static void fz_args(FArgs &fa, uint8_t *arena, uint64_t asz,
+		   const struct sgpu_fused *f)
+{
+	memset(&fa, 0, sizeof(fa));
+	KArgs &a = fa.a;
+	a.arena = arena;
+	a.asz = asz;
+	a.comps = (const struct sgpu_comp *)g_table;
+	a.t0 = g_T0_dev;
+	a.verdict = f->verdict;
+	a.save = f->save;
+	/* what the launches behind it (k_ctr_refix_list, the undo) read as a
+	 * compact batch: windows with the original ends, the parsed headers,
+	 * the descriptors, the context index the launch stored */
+	a.c.pos = f->pos;
+	a.c.end = f->es;
+	a.c.hdr = f->hdr;
+	a.c.desc = f->desc;
+	a.c.compmap = f->cm_out;
+	a.c.n = f->in.n;
+	a.c.verdict = f->verdict;
+	a.c.save = f->save;
+	a.c.nfail = &f->out->nfail;
+	a.c.flist = f->flist;
+	a.c.uniform = 2;
+	fa.p = *f;
+}
+
+extern "C" unsigned sgpu_fused_block(void)
+{
+	return FZ_BLOCK;
+}
+
+extern "C" int sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
+			      struct sgpu_fused *f, int nr, void *stream)
+{
+	FArgs fa;
+	if (!f->in.n || (nr != 10 && nr != 14))
+		return EINVAL;
+	const int prot = f->in.prot != 0;
+	const uint32_t nwg = (f->in.n + FZ_BLOCK - 1) / FZ_BLOCK;
+	f->ntickets = nwg;
+	fz_args(fa, arena, arena_size, f);
+	return launch_fused(sgpu_pick_fused(nr, prot, 0), fa, nwg * FZ_BLOCK,
+			    f->in.n, prof_slot(SGPU_MODE_CTR, nr, 3, prot),
+			    (hipStream_t)stream, FZ_BLOCK, "k_ctr_fused", nr,
+			    prot);
+}
+
+extern "C" int sgpu_fused_undo(uint8_t *arena, uint64_t arena_size,
+			       const struct sgpu_fused *f, int nr, int prot,
+			       void *stream)
+{
+	FArgs fa;
+	if (!f->in.n || (nr != 10 && nr != 14) || f->shift > 3)
+		return EINVAL;
+	fz_args(fa, arena, arena_size, f);
+	hipLaunchKernelGGL(sgpu_pick_fused(nr, prot, 1),
+			   dim3((f->in.n + FZ_BLOCK - 1) / FZ_BLOCK),
+			   dim3(FZ_BLOCK), 0, (hipStream_t)stream, fa);
+	return herr(hipGetLastError(), "fused undo launch");
+}
+
+extern "C" int sgpu_fused_refix(uint8_t *arena, uint64_t arena_size,
+				const struct sgpu_fused *f, int nr,
+				void *stream)
+{
+	FArgs fa;
+	if (!f->in.n || (nr != 10 && nr != 14))
+		return EINVAL;
+	fz_args(fa, arena, arena_size, f);
+	/* one workgroup per listed forged packet, grid-strided past 1024 */
+	const uint32_t g = f->in.n < 1024u ? f->in.n : 1024u;
+	hipLaunchKernelGGL(nr == 10 ? sgpu_pick_ctr10_fast(0, 2)
+				    : sgpu_pick_ctr14_fast(0, 2),
+			   dim3(g), dim3(256), 0, (hipStream_t)stream, fa.a);
+	return herr(hipGetLastError(), "fused refix launch");
 }
 
 extern "C" int sgpu_parse_headers(const uint8_t *arena, uint64_t arena_size,

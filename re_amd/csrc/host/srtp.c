@@ -94,6 +94,7 @@ static void env_read(void)
 	g_env.trace = getenv("RE_SRTP_TRACE") != NULL;
 	g_env.nosmall = getenv("RE_SRTP_NOSMALL") != NULL;
 	g_env.times = getenv("RE_SRTP_TIMES") != NULL;
+	g_env.noplanfuse = getenv("RE_SRTP_NOPLANFUSE") != NULL;
 	if (getenv("RE_SRTP_NOCOOP"))
 		sgpu_set_coop(0);
 	e = getenv("RE_SRTP_CHUNK");
@@ -115,6 +116,8 @@ static uint64_t g_cnt_folds;    /* batches re-run to fold verdicts */
 static uint64_t g_cnt_rejects;  /* device plans rejected */
 static uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 static uint64_t g_cnt_splans;   /* per-stream device plans accepted */
+static uint64_t g_cnt_fused;    /* batches planned inside the crypto launch
+				   (dev_fused), accepted */
 /* a session's first batch (no stream yet) goes to the per-stream planner
  * while the last first batch planned showed several SSRCs: a one-stream
  * plan for it is rejected at completion and the batch planned again, a
@@ -161,6 +164,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_devfolds, __ATOMIC_RELAXED);
 	if (!strcmp(name, "splans"))
 		return __atomic_load_n(&g_cnt_splans, __ATOMIC_RELAXED);
+	if (!strcmp(name, "fused"))
+		return __atomic_load_n(&g_cnt_fused, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcbatches"))
 		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcpackets"))
@@ -224,6 +229,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "nosmall"))
 		g_env.nosmall = value > 0;
+	else if (!strcmp(name, "noplanfuse"))
+		g_env.noplanfuse = value > 0;
 	else if (!strcmp(name, "nofuse"))
 		g_env.nofuse = value > 0;
 	else if (!strcmp(name, "smallsync"))
@@ -3485,6 +3492,180 @@ static int dev_planned_finish(struct dcall *k)
 	return -1;
 }
 
+
+/* ---- one stream, planned inside the crypto launch (k_ctr_fused.h) ----- */
+
+#define FZ_HEAD 64u             /* ticket word, padded */
+#define FZ_PO_SZ ((sizeof(struct sgpu_plan_out) + 63u) & ~(size_t)63)
+
+/*
+ * Synchronous single-stream AES-CM batch: one launch parses, plans and
+ * encrypts / decrypts (srtpgpu.h struct sgpu_fused); with no forged packet
+ * nothing else runs on the device.  Forged packets: their ciphertext back
+ * (k_ctr_refix_list) and the device verdict fold (sgpu_fold_rtp), launched
+ * after the synchronisation showed a miss.  A rejected plan or a fold the
+ * device cannot settle: every processed packet undone (sgpu_fused_undo),
+ * the ends restored, and -1 (*pfail: the plan's SPF_* bits, 0 for a fold)
+ * -- the caller plans on the host, as for dev_planned.
+ */
+static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
+		     uint32_t *pfail)
+{
+	const int prot = op == OP_RTP_ENC;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const uint32_t T = c0->tag_len;
+	const uint32_t need = prot ? (T > 4 ? T : 4u) : 0u;
+	const uint32_t B = sgpu_fused_block();
+	const uint32_t nblk = (uint32_t)((n + B - 1) / B);
+	const unsigned ns0 = s->nstreams;
+	struct ws *w = ws_get();
+	struct sgpu_fused F;
+	struct sgpu_plan_out *po;
+	struct srtp_stream old;
+	void *stream = d->stream;
+	uint8_t *fz;
+	size_t poff;
+	int err;
+
+	*pfail = 0;
+	if (!w)
+		return ENOMEM;
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 8);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 9 + 72);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, 64 + (n / 256 + 4) * 20);
+	if (!err)
+		err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_PO_SZ +
+				   (size_t)nblk * 8);
+	if (err)
+		return err;
+	fz = w->fz.d;
+	if (w->fz_d != fz || w->fz_epoch == 0 || w->fz_epoch > 0xffffu) {
+		/* a new pool (or the look-back epoch wrapped): counters,
+		 * plan outs and look-back words from zero */
+		err = sgpu_memset(fz, 0, w->fz.cap, stream);
+		if (err)
+			return err;
+		w->fz_d = fz;
+		w->fz_epoch = 1;
+		w->fz_tbase = 0;
+		w->fz_par = 0;
+	}
+	poff = FZ_HEAD + (size_t)w->fz_par * FZ_PO_SZ;
+
+	memset(&F, 0, sizeof(F));
+	plan_in(&F.in, s, (uint32_t)n, prot, T, need);
+	F.in.zeroed = 1;
+	F.pos = d->pos;
+	F.end = d->end;
+	F.cap = d->cap;
+	F.err = d->err;
+	F.es = (uint32_t *)w->es.d;
+	F.hdr = (struct sgpu_hdr *)w->hd.d;
+	F.desc = (uint64_t *)w->dsc.d;
+	F.save = (uint32_t *)(w->vs.d + 64);
+	F.verdict = w->vs.d + 64 + n * 4;
+	F.flist = (uint32_t *)(w->vs.d + ((64 + n * 5 + 3) & ~(size_t)3));
+	F.out = (struct sgpu_plan_out *)(fz + poff);
+	F.out_next = (struct sgpu_plan_out *)(fz + FZ_HEAD +
+					      (size_t)(w->fz_par ^ 1) * FZ_PO_SZ);
+	F.cm_out = (uint32_t *)w->cm.d;
+	F.agg = (unsigned long long *)(fz + FZ_HEAD + 2 * FZ_PO_SZ);
+	F.ticket = (uint32_t *)fz;
+	F.tbase = w->fz_tbase;
+	F.epoch = w->fz_epoch;
+	F.comp = c0->dev;
+	F.delta = prot ? (int32_t)T : -(int32_t)T;
+	if (prot) {
+		F.verdict = NULL;
+		F.save = NULL;
+		F.flist = NULL;
+	}
+	err = sgpu_run_fused(d->arena, d->arena_size, &F, (int)c0->nr, stream);
+	if (!err) {
+		w->fz_tbase += F.ntickets;
+		w->fz_epoch++;
+		w->fz_par ^= 1;
+		err = sgpu_memcpy_d2h(w->fz.h + poff, F.out, sizeof(*po), stream);
+	}
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err) {
+		w->fz_d = NULL;         /* counters unknown: from zero next time */
+		return err;
+	}
+	po = (struct sgpu_plan_out *)(w->fz.h + poff);
+	if (po->fail) {
+		*pfail = po->fail;
+		if (po->fail & SPF_BAD)
+			w->fz_d = NULL; /* ticket / look-back state from zero */
+		if ((po->fail & SPF_SSRC) && !ns0)
+			__atomic_store_n(&g_fresh_multi, 1, __ATOMIC_RELAXED);
+		count(&g_cnt_rejects, 1);
+		goto undo;
+	}
+	plan_apply(s, po, prot, n, &old);
+	count(&g_cnt_fused, 1);
+	if (!po->nfail)
+		return 0;
+	count(&g_cnt_misses, po->nfail);
+	if (!g_env.nodevfold) {
+		/* forged packets: ciphertext back, verdicts folded on the
+		 * device; its outcome comes back in one copy */
+		struct sgpu_fold_out *fo_d = (struct sgpu_fold_out *)w->pl.d;
+		const struct sgpu_fold_out *fo = (const struct sgpu_fold_out *)
+						 w->pl.h;
+		err = sgpu_fused_refix(d->arena, d->arena_size, &F,
+				       (int)c0->nr, stream);
+		if (!err)
+			err = sgpu_fold_rtp(0, &F.out->nfail, &F.in, F.hdr,
+					    F.desc, F.verdict, F.es, d->pos,
+					    d->end, d->err, 0,
+					    (uint32_t *)(w->pl.d + 64), fo_d,
+					    stream);
+		if (!err)
+			err = sgpu_memcpy_d2h(w->pl.h, fo_d, sizeof(*fo),
+					      stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		if (err)
+			return err;
+		if (!fo->fail) {
+			struct srtp_stream *st = &s->streams[0];
+			st->s_l = (uint16_t)fo->s_l;
+			st->replay_rtp.lix = fo->lix;
+			st->replay_rtp.bitmap = fo->bitmap;
+			count(&g_cnt_devfolds, 1);
+			return 0;
+		}
+	}
+	/* the fold cannot be settled on the device (or nodevfold): undo --
+	 * forged packets still decrypted are re-encrypted with the rest --
+	 * and fold on the host */
+	count(&g_cnt_folds, 1);
+	plan_unapply(s, ns0, &old);
+ undo:
+	if (po->hl0 != 0xffffffffu && !(po->fail & SPF_PRED)) {
+		F.shift = (po->hl0 >> 2) & 3u;
+		err = sgpu_fused_undo(d->arena, d->arena_size, &F, (int)c0->nr,
+				      prot, stream);
+		if (err)
+			return err;
+	}
+	err = sgpu_memcpy_d2d(d->end, F.es, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	return err ? err : -1;
+}
+
 /* synchronous: -1 not plannable (nothing modified; *pfail: why, 0 for a
  * forged packet the host must fold), else 0 / errno */
 static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
@@ -3492,6 +3673,8 @@ static int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
 {
 	struct dcall k;
 	int err;
+	if (s->rtp.mode == SGPU_MODE_CTR && !g_env.noplanfuse)
+		return dev_fused(op, s, d, pfail);
 	memset(&k, 0, sizeof(k));
 	k.op = op;
 	k.sessv = &s;

@@ -108,6 +108,10 @@ struct srtp_env {
 	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
 				   launch by a stream synchronisation, not
 				   its completion word */
+	int noplanfuse;         /* srtp_gpu_tune noplanfuse: single-stream
+				   batches take the separate device planner
+				   (k_parse + k_plan_*), not the plan inside
+				   the crypto launch (k_ctr_fused.h) */
 	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
 				   shared per-packet launch run as separate
 				   launches (helper thread), not one */
@@ -196,6 +200,13 @@ struct ws {
 				   (on the side stream w->stream) */
 	size_t nev;
 	struct ulogv ulog[1];   /* stream-state undo log */
+	/* single-stream batches planned inside the crypto launch
+	 * (dev_fused): ticket | pad | plan out x2 | look-back words */
+	struct pool fz;
+	uint8_t *fz_d;          /* fz.d the state below belongs to */
+	uint32_t fz_tbase;      /* the next launch's first ticket */
+	uint32_t fz_epoch;      /* the next launch's look-back epoch */
+	uint32_t fz_par;        /* which plan out the next launch uses */
 	/* the small kernel's completion word (small_wait) */
 	uint32_t *sm_cnt;       /* device */
 	uint32_t *sm_flag;      /* pinned host */

@@ -281,6 +281,66 @@ struct sgpu_plan_out {
 	uint64_t tail_ix[SGPU_PLAN_TAIL]; /* ix of the last min(n,65) packets */
 };
 
+/*
+ * Single-stream AES-CM batch planned INSIDE its crypto launch
+ * (k_ctr_fused.h): each workgroup parses its packets' headers, makes every
+ * check of sgpu_plan_rtp, takes its ROC prefix from the workgroups before
+ * it by a decoupled look-back over agg[] (ticket order, so each
+ * predecessor is running or done), then encrypts / decrypts.  A workgroup
+ * that sees a failed check (its own, or one published before it) does
+ * nothing; out->fail != 0 after the launch means the batch must be undone
+ * (sgpu_fused_undo: every packet whose desc has SD_RUN back to its bytes)
+ * and planned on the host -- the same "a rejected plan modifies nothing"
+ * as the separate planner.  Per packet the launch writes hdr, es (the end
+ * before the call) and desc (0: not processed); processed packets also
+ * end + delta, err = 0 and (unprotect) verdict / save / flist / nfail.
+ * out (fail, nfail) must be zero at launch: the workgroup with ticket 0
+ * zeroes out_next's for the workspace's next launch.  agg: one word per
+ * workgroup (n / sgpu_fused_block()), (epoch << 48 | status << 46 |
+ * fail << 32 | wraps); epoch 1..65535, the host zeroes agg when it wraps.
+ * ticket: the workgroups take tbase, tbase + 1, ... (the next launch's
+ * tbase: + f->ntickets).
+ */
+struct sgpu_fused {
+	struct sgpu_plan_in in;
+	const uint32_t *pos;
+	uint32_t *end;
+	const uint32_t *cap;            /* or NULL */
+	int32_t *err;
+	uint32_t *es;
+	struct sgpu_hdr *hdr;
+	uint64_t *desc;
+	uint8_t *verdict;               /* unprotect */
+	uint32_t *save;                 /* unprotect: tag word under the ROC */
+	uint32_t *flist;                /* unprotect: forged packets */
+	struct sgpu_plan_out *out;
+	struct sgpu_plan_out *out_next;
+	uint32_t *cm_out;               /* *cm_out = comp (for later launches) */
+	unsigned long long *agg;
+	uint32_t *ticket;
+	uint32_t tbase;
+	uint32_t epoch;
+	uint32_t comp;                  /* the session's sgpu_comp index */
+	int32_t delta;                  /* end change of a processed packet */
+	uint32_t shift;                 /* undo: the batch's header class */
+	uint32_t ntickets;              /* (out) tickets the launch takes (its
+					   workgroups) -- the next tbase */
+};
+unsigned sgpu_fused_block(void);        /* packets per workgroup */
+int   sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
+		     struct sgpu_fused *f, int nr, void *stream);
+/* after a rejected fused launch (f->shift = class of packet 0's header):
+ * every processed packet back to its bytes before the call -- protect: the
+ * keystream re-applied over [hl, L); unprotect: over [hl, L - tag) where
+ * still decrypted (SV_CIPHERED), and the tag word under the ROC restored */
+int   sgpu_fused_undo(uint8_t *arena, uint64_t arena_size,
+		      const struct sgpu_fused *f, int nr, int prot,
+		      void *stream);
+/* unprotect with forged packets: their ciphertext back (the list the
+ * launch filled, k_ctr_refix_list) -- before sgpu_fold_rtp */
+int   sgpu_fused_refix(uint8_t *arena, uint64_t arena_size,
+		       const struct sgpu_fused *f, int nr, void *stream);
+
 /* plan n packets (hdr/pos/end/cap device arrays; cap may be NULL) into
  * desc (device); scratch holds >= n/256 + 2 words; out is a device
  * pointer.  out->fail is the guard of the launches that follow. */

@@ -14,9 +14,11 @@ while [ $# -ge 2 ]; do
   $HIPCC $FL $defs -c csrc/hip/ctr10a.hip -o /tmp/variants/ctr10a_$name.o &
   $HIPCC $FL $defs -c csrc/hip/gcm.hip -o /tmp/variants/gcm_$name.o &
   $HIPCC $FL $defs -c csrc/hip/plan_multi.hip -o /tmp/variants/plan_multi_$name.o &
+  $HIPCC $FL $defs -c csrc/hip/fused.hip -o /tmp/variants/fused_$name.o &
   wait
   objs="build/srtp.o build/percall.o build/rxfold.o build/pool.o build/udp.o build/keying.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/ctr14a.o build/plan_streams.o build/dtls_prf.o build/rtcp_walk.o build/rtcp_encode.o build/small.o"
   $HIPCC -shared -fPIC --offload-arch=gfx950 -o lib/variants/$name.so $objs -Wl,--version-script=build/exports.map \
-    /tmp/variants/ctr10_$name.o /tmp/variants/ctr10a_$name.o /tmp/variants/gcm_$name.o /tmp/variants/plan_multi_$name.o -lpthread
+    /tmp/variants/ctr10_$name.o /tmp/variants/ctr10a_$name.o /tmp/variants/gcm_$name.o /tmp/variants/plan_multi_$name.o \
+    /tmp/variants/fused_$name.o -lpthread
   echo "built lib/variants/$name.so ($defs)"
 done

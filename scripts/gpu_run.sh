@@ -17,7 +17,7 @@ fi
 IFS=';' read -ra BS <<< "${BENCHES:-}"
 for nb in "${BS[@]}"; do
   n=${nb%%=*}; a=${nb#*=}
-  timeout -k 10 300 python bench.py $a > $O/$n.json 2> $O/$n.err || exit $?
+  timeout -k 10 ${BENCH_TIMEOUT:-150} python bench.py $a > $O/$n.json 2> $O/$n.err || exit $?
 done
 IFS=';' read -ra TS <<< "${TRACES:-}"
 for nb in "${TS[@]}"; do

@@ -1,0 +1,185 @@
+"""Single-stream AES-CM batches planned inside the crypto launch
+(k_ctr_fused.h, host dev_fused): srtp_*_batch_dev of one session and one
+SSRC runs one launch that parses, plans (decoupled look-back over its
+1024-packet workgroups) and encrypts / decrypts.  It must give exactly the
+separate device planner's results (srtp_gpu_tune noplanfuse: k_parse +
+k_plan_* + the lean kernel, pinned by the reference digests in earlier
+rounds) and the general engine's: arena, pos, end, errno and stream
+state -- for batches the plan accepts and for every rejection, wherever in
+the batch the broken assumption sits (first, middle or last workgroup),
+which the fused path must undo completely before the host re-plans
+(srtp.c:183-432, misc.c:22-41, replay.c:32-62 of the reference).
+"""
+import numpy as np
+import pytest
+
+import re_amd.srtp as P
+from tests.test_gpu_fastpath import keys_for, rtp_packet, run_dev, states, \
+    to_arena
+
+pytestmark = pytest.mark.gpu
+
+SSRC = 0x5151
+N = 5000                # five workgroups of 1024 packets
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    P.load()
+    return torch
+
+
+def batch(rng, seqs, ssrc_at=(), csrc_at=(), short_at=(), plen=64):
+    out = []
+    for i, s in enumerate(seqs):
+        pkt = rtp_packet(rng, s & 0xffff, 0x7777 if i in ssrc_at else SSRC,
+                         cc=1 if i in csrc_at else 0, plen=plen)
+        if i in short_at:
+            pkt = pkt[:7]
+        out.append((0, pkt))
+    return out
+
+
+def cases(s0):
+    base = list(range(s0, s0 + N))
+    mid, last = 2600, N - 3
+    return {
+        "inorder": (base, {}),
+        "reorder_first": (base[:5] + [base[6], base[5]] + base[7:], {}),
+        "reorder_mid": (base[:mid] + [base[mid + 1], base[mid]] +
+                        base[mid + 2:], {}),
+        "reorder_last": (base[:last] + [base[last + 1], base[last]] +
+                         base[last + 2:], {}),
+        "replay_mid": (base[:mid] + [base[mid - 10]] + base[mid + 1:], {}),
+        "jump_last": (base[:last] + [base[last] + 40000] + base[last + 1:],
+                      {}),
+        "class_mid": (base, {"csrc_at": (mid,)}),
+        "ssrc_last": (base, {"ssrc_at": (N - 1,)}),
+        "short_mid": (base, {"short_at": (mid,)}),
+    }
+
+
+def run_modes(torch, suite, key, op, pkts, state_from=None, cap_short=()):
+    """the batch through the fused path, the separate planner and the
+    general engine; returns {mode: (outputs, state, counters)}"""
+    arena, pos, end, cap, _ = to_arena(pkts, short_cap=cap_short)
+    res = {}
+    for mode, tune in (("fused", {}), ("planner", {"noplanfuse": 1}),
+                       ("general", {"general": 1})):
+        ctx = P.Srtp(suite, key)
+        if state_from is not None:
+            assert ctx.import_(state_from) == 0
+        f0, r0 = P.counter("fused"), P.counter("rejects")
+        with P.tune(**tune):
+            out = run_dev(torch, op, [ctx], arena, pos, end, cap, None)
+        res[mode] = (out, states([ctx], [SSRC]),
+                     (P.counter("fused") - f0, P.counter("rejects") - r0))
+        ctx.close()
+    return res
+
+
+def same(res, name):
+    A = res["fused"]
+    for mode in ("planner", "general"):
+        B = res[mode]
+        for k, (x, y) in enumerate(zip(A[0], B[0])):
+            assert (x == y).all(), (name, mode, ("arena", "pos", "end",
+                                                 "err")[k])
+        assert A[1] == B[1], (name, mode, A[1], B[1])
+
+
+@pytest.mark.parametrize("suite", [1, 0, 2])
+@pytest.mark.parametrize("s0", [65000, 100])
+def test_fused_equals_planner_and_general(suite, s0, torch_cuda):
+    torch = torch_cuda
+    rng = np.random.default_rng(1000 + suite + s0)
+    key = keys_for(suite, 1)[0]
+    for name, (seqs, kw) in cases(s0).items():
+        pkts = batch(rng, seqs, **kw)
+        res = run_modes(torch, suite, key, "srtp_encrypt", pkts)
+        same(res, name + "/protect")
+        # a forward jump of 40000 is only ETIMEDOUT for the receiver
+        accepted = name in ("inorder", "jump_last")
+        assert res["fused"][2] == ((1, 0) if accepted else (0, 1)), \
+            (name, res["fused"][2])
+        # receive what the accepted protect produced (in-order stream),
+        # with the same defect injected on the protected packets
+        out = res["fused"][0]
+        prot = [(0, out[0][out[1][i]:out[2][i]].tobytes())
+                for i in range(len(pkts)) if out[3][i] == 0]
+        if name == "reorder_mid":
+            prot = prot[:2600] + [prot[2601], prot[2600]] + prot[2602:]
+        elif name == "replay_mid":
+            prot = prot[:2600] + [prot[2590]] + prot[2601:]
+        dres = run_modes(torch, suite, key, "srtp_decrypt", prot)
+        same(dres, name + "/unprotect")
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_fused_forged_packets_fold_on_device(suite, torch_cuda):
+    """forged packets in several workgroups: the fused launch counts the
+    misses, the host then restores their ciphertext and folds the verdicts
+    on the device (no rejection); a forged packet followed by a rollover
+    the fold cannot settle is undone and folded on the host"""
+    torch = torch_cuda
+    rng = np.random.default_rng(33 + suite)
+    key = keys_for(suite, 1)[0]
+    seqs = list(range(65500, 65500 + N))
+    pkts = batch(rng, seqs)
+    res = run_modes(torch, suite, key, "srtp_encrypt", pkts)
+    same(res, "protect")
+    out = res["fused"][0]
+    prot = [(0, out[0][out[1][i]:out[2][i]].tobytes())
+            for i in range(len(pkts))]
+    for forged in ([17], [36], [3, 1500, 4096, N - 1], list(range(0, N, 97))):
+        q = list(prot)
+        for i in forged:
+            b = bytearray(q[i][1])
+            b[20] ^= 0x10
+            q[i] = (0, bytes(b))
+        dres = run_modes(torch, suite, key, "srtp_decrypt", q)
+        same(dres, "forged %d" % len(forged))
+        errs = dres["fused"][0][3]
+        assert (errs[forged] == P.EAUTH).all()
+        assert dres["fused"][2] == (1, 0)
+
+
+def test_fused_short_capacity_and_continuation(torch_cuda):
+    """protect with one packet short of tag room (ENOMEM on the host
+    re-plan) in the last workgroup, then a second batch continuing the
+    stream from the first one's state (the fused path's state update)"""
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    key = keys_for(1, 1)[0]
+    seqs = list(range(65530, 65530 + N))
+    pkts = batch(rng, seqs)
+    res = run_modes(torch, 1, key, "srtp_encrypt", pkts, cap_short=(N - 2,))
+    same(res, "short cap")
+    assert res["fused"][0][3][N - 2] != 0
+    # two accepted batches back to back on one context, against one
+    # batch of both through the separate planner
+    a, b = batch(rng, seqs[:2100]), batch(rng, seqs[2100:])
+    ctx = P.Srtp(1, key)
+    outs = []
+    for part in (a, b):
+        ar, pos, end, cap, _ = to_arena(part)
+        outs.append(run_dev(torch, "srtp_encrypt", [ctx], ar, pos, end, cap,
+                            None))
+    st = states([ctx], [SSRC])
+    ctx.close()
+    ref = P.Srtp(1, key)
+    with P.tune(noplanfuse=1):
+        routs = []
+        for part in (a, b):
+            ar, pos, end, cap, _ = to_arena(part)
+            routs.append(run_dev(torch, "srtp_encrypt", [ref], ar, pos, end,
+                                 cap, None))
+    assert states([ref], [SSRC]) == st
+    ref.close()
+    for x, y in zip(outs, routs):
+        for u, v in zip(x, y):
+            assert (u == v).all()

@@ -310,7 +310,7 @@ def main():
                          "stream state)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (traffic, integer roofline) to "
-                         "attach; default profiles/r04_pmc.json")
+                         "attach; default profiles/r05_pmc.json")
     ap.add_argument("--room", type=int, default=None,
                     help="A/B: bytes of slack per packet slot (default 16: "
                          "1216-B slots for 1200-B packets; 80: 1280-B, "
@@ -777,7 +777,7 @@ def main():
     wl = "config%d%s%s%s" % (cfg_id, "_rtcp" if args.rtcp else "",
                              "_ssrc%d" % K if K > 1 else "",
                              "_room%d" % args.room if args.room else "")
-    pj = args.traffic_json or os.path.join(ROOT, "profiles", "r04_pmc.json")
+    pj = args.traffic_json or os.path.join(ROOT, "profiles", "r05_pmc.json")
     ent = None
     if dom and os.path.exists(pj):
         for e in json.load(open(pj)).get("entries", []):
@@ -797,8 +797,14 @@ def main():
                 if ent and ent.get("lds_frac") is not None else None,
                 "lds_floor_frac": round(ent["lds_floor_frac"], 4)
                 if ent and ent.get("lds_floor_frac") is not None else None,
-                "issue_frac": round(ent["issue_frac"], 4)
-                if ent and ent.get("issue_frac") is not None else None,
+                # the integer issue floor, co-issue corrected
+                # (scripts/pmc_r05.py): max(VALU, LDS) + c x min(VALU, LDS)
+                # of the launch, c measured (profiles/r04_ubench_coissue.txt)
+                "issue_frac": round(ent["issue_floor_frac"], 4)
+                if ent and ent.get("issue_floor_frac") is not None else None,
+                "coissue_c": ent.get("coissue_c") if ent else None,
+                "issue_sum_frac": round(ent["issue_sum_frac"], 4)
+                if ent and ent.get("issue_sum_frac") is not None else None,
                 "pmc_src": os.path.basename(pj) + ":" + wl if ent else None,
                 "kernel": dom["kernel"],
                 "dir": dom["dir"],

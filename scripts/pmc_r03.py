@@ -125,8 +125,9 @@ def main():
                 e["write_bytes"]
         s = {c: sum(v) / len(v) for c, v in sa.get(k, {}).items()}
         t = sorted(sdur[k])[len(sdur[k]) // 2] * 1e-9 if sdur.get(k) else 0
-        if t and "SQ_INSTS_VALU" in s and name in mix:
-            cl = mix[name]["classes"]
+        mname = name.replace("k_ctr_fused", "k_ctr_fast_any")
+        if t and "SQ_INSTS_VALU" in s and mname in mix:
+            cl = mix[mname]["classes"]
             nv = cl.get("fast", 0) + cl.get("slow", 0)
             floor = s["SQ_INSTS_VALU"] * 64 * (
                 cl.get("fast", 0) / nv / r_fast +

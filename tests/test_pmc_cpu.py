@@ -1,0 +1,52 @@
+"""The bench's integer roofline (profiles/r05_pmc.json, scripts/pmc_r05.py)
+is a floor: a kernel cannot run faster than the issue time of its measured
+VALU and LDS instructions, corrected for the partial co-issue measured on
+gfx950 (profiles/r04_ubench_coissue.txt).  issue_floor_frac = max(V, L) +
+c x min(V, L) of the launch must therefore stay at or below ~1; the plain
+sum V + L (round 4's issue_frac) did not (1.21 for the headline kernel)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def entries():
+    with open(os.path.join(ROOT, "profiles", "r05_pmc.json")) as f:
+        return [e for e in json.load(f)["entries"]
+                if e.get("issue_floor_frac") is not None]
+
+
+def test_coissue_floor_is_a_floor():
+    es = entries()
+    # the bench's dominant kernels of configs 2, 3 (RTP and SRTCP) and 4
+    names = {(e["kernel"], e["workload"]) for e in es}
+    for want in (("k_ctr_fused<10,1>", "config2"),
+                 ("k_gcmu<14,0>", "config3"),
+                 ("k_ctr_fast_mk<10,1>", "config4"),
+                 ("k_ctr_fast_rtcp<10,1>", "config2_rtcp")):
+        assert want in names, want
+    for e in es:
+        v, l, c = e["int_frac"], e["lds_floor_frac"], e["coissue_c"]
+        assert 0 < c < 1
+        assert abs(e["issue_floor_frac"] - (max(v, l) + c * min(v, l))) \
+            < 1e-4
+        assert e["issue_sum_frac"] >= e["issue_floor_frac"]
+        # the model's error: GCM protect runs ~5 % under it
+        assert e["issue_floor_frac"] <= 1.08, e
+        if e["workload"] in ("config2", "config4", "config2_rtcp"):
+            assert e["issue_floor_frac"] <= 1.0, e
+
+
+def test_coissue_factor_from_the_measured_rows():
+    import pmc_r05 as M
+    rows = M.coissue_rows(os.path.join(ROOT, "profiles",
+                                       "r04_ubench_coissue.txt"))
+    assert set(rows) == {4, 8}
+    # an all-b32 full-rate mix takes the 1:3 b32 full row exactly
+    assert M.coissue_c(rows, 4, {"fast": 10, "slow": 0, "lds": 5}) == \
+        rows[4][("b32", "full", "1:3")]
+    # an all-b128 half-rate mix the b128 half row
+    assert M.coissue_c(rows, 4, {"fast": 0, "slow": 10, "lds_b128": 5}) == \
+        rows[4][("b128", "half", None)]

@@ -964,6 +964,7 @@ struct prof_ev { hipEvent_t a, b; int slot; uint32_t jobs;
 		  const char *name; int nr, prot; int gw; int gslot; };
 static struct prof_ev *g_pev;
 static size_t g_npev, g_pev_cap;
+static uint32_t g_prof_gen;             /* + 1 per drain of g_pev */
 /* a launch behind a device plan does nothing when the plan was rejected
  * (its guard words, k_ctr_fast.h fast_class, k_ctr.h k_ctr_hmac_any, the
  * single-word guards): the kernel itself stores the words it saw into a
@@ -994,9 +995,10 @@ static void prof_drain_locked(void)
 		(void)hipEventSynchronize(g_pev[k].b);
 		(void)hipEventElapsedTime(&ms, g_pev[k].a, g_pev[k].b);
 		if (g_pev[k].gw) {
-			const volatile uint32_t *w = g_pguard +
-						     4 * g_pev[k].gslot;
-			const bool work = g_pev[k].gw == 4 ?
+			/* gw < 0: voided by the host (sgpu_prof_void) */
+			const volatile uint32_t *w = g_pev[k].gw < 0 ? NULL :
+				g_pguard + 4 * g_pev[k].gslot;
+			const bool work = !w ? false : g_pev[k].gw == 4 ?
 				(!w[0] || !w[1] || !w[2] || !w[3]) : !w[0];
 			if (!work) {
 				g_prof_voided++;
@@ -1020,6 +1022,7 @@ static void prof_drain_locked(void)
 		(void)hipEventDestroy(g_pev[k].b);
 	}
 	g_npev = 0;
+	g_prof_gen++;
 	g_ngslot = 0;
 }
 
@@ -1121,11 +1124,13 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 typedef void (*kfn_f)(const FArgs);
 kfn_f sgpu_pick_fused(int nr, int prot, int undo);      /* fused.hip */
 
-/* grid = n / block; jobs: the packets it processes (srtp_gpu_prof) */
+/* grid = n / block; jobs: the packets it processes (srtp_gpu_prof);
+ * *pid: the profiling record of the launch (sgpu_prof_void), or 0 */
 static int launch_fused(kfn_f f, const FArgs &a, uint32_t n, uint32_t jobs,
 			int slot, hipStream_t stream, uint32_t block,
-			const char *name, int nr, int prot)
+			const char *name, int nr, int prot, uint64_t *pid)
 {
+	*pid = 0;
 	struct prof_ev pe;
 	int prof = 0;
 	if (g_prof_on && slot >= 0) {
@@ -1156,11 +1161,26 @@ static int launch_fused(kfn_f f, const FArgs &a, uint32_t n, uint32_t jobs,
 				g_pev_cap = nc;
 			}
 		}
-		if (g_npev < g_pev_cap)
+		if (g_npev < g_pev_cap) {
+			*pid = (uint64_t)g_prof_gen << 32 | (g_npev + 1);
 			g_pev[g_npev++] = pe;
+		}
 		pthread_mutex_unlock(&g_prof_lock);
 	}
 	return e;
+}
+
+/* a fused launch whose plan the host found rejected did no work that
+ * counts (it was undone): leave it out of the kernel profile */
+extern "C" void sgpu_prof_void(uint64_t id)
+{
+	if (!id)
+		return;
+	pthread_mutex_lock(&g_prof_lock);
+	const uint32_t k = (uint32_t)id - 1;
+	if ((uint32_t)(id >> 32) == g_prof_gen && k < g_npev)
+		g_pev[k].gw = -1;
+	pthread_mutex_unlock(&g_prof_lock);
 }
 
 static int prof_slot(int mode, int nr, int shift, int prot)
@@ -1426,7 +1446,7 @@ extern "C" int sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
 	return launch_fused(sgpu_pick_fused(nr, prot, 0), fa, nwg * FZ_BLOCK,
 			    f->in.n, prof_slot(SGPU_MODE_CTR, nr, 3, prot),
 			    (hipStream_t)stream, FZ_BLOCK, "k_ctr_fused", nr,
-			    prot);
+			    prot, &f->prof_id);
 }
 
 extern "C" int sgpu_fused_undo(uint8_t *arena, uint64_t arena_size,

@@ -3300,14 +3300,24 @@ struct dcall {
 	double t[3];
 	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
 	struct sgpu_splan_in sin; /* several streams: the plan input */
-	int devfold;            /* many sessions: fold queued on the device */
+	int devfold;            /* fold queued on the device */
 	int radix;              /* ... grouped by the radix sort */
+	int fused;              /* single stream planned inside the crypto
+				   launch (fz_issue / fz_finish) */
+	struct sgpu_fused fz;   /* ... its launch */
 };
 
 /* single-stream RTP batch planned and processed on the device: the
  * launches (no host synchronisation) */
+static int fz_issue(struct dcall *k, int sync);
+static int fz_finish(struct dcall *k, int sync);
+
 static int dev_planned_issue(struct dcall *k)
 {
+	if (k->sessv[0]->rtp.mode == SGPU_MODE_CTR && !g_env.noplanfuse) {
+		k->fused = 1;
+		return fz_issue(k, 0);
+	}
 	const int prot = k->op == OP_RTP_ENC;
 	struct srtp *s = k->sessv[0];
 	struct srtp_batch_dev *d = &k->d;
@@ -3416,6 +3426,8 @@ static int dev_planned_issue(struct dcall *k)
  * chained call before (nothing modified) */
 static int dev_planned_finish(struct dcall *k)
 {
+	if (k->fused)
+		return fz_finish(k, 0);
 	const int prot = k->op == OP_RTP_ENC;
 	struct srtp *s = k->sessv[0];
 	struct srtp_batch_dev *d = &k->d;
@@ -3496,41 +3508,44 @@ static int dev_planned_finish(struct dcall *k)
 /* ---- one stream, planned inside the crypto launch (k_ctr_fused.h) ----- */
 
 #define FZ_HEAD 64u             /* ticket word, padded */
-#define FZ_PO_SZ ((sizeof(struct sgpu_plan_out) + 63u) & ~(size_t)63)
 
 /*
- * Synchronous single-stream AES-CM batch: one launch parses, plans and
- * encrypts / decrypts (srtpgpu.h struct sgpu_fused); with no forged packet
- * nothing else runs on the device.  Forged packets: their ciphertext back
- * (k_ctr_refix_list) and the device verdict fold (sgpu_fold_rtp), launched
- * after the synchronisation showed a miss.  A rejected plan or a fold the
- * device cannot settle: every processed packet undone (sgpu_fused_undo),
- * the ends restored, and -1 (*pfail: the plan's SPF_* bits, 0 for a fold)
- * -- the caller plans on the host, as for dev_planned.
+ * Single-stream AES-CM batch planned inside its crypto launch
+ * (srtpgpu.h struct sgpu_fused): one launch parses, plans and encrypts /
+ * decrypts.  Synchronous calls (dev_fused): with no forged packet nothing
+ * else runs on the device; forged packets get their ciphertext back
+ * (k_ctr_refix_list) and the device verdict fold (sgpu_fold_rtp) after the
+ * synchronisation showed a miss.  Asynchronous calls (dev_planned_issue):
+ * the refix and fold are queued behind the launch (each exits at once
+ * without a miss) with the chained gate word, so no host round trip is
+ * needed.  A rejected plan or a fold the device cannot settle: every
+ * processed packet undone (sgpu_fused_undo), the ends restored, and -1
+ * (k->pfail: the plan's SPF_* bits, 0 for a fold) -- the caller plans on
+ * the host, as for the separate device planner.
+ *
+ * w->fz: ticket | (plan out, fold out) x 2 | look-back words
  */
-static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
-		     uint32_t *pfail)
+#define FZ_FO_OFF ((sizeof(struct sgpu_plan_out) + 63u) & ~(size_t)63)
+#define FZ_SLOT (FZ_FO_OFF + 64u)
+
+static int fz_issue(struct dcall *k, int sync)
 {
-	const int prot = op == OP_RTP_ENC;
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
 	const struct comp *c0 = &s->rtp;
 	const size_t n = d->n;
 	const uint32_t T = c0->tag_len;
 	const uint32_t need = prot ? (T > 4 ? T : 4u) : 0u;
 	const uint32_t B = sgpu_fused_block();
 	const uint32_t nblk = (uint32_t)((n + B - 1) / B);
-	const unsigned ns0 = s->nstreams;
-	struct ws *w = ws_get();
-	struct sgpu_fused F;
-	struct sgpu_plan_out *po;
-	struct srtp_stream old;
+	struct ws *w = k->w;
+	struct sgpu_fused *F = &k->fz;
 	void *stream = d->stream;
 	uint8_t *fz;
 	size_t poff;
 	int err;
 
-	*pfail = 0;
-	if (!w)
-		return ENOMEM;
 	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
 	if (!err)
 		err = pool_reserve(w, &w->dsc, n * 8);
@@ -3543,7 +3558,7 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 	if (!err)
 		err = pool_reserve(w, &w->pl, 64 + (n / 256 + 4) * 20);
 	if (!err)
-		err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_PO_SZ +
+		err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_SLOT +
 				   (size_t)nblk * 8);
 	if (err)
 		return err;
@@ -3559,52 +3574,108 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 		w->fz_tbase = 0;
 		w->fz_par = 0;
 	}
-	poff = FZ_HEAD + (size_t)w->fz_par * FZ_PO_SZ;
+	poff = FZ_HEAD + (size_t)w->fz_par * FZ_SLOT;
+	k->foff = poff;
 
-	memset(&F, 0, sizeof(F));
-	plan_in(&F.in, s, (uint32_t)n, prot, T, need);
-	F.in.zeroed = 1;
-	F.pos = d->pos;
-	F.end = d->end;
-	F.cap = d->cap;
-	F.err = d->err;
-	F.es = (uint32_t *)w->es.d;
-	F.hdr = (struct sgpu_hdr *)w->hd.d;
-	F.desc = (uint64_t *)w->dsc.d;
-	F.save = (uint32_t *)(w->vs.d + 64);
-	F.verdict = w->vs.d + 64 + n * 4;
-	F.flist = (uint32_t *)(w->vs.d + ((64 + n * 5 + 3) & ~(size_t)3));
-	F.out = (struct sgpu_plan_out *)(fz + poff);
-	F.out_next = (struct sgpu_plan_out *)(fz + FZ_HEAD +
-					      (size_t)(w->fz_par ^ 1) * FZ_PO_SZ);
-	F.cm_out = (uint32_t *)w->cm.d;
-	F.agg = (unsigned long long *)(fz + FZ_HEAD + 2 * FZ_PO_SZ);
-	F.ticket = (uint32_t *)fz;
-	F.tbase = w->fz_tbase;
-	F.epoch = w->fz_epoch;
-	F.comp = c0->dev;
-	F.delta = prot ? (int32_t)T : -(int32_t)T;
-	if (prot) {
-		F.verdict = NULL;
-		F.save = NULL;
-		F.flist = NULL;
+	memset(F, 0, sizeof(*F));
+	plan_in(&F->in, s, (uint32_t)n, prot, T, need);
+	F->in.zeroed = 1;
+	F->in.pred = k->pred;   /* the chained call before: its gate word */
+	F->pos = d->pos;
+	F->end = d->end;
+	F->cap = d->cap;
+	F->err = d->err;
+	F->es = (uint32_t *)w->es.d;
+	F->hdr = (struct sgpu_hdr *)w->hd.d;
+	F->desc = (uint64_t *)w->dsc.d;
+	if (!prot) {
+		F->save = (uint32_t *)(w->vs.d + 64);
+		F->verdict = w->vs.d + 64 + n * 4;
+		F->flist = (uint32_t *)(w->vs.d +
+					((64 + n * 5 + 3) & ~(size_t)3));
 	}
-	err = sgpu_run_fused(d->arena, d->arena_size, &F, (int)c0->nr, stream);
-	if (!err) {
-		w->fz_tbase += F.ntickets;
-		w->fz_epoch++;
-		w->fz_par ^= 1;
-		err = sgpu_memcpy_d2h(w->fz.h + poff, F.out, sizeof(*po), stream);
-	}
-	if (!err)
-		err = sgpu_stream_sync(stream);
+	F->out = (struct sgpu_plan_out *)(fz + poff);
+	F->out_next = (struct sgpu_plan_out *)(fz + FZ_HEAD +
+					       (size_t)(w->fz_par ^ 1) * FZ_SLOT);
+	F->cm_out = (uint32_t *)w->cm.d;
+	F->agg = (unsigned long long *)(fz + FZ_HEAD + 2 * FZ_SLOT);
+	F->ticket = (uint32_t *)fz;
+	F->tbase = w->fz_tbase;
+	F->epoch = w->fz_epoch;
+	F->comp = c0->dev;
+	F->delta = prot ? (int32_t)T : -(int32_t)T;
+	err = sgpu_run_fused(d->arena, d->arena_size, F, (int)c0->nr, stream);
 	if (err) {
 		w->fz_d = NULL;         /* counters unknown: from zero next time */
 		return err;
 	}
-	po = (struct sgpu_plan_out *)(w->fz.h + poff);
+	w->fz_tbase += F->ntickets;
+	w->fz_epoch++;
+	w->fz_par ^= 1;
+	k->devfold = !sync && !prot && !g_env.nodevfold;
+	if (!sync) {
+		/* queued behind the launch: forged packets' ciphertext and the
+		 * verdict fold (unprotect), the gate word of the next chained
+		 * call (set if this call must be completed on the host) */
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(fz + poff + FZ_FO_OFF);
+		uint32_t *fscr = (uint32_t *)(w->pl.d + 64);
+		if (k->devfold) {
+			err = sgpu_fused_refix(d->arena, d->arena_size, F,
+					       (int)c0->nr, stream);
+			if (!err)
+				err = sgpu_fold_rtp(1, &F->out->nfail, &F->in,
+						    F->hdr, F->desc, F->verdict,
+						    F->es, d->pos, d->end, d->err,
+						    0, fscr, fo_d, stream);
+		}
+		if (!err && k->gate)
+			err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0,
+					       0, &F->out->nfail, k->gate, NULL,
+					       k->devfold ? &fo_d->fail : NULL,
+					       stream);
+		if (!err && k->devfold)
+			err = sgpu_fold_rtp(2, &F->out->nfail, &F->in, F->hdr,
+					    F->desc, F->verdict, F->es, d->pos,
+					    d->end, d->err, 0, fscr, fo_d,
+					    stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
+				      k->devfold ? FZ_SLOT
+						 : sizeof(struct sgpu_plan_out),
+				      stream);
+	return err;
+}
+
+/* ... after its launches completed: 0 / errno, -1 not plannable or a
+ * forged packet the host must fold (nothing modified), -2 gated by the
+ * chained call before (nothing modified) */
+static int fz_finish(struct dcall *k, int sync)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	const struct comp *c0 = &s->rtp;
+	const size_t n = d->n;
+	const unsigned ns0 = s->nstreams;
+	struct ws *w = k->w;
+	struct sgpu_fused *F = &k->fz;
+	const size_t poff = k->foff;
+	const struct sgpu_plan_out *po =
+		(const struct sgpu_plan_out *)(w->fz.h + poff);
+	const struct sgpu_fold_out *fo =
+		(const struct sgpu_fold_out *)(w->fz.h + poff + FZ_FO_OFF);
+	void *stream = d->stream;
+	struct srtp_stream old;
+	int err;
+
+	k->pfail = po->fail;
 	if (po->fail) {
-		*pfail = po->fail;
+		/* no work that counts: nothing (gated) or undone */
+		sgpu_prof_void(F->prof_id);
+		if (po->fail & SPF_PRED)
+			return -2;      /* every workgroup did nothing */
 		if (po->fail & SPF_BAD)
 			w->fz_d = NULL; /* ticket / look-back state from zero */
 		if ((po->fail & SPF_SSRC) && !ns0)
@@ -3617,35 +3688,35 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 	if (!po->nfail)
 		return 0;
 	count(&g_cnt_misses, po->nfail);
-	if (!g_env.nodevfold) {
+	if (sync && !g_env.nodevfold) {
 		/* forged packets: ciphertext back, verdicts folded on the
 		 * device; its outcome comes back in one copy */
-		struct sgpu_fold_out *fo_d = (struct sgpu_fold_out *)w->pl.d;
-		const struct sgpu_fold_out *fo = (const struct sgpu_fold_out *)
-						 w->pl.h;
-		err = sgpu_fused_refix(d->arena, d->arena_size, &F,
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(w->fz.d + poff + FZ_FO_OFF);
+		err = sgpu_fused_refix(d->arena, d->arena_size, F,
 				       (int)c0->nr, stream);
 		if (!err)
-			err = sgpu_fold_rtp(0, &F.out->nfail, &F.in, F.hdr,
-					    F.desc, F.verdict, F.es, d->pos,
+			err = sgpu_fold_rtp(0, &F->out->nfail, &F->in, F->hdr,
+					    F->desc, F->verdict, F->es, d->pos,
 					    d->end, d->err, 0,
 					    (uint32_t *)(w->pl.d + 64), fo_d,
 					    stream);
 		if (!err)
-			err = sgpu_memcpy_d2h(w->pl.h, fo_d, sizeof(*fo),
-					      stream);
+			err = sgpu_memcpy_d2h(w->fz.h + poff + FZ_FO_OFF, fo_d,
+					      sizeof(*fo), stream);
 		if (!err)
 			err = sgpu_stream_sync(stream);
 		if (err)
 			return err;
-		if (!fo->fail) {
-			struct srtp_stream *st = &s->streams[0];
-			st->s_l = (uint16_t)fo->s_l;
-			st->replay_rtp.lix = fo->lix;
-			st->replay_rtp.bitmap = fo->bitmap;
-			count(&g_cnt_devfolds, 1);
-			return 0;
-		}
+		k->devfold = 1;
+	}
+	if (k->devfold && !fo->fail) {
+		struct srtp_stream *st = &s->streams[0];
+		st->s_l = (uint16_t)fo->s_l;
+		st->replay_rtp.lix = fo->lix;
+		st->replay_rtp.bitmap = fo->bitmap;
+		count(&g_cnt_devfolds, 1);
+		return 0;
 	}
 	/* the fold cannot be settled on the device (or nodevfold): undo --
 	 * forged packets still decrypted are re-encrypted with the rest --
@@ -3653,17 +3724,44 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 	count(&g_cnt_folds, 1);
 	plan_unapply(s, ns0, &old);
  undo:
-	if (po->hl0 != 0xffffffffu && !(po->fail & SPF_PRED)) {
-		F.shift = (po->hl0 >> 2) & 3u;
-		err = sgpu_fused_undo(d->arena, d->arena_size, &F, (int)c0->nr,
+	if (po->hl0 != 0xffffffffu) {
+		F->shift = (po->hl0 >> 2) & 3u;
+		err = sgpu_fused_undo(d->arena, d->arena_size, F, (int)c0->nr,
 				      prot, stream);
 		if (err)
 			return err;
 	}
-	err = sgpu_memcpy_d2d(d->end, F.es, n * 4, stream);
+	err = sgpu_memcpy_d2d(d->end, F->es, n * 4, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	return err ? err : -1;
+}
+
+/* synchronous (dev_planned): -1 not plannable (nothing modified;
+ * *pfail: why, 0 for a forged packet the host must fold), else 0 /
+ * errno */
+static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
+		     uint32_t *pfail)
+{
+	struct dcall k;
+	int err;
+	memset(&k, 0, sizeof(k));
+	k.op = op;
+	k.sessv = &s;
+	k.nsess = 1;
+	k.d = *d;
+	k.w = ws_get();
+	*pfail = 0;
+	if (!k.w)
+		return ENOMEM;
+	err = fz_issue(&k, 1);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	if (err)
+		return err;
+	err = fz_finish(&k, 1);
+	*pfail = k.pfail;
+	return err;
 }
 
 /* synchronous: -1 not plannable (nothing modified; *pfail: why, 0 for a

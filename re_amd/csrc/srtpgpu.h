@@ -325,6 +325,7 @@ struct sgpu_fused {
 	uint32_t shift;                 /* undo: the batch's header class */
 	uint32_t ntickets;              /* (out) tickets the launch takes (its
 					   workgroups) -- the next tbase */
+	uint64_t prof_id;               /* (out) its srtp_gpu_prof record */
 };
 unsigned sgpu_fused_block(void);        /* packets per workgroup */
 int   sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
@@ -644,6 +645,9 @@ void  sgpu_prof_enable(int on);
 /* launches behind a rejected device plan (they did nothing), not counted
  * by sgpu_prof_read */
 uint64_t sgpu_prof_voided(void);
+/* ... and a fused launch the host found rejected (struct sgpu_fused
+ * prof_id) */
+void  sgpu_prof_void(uint64_t id);
 /* RTCP compound decode (rtcp_walk.hip, include/re_rtcp_batch.h) */
 struct rtcp_desc;
 struct rtcp_item;

@@ -315,6 +315,13 @@ def main():
                     help="A/B: bytes of slack per packet slot (default 16: "
                          "1216-B slots for 1200-B packets; 80: 1280-B, "
                          "128-B aligned slots)")
+    ap.add_argument("--libre-helper", action="store_true",
+                    help="one libre re_main thread receiving config-2 SRTP "
+                         "over loopback (oracle/libre_helper_bench.c): no "
+                         "helper / the reference srtp_decrypt per datagram "
+                         "/ the batched GPU helper at several batch sizes; "
+                         "delivered rate, added latency, loop CPU per "
+                         "packet; reported in DESIGN.md, not the headline")
     ap.add_argument("--percall", action="store_true",
                     help="the unchanged per-packet API: srtp_encrypt + "
                          "srtp_decrypt of one 1200-B mbuf per call "
@@ -350,6 +357,8 @@ def main():
                        int(os.environ.get("RANK", "0")))
     if args.percall:
         return percall_bench(args)
+    if args.libre_helper:
+        return libre_helper_bench(args)
     if args.rtcp_report:
         return rtcp_report_bench(args)
 
@@ -979,6 +988,47 @@ def udp_bench(args):
     for pr in pairs:
         pr["st"].close()
         pr["sr"].close()
+
+
+def libre_helper_bench(args):
+    """a single-threaded libre application (re_main,
+    libre's udp_read per datagram) receiving config-2 SRTP over loopback,
+    its transform on libre's UDP helper chain (/root/reference/src/udp/
+    udp.c:830-928).  oracle/_ref/helper_bench_{ref,gpu} (built by
+    oracle/Makefile, libre's loop from oracle/_ref/libre_net.so): flat out
+    and paced runs, 200K datagrams each"""
+    refx = os.path.join(ROOT, "oracle", "_ref", "helper_bench_ref")
+    gpux = os.path.join(ROOT, "oracle", "_ref", "helper_bench_gpu")
+    n = 200000
+    runs = [(refx, "none", 0, 0, 0), (refx, "none", 600000, 0, 0)]
+    for rate in (0, 100000, 300000, 400000):
+        runs.append((refx, "ref", rate, 0, 0))
+    for rate, batch in ((0, 1024), (0, 256), (100000, 64), (100000, 256),
+                        (200000, 64), (200000, 256), (400000, 256),
+                        (400000, 1024), (500000, 1024), (600000, 1024)):
+        runs.append((gpux, "gpu", rate, batch, 1))
+    res = []
+    for exe, mode, rate, batch, flush in runs:
+        cmd = [exe, mode, str(n), str(rate)] + \
+            ([str(batch), str(flush)] if mode == "gpu" else [])
+        out = subprocess.run(cmd, capture_output=True, text=True,
+                             timeout=120, check=True, cwd=ROOT).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+        print("bench.py: %s rate %s batch %s: %s pkt/s, lost %s, p50 %s us"
+              % (mode, rate, batch, r["pkt_s"], r["lost"],
+                 r["lat_us"]["p50"]), file=sys.stderr, flush=True)
+        res.append(r)
+    best = max((r for r in res if r["mode"] == "gpu"),
+               key=lambda r: r["pkt_s"] * (r["lost"] == 0))
+    line = {"metric": "SRTP unprotect on libre's UDP helper chain, one "
+                      "re_main thread, 1200-B RTP over loopback",
+            "value": best["pkt_s"], "unit": "pkt/s",
+            "higher_is_better": True, "n_gpus": 1, "data": "synthetic",
+            "dtype": "u8", "runs": res,
+            "config": {"workload": "config2 datagrams, libre re_main + "
+                                   "udp_read, srtp_udp_helper_alloc"}}
+    print(json.dumps(line))
+    return 0
 
 
 def percall_bench(args):

@@ -44,6 +44,7 @@ struct pc_req {
 static pthread_mutex_t pc_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct pc_req *pc_head, *pc_tail;
 static int pc_running;
+static int pc_nq;               /* requests queued (under pc_lock) */
 
 /* the owner learns v; a futex wake only if it went to sleep (PC_SLEEP) */
 static void pc_wake(int *state, int v)
@@ -155,6 +156,9 @@ static void pc_run_op(struct pc_req *list, int op)
 /* runners 1..4 at 64 threads: 230, 278, 306, 326 K pairs/s
  * (profiles/r04_percall_runners.txt) */
 enum { PC_SLOTS = 4, PC_RUNNERS = 4 };
+/* a new runner's hold (srtp_gpu_tune pchold, us) ends early at this many
+ * requests queued */
+enum { PC_HOLD_N = 32 };
 
 static struct pc_slot {
 	struct ws *ws;
@@ -421,7 +425,7 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 {
 	struct pc_req req;
 	struct pc_slot *sl;
-	int e = 0, err, run, slot = 0, nrun;
+	int e = 0, err, run, busy, slot = 0, nrun;
 
 	if (!srtp || !mb)
 		return EINVAL;
@@ -444,7 +448,9 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 	else
 		pc_head = &req;
 	pc_tail = &req;
+	pc_nq++;
 	run = pc_running < nrun;
+	busy = pc_running > 0;
 	if (run) {
 		/* a free slot: run the queue now (taken here, in the same
 		 * critical section, so no hand-off can take this request) */
@@ -453,8 +459,28 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 		pc_slot_used |= 1u << slot;
 		req.list = pc_head;
 		pc_head = pc_tail = NULL;
+		pc_nq = 0;
 	}
 	pthread_mutex_unlock(&pc_lock);
+	if (run && busy && g_env.pchold > 0) {
+		/* other runners are in flight, so other callers are active:
+		 * hold the new launch a few us (or until PC_HOLD_N more
+		 * requests queued) and take what arrived -- a launch of 10
+		 * packets costs about what one of 30 does (the small kernel runs
+		 * one packet per workgroup) */
+		const uint64_t until = mono_ns() + (uint64_t)g_env.pchold * 1000u;
+		struct pc_req *last = req.list;
+		while (mono_ns() < until &&
+		       __atomic_load_n(&pc_nq, __ATOMIC_RELAXED) < PC_HOLD_N)
+			__builtin_ia32_pause();
+		while (last->next)
+			last = last->next;
+		pthread_mutex_lock(&pc_lock);
+		last->next = pc_head;
+		pc_head = pc_tail = NULL;
+		pc_nq = 0;
+		pthread_mutex_unlock(&pc_lock);
+	}
 	if (!run && pc_wait(&req.state) == PC_DONE)
 		return req.err;
 	/* the runner (PC_RUN: slot and queue handed over): its queue on the
@@ -477,6 +503,7 @@ static int one(int op, struct srtp *srtp, struct mbuf *mb)
 			next_runner->slot = slot;
 			next_runner->list = pc_head;
 			pc_head = pc_tail = NULL;
+			pc_nq = 0;
 		}
 		else {
 			pc_running--;

@@ -241,6 +241,8 @@ int srtp_gpu_tune(const char *name, long value)
 		__atomic_store_n(&g_fresh_multi, value > 0, __ATOMIC_RELAXED);
 	else if (!strcmp(name, "pcrunners"))
 		g_env.pcrunners = value > 0 ? value : 0;
+	else if (!strcmp(name, "pchold"))
+		g_env.pchold = value > 0 ? value : 0;
 	else if (!strcmp(name, "pcspin"))
 		g_env.pcspin = value > 0 ? value : 0;
 	else if (!strcmp(name, "trace"))

@@ -100,6 +100,9 @@ struct srtp_env {
 	long pcrunners;         /* srtp_gpu_tune pcrunners: per-packet runners
 				   at once (default PC_RUNNERS, at most
 				   PC_SLOTS) */
+	long pchold;            /* srtp_gpu_tune pchold: us a new per-packet
+				   runner holds its launch while other
+				   runners are in flight (percall.c) */
 	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
 				   per-packet caller spins before it sleeps
 				   (default 1000) */

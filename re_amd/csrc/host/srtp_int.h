@@ -1,8 +1,10 @@
 /*
  * srtp_int.h -- what the host translation units of the library share
- * (srtp.c: sessions, planning engine and batch paths; percall.c: the
- * per-packet calls' shared launches; rxfold.c: the cross-rank replay
- * fold).  Internal: nothing here is exported (exports.map).
+ * (srtp.c: sessions, the planning engine and the mbuf front-end;
+ * batch_host.c: host-planned device batches; batch_dev.c: device-planned
+ * batches; batch_async.c: entry points and asynchronous tickets;
+ * percall.c: the per-packet calls' shared launches; rxfold.c: the
+ * cross-rank replay fold).  Internal: nothing here is exported (exports.map).
  */
 #ifndef RE_AMD_SRTP_INT_H
 #define RE_AMD_SRTP_INT_H
@@ -229,8 +231,21 @@ struct mbc {
 };
 
 
+/* where a session's stream-0 RTP state lives (struct srtp dres; srtp.c) */
+enum { DRES_HOST = 0, DRES_BOTH = 1, DRES_DEV = 2, DRES_LISTED = 3 };
+/* round_launch: the jobs to run, or the undo jobs of dirty records */
+enum { SEL_RUN = 0, SEL_UNDO = 1 };
+
 /* diagnostics counters (srtp_gpu_counter, srtp.c) */
 extern uint64_t g_cnt_pcbatch, g_cnt_pcpkts, g_cnt_pcfused, g_cnt_rxw_redo;
+extern uint64_t g_cnt_misses, g_cnt_folds, g_cnt_rejects, g_cnt_devfolds;
+extern uint64_t g_cnt_splans, g_cnt_fused, g_cnt_gated;
+extern int g_fresh_multi;       /* srtp.c: the last first batch of a session
+				   showed several SSRCs (see there) */
+extern __thread struct tk_owner *t_own; /* srtp.c: this thread's async
+					   completion counter */
+extern __thread int t_noplan;   /* batch_host.c: a rejected device plan's
+				   fallback runs without device planners */
 extern uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
 extern uint64_t g_ns_fused_prep, g_ns_fused_post;
 
@@ -280,5 +295,88 @@ int run_mbufs_(int op, struct srtp **sessv, size_t nsess,
 	       const uint32_t *sidx, struct mbuf **mbv, int *errv, size_t n);
 int run_mbufs(int op, struct srtp *srtp, struct mbuf **mbv, int *errv,
 	      size_t n);
+
+
+/* one device-planned batch between its launches and its completion
+ * (the synchronous calls and the asynchronous tickets share it) */
+struct dcall {
+	int op;
+	struct srtp **sessv;
+	size_t nsess;
+	struct srtp_batch_dev d;
+	struct ws *w;
+	const uint32_t *pred;   /* gate word of the pending call before */
+	uint32_t *gate;         /* this call's gate word (chained) or NULL */
+	struct sgpu_plan_in in; /* single stream: the plan input */
+	size_t foff;            /* ... fold area in w->pl */
+	uint32_t nup;           /* many sessions: states uploaded */
+	uint64_t pend, done;    /* async: sequence numbers (mpg) */
+	double t[3];
+	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
+	struct sgpu_splan_in sin; /* several streams: the plan input */
+	int devfold;            /* fold queued on the device */
+	int radix;              /* ... grouped by the radix sort */
+	int fused;              /* single stream planned inside the crypto
+				   launch (fz_issue / fz_finish) */
+	struct sgpu_fused fz;   /* ... its launch */
+};
+
+/* srtp.c */
+struct tk_owner *tk_me(void);
+void env_init(void);
+int stream_get(struct srtp_stream **sp, struct srtp *s, uint32_t ssrc);
+uint32_t buf_grow(uint32_t size, uint32_t need);
+int cap_short(const struct pinfo *pi, const struct comp *c, int rtcp);
+void snap_take(struct engine *E);
+void snap_restore(struct engine *E);
+size_t plan_all(struct engine *E);
+int engine_init(struct engine *E, int op, size_t n,
+		       struct srtp **sessv, size_t nsess, const uint32_t *sidx);
+void engine_free(struct engine *E);
+int rec_dirty(const struct rec *r);
+int round_launch(struct ws *w, struct engine *E, int sel,
+			uint8_t *arena_d, uint64_t asz, const uint32_t *joff,
+			int prot, uint32_t *pm, void *stream);
+int round_fetch(struct ws *w, uint32_t m, void *stream);
+void round_collect(struct ws *w, struct engine *E, uint32_t m);
+
+/* batch_host.c */
+double now_ms(void);
+struct replay plan_replay(const struct replay *r0,
+				 const uint64_t *tail_ix, size_t n);
+void plan_in(struct sgpu_plan_in *in, const struct srtp *s,
+		    uint32_t n, int prot, uint32_t T, uint32_t need);
+void plan_apply(struct srtp *s, const struct sgpu_plan_out *po,
+		       int prot, size_t n, struct srtp_stream *old);
+void plan_unapply(struct srtp *s, unsigned nstreams0,
+			 const struct srtp_stream *old);
+int mplan_gather_res(struct srtp **sessv, size_t nsess,
+			    struct sgpu_sstate *st, uint32_t *cm,
+			    uint8_t *need, uint32_t *nup, uint64_t pend,
+			    uint64_t done);
+int run_classes(uint8_t *arena, uint64_t asz, struct sgpu_compact C,
+		       const struct comp *c0, struct sgpu_plan_out *po_d,
+		       int prot, void *stream);
+int run_batch(int op, struct srtp **sessv, size_t nsess,
+		     struct srtp_batch *b);
+
+/* batch_dev.c */
+int dev_planned_issue(struct dcall *k);
+int dev_planned_finish(struct dcall *k);
+int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
+		       uint32_t *pfail);
+int dev_splanned_issue(struct dcall *k);
+int dev_splanned_finish(struct dcall *k);
+int dev_splanned(int op, struct srtp *s, struct srtp_batch_dev *d);
+int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d);
+int dev_mplanned_issue(struct dcall *k);
+int dev_mplanned_finish(struct dcall *k);
+int dev_mplanned_(int op, struct srtp **sessv, size_t nsess,
+			 struct srtp_batch_dev *d, int radix, uint32_t *pfail);
+int dev_mplanned(int op, struct srtp **sessv, size_t nsess,
+			struct srtp_batch_dev *d);
+
+/* batch_async.c */
+void tk_drain(void);
 
 #endif

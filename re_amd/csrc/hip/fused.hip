@@ -18,3 +18,15 @@ kfn_f sgpu_pick_fused(int nr, int prot, int undo)
 	return nr == 10 ? (prot ? k_ctr_fused<10, true> : k_ctr_fused<10, false>)
 			: (prot ? k_ctr_fused<14, true> : k_ctr_fused<14, false>);
 }
+
+#ifdef FZ_WTIME
+/* the diagnostic stamps of the last launches (scripts/fz_wtime.py) */
+extern "C" __attribute__((visibility("default"))) int
+sgpu_fz_wtime(uint64_t *out, size_t n)
+{
+	if (n > 20u * FZ_WTIME_MAX)
+		n = 20u * FZ_WTIME_MAX;
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fzw), n * 8, 0,
+				   hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

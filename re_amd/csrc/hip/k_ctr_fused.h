@@ -335,16 +335,35 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	return (int)((hl0 >> 2) & 3u);
 }
 
+#ifdef FZ_WTIME
+#define FZ_WTIME_MAX 4096u
+/* per ticket: [0] start (thread 0), [1] CU id, [2 + w] wave w's end */
+__device__ uint64_t g_fzw[20u * FZ_WTIME_MAX];
+#endif
+
 template <int NR, bool PROT>
 __global__ void
 __attribute__((amdgpu_flat_work_group_size(1, CTRF_BLK(PROT))))
 __attribute__((amdgpu_waves_per_eu(CTRF_BLK(PROT) / 256, 8)))
 k_ctr_fused(const FArgs fa)
 {
+#ifdef FZ_WTIME
+	uint64_t t_start = 0;
+	if (threadIdx.x == 0)
+		t_start = __builtin_amdgcn_s_memrealtime();
+#endif
 	__shared__ __attribute__((aligned(16))) uint8_t smem[TT4_BYTES];
 	__shared__ FShared S;
 	FastPkt f;
 	const int cls = fz_plan<PROT>(fa, S, smem, f);
+#ifdef FZ_WTIME
+	if (threadIdx.x == 0 && S.t < FZ_WTIME_MAX) {
+		uint32_t hw;
+		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+		g_fzw[20u * S.t] = t_start;
+		g_fzw[20u * S.t + 1u] = hw;
+	}
+#endif
 	if (cls < 0)
 		return;
 	const uint32_t ci = fa.p.comp;
@@ -357,6 +376,16 @@ k_ctr_fused(const FArgs fa)
 	}
 	/* (no stamp after the crypto: a value kept live across its body
 	 * costs the SGPRs that hold the round keys -- it spilled ~90 VGPRs) */
+#ifdef FZ_WTIME
+	/* A/B diagnostic build only (scripts/fz_wtime.py): each wave's end
+	 * time, the ticket re-read from LDS, not kept live */
+	if ((threadIdx.x & 63u) == 0) {
+		const uint32_t t = S.t;
+		if (t < FZ_WTIME_MAX)
+			g_fzw[20u * t + 2u + threadIdx.x / 64u] =
+				__builtin_amdgcn_s_memrealtime();
+	}
+#endif
 }
 
 /*

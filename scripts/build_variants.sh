@@ -16,8 +16,10 @@ while [ $# -ge 2 ]; do
   $HIPCC $FL $defs -c csrc/hip/plan_multi.hip -o /tmp/variants/plan_multi_$name.o &
   $HIPCC $FL $defs -c csrc/hip/fused.hip -o /tmp/variants/fused_$name.o &
   wait
-  objs="build/srtp.o build/percall.o build/rxfold.o build/pool.o build/udp.o build/keying.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/ctr14a.o build/plan_streams.o build/dtls_prf.o build/rtcp_walk.o build/rtcp_encode.o build/small.o"
-  $HIPCC -shared -fPIC --offload-arch=gfx950 -o lib/variants/$name.so $objs -Wl,--version-script=build/exports.map \
+  objs="build/srtp.o build/batch_host.o build/batch_dev.o build/batch_async.o build/percall.o build/rxfold.o build/pool.o build/udp.o build/keying.o build/mem.o build/mbuf.o build/srtp_kernels.o build/ctr14.o build/ctr14a.o build/plan_streams.o build/dtls_prf.o build/rtcp_walk.o build/rtcp_encode.o build/small.o"
+  # NOMAP=1: every symbol exported (diagnostic variants' dump functions)
+  map="-Wl,--version-script=build/exports.map"; [ -n "$NOMAP" ] && map=
+  $HIPCC -shared -fPIC --offload-arch=gfx950 -o lib/variants/$name.so $objs $map \
     /tmp/variants/ctr10_$name.o /tmp/variants/ctr10a_$name.o /tmp/variants/gcm_$name.o /tmp/variants/plan_multi_$name.o \
     /tmp/variants/fused_$name.o -lpthread
   echo "built lib/variants/$name.so ($defs)"

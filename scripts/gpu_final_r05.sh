@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-5 final set on the final build: the GPU suite, smoke, the driver's
+# default bench command, then every config's bench line at the ramped
+# clocks (--steps 20 --warmup 5) and the per-packet API.  Into
+# gpurun_out/final_r05/; every GPU step under its own time limit, the first
+# failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/final_r05
+mkdir -p $O
+cd $R
+if [ -z "$NOTESTS" ]; then
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || exit $?
+  timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+fi
+timeout -k 10 300 python3 bench.py --gpus 1 > $O/default.json 2> $O/default.err || exit $?
+S="--steps 20 --warmup 5"
+IFS=';' read -ra BS <<< "${BENCHES:-c2=--config 2 $S;c3=--config 3 $S;c4=--config 4 $S;c2_rtcp=--config 2 --rtcp $S;c3_rtcp=--config 3 --rtcp $S;c1=--config 1 $S --no-cpu-baseline;percall=--percall;percall_gcm=--percall --percall-suite 4 --no-cpu-baseline}"
+for nb in "${BS[@]}"; do
+  n=${nb%%=*}; a=${nb#*=}
+  timeout -k 10 300 python3 bench.py $a > $O/$n.json 2> $O/$n.err || exit $?
+done
+echo done > $O/done

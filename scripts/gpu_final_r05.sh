@@ -15,7 +15,7 @@ if [ -z "$NOTESTS" ]; then
 fi
 timeout -k 10 300 python3 bench.py --gpus 1 > $O/default.json 2> $O/default.err || exit $?
 S="--steps 20 --warmup 5"
-IFS=';' read -ra BS <<< "${BENCHES:-c2=--config 2 $S;c3=--config 3 $S;c4=--config 4 $S;c2_rtcp=--config 2 --rtcp $S;c3_rtcp=--config 3 --rtcp $S;c1=--config 1 $S --no-cpu-baseline;percall=--percall;percall_gcm=--percall --percall-suite 4 --no-cpu-baseline}"
+IFS=';' read -ra BS <<< "${BENCHES:-c2=--config 2 $S;c3=--config 3 $S;c4=--config 4 $S;c2_rtcp=--config 2 --rtcp $S;c3_rtcp=--config 3 --rtcp $S;percall=--percall;percall_gcm=--percall --percall-suite 4 --no-cpu-baseline}"
 for nb in "${BS[@]}"; do
   n=${nb%%=*}; a=${nb#*=}
   timeout -k 10 300 python3 bench.py $a > $O/$n.json 2> $O/$n.err || exit $?

@@ -45,6 +45,14 @@
 			       147 VGPRs instead of 110 */
 #define CTRF_SB_ST 0
 #endif
+#ifndef CTRF_PRIO           /* steady chunks lower the wave's issue priority
+				   as it advances (s_setprio 3..0 by quarter of
+				   the packet): the SIMD's oldest-first
+				   arbitration otherwise finishes its 4 waves at
+				   51/68/84/100 % of a workgroup's lifetime
+				   (profiles/r05/fused_waves.txt) */
+#define CTRF_PRIO 0
+#endif
 #ifndef CTRF_SHAFIRST_U     /* unprotect steady chunk: MAC, then decrypt */
 #define CTRF_SHAFIRST_U 1
 #endif
@@ -325,6 +333,20 @@ __device__ __forceinline__ void ctr_fast_pkt(const KArgs &a, uint8_t *smem,
 	auto steady = [&](uint32_t k, auto coal) {
 		constexpr bool CO = decltype(coal)::value;
 		const uint32_t c0 = 64u * k;
+		if (CTRF_PRIO) {
+			/* wave-uniform progress quarter -> priority 3..0 */
+			const uint32_t q4 =
+				(uint32_t)__builtin_amdgcn_readfirstlane(4u * k) /
+				(uint32_t)__builtin_amdgcn_readfirstlane(nb);
+			if (q4 == 0)
+				__builtin_amdgcn_s_setprio(3);
+			else if (q4 == 1)
+				__builtin_amdgcn_s_setprio(2);
+			else if (q4 == 2)
+				__builtin_amdgcn_s_setprio(1);
+			else
+				__builtin_amdgcn_s_setprio(0);
+		}
 		uint32_t d[16], w[16];
 		if constexpr (CO) {
 			uint32_t x[4][4];

@@ -297,6 +297,12 @@ static int fz_issue(struct dcall *k, int sync)
 		w->fz_tbase = 0;
 		w->fz_par = 0;
 	}
+	{
+		const long e = __atomic_exchange_n(&g_env.fzepoch, 0,
+						   __ATOMIC_RELAXED);
+		if (e > 0 && e <= 0xffff)
+			w->fz_epoch = (uint32_t)e;
+	}
 	poff = FZ_HEAD + (size_t)w->fz_par * FZ_SLOT;
 	k->foff = poff;
 

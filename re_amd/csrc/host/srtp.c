@@ -236,6 +236,11 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nosmall = value > 0;
 	else if (!strcmp(name, "noplanfuse"))
 		g_env.noplanfuse = value > 0;
+	else if (!strcmp(name, "fzepoch"))
+		/* test hook: the calling thread's next fused launch uses this
+		 * look-back epoch (tests/test_gpu_fused.py: the wrap) */
+		__atomic_store_n(&g_env.fzepoch, value > 0 ? value : 0,
+				 __ATOMIC_RELAXED);
 	else if (!strcmp(name, "nofuse"))
 		g_env.nofuse = value > 0;
 	else if (!strcmp(name, "smallsync"))

@@ -117,6 +117,8 @@ struct srtp_env {
 				   batches take the separate device planner
 				   (k_parse + k_plan_*), not the plan inside
 				   the crypto launch (k_ctr_fused.h) */
+	long fzepoch;           /* srtp_gpu_tune fzepoch: the next fused
+				   launch's look-back epoch (test hook) */
 	int nofuse;             /* srtp_gpu_tune nofuse: the operations of a
 				   shared per-packet launch run as separate
 				   launches (helper thread), not one */

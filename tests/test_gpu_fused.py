@@ -183,3 +183,42 @@ def test_fused_short_capacity_and_continuation(torch_cuda):
     for x, y in zip(outs, routs):
         for u, v in zip(x, y):
             assert (u == v).all()
+
+
+def test_fused_many_launches_sizes_and_epoch_wrap(torch_cuda):
+    """one stream continued over many fused launches of every workgroup
+    shape (1 packet, a partial, exactly one, one past, several) -- the
+    ticket base, the double-buffered plan out and the look-back epoch move
+    on every launch -- and across the epoch's wrap (the host zeroes the
+    look-back words and counters, srtp_gpu_tune fzepoch starts it just
+    short of 0xffff): every batch equal to the separate planner's, and the
+    final stream state too"""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    key = keys_for(1, 1)[0]
+    sizes = [1, 2, 1023, 1024, 1025, 3000, 1, 700, 2049, 5]
+    seq = 65400
+    parts = []
+    for n in sizes:
+        parts.append(batch(rng, list(range(seq, seq + n))))
+        seq += n
+    outs = {}
+    for mode, tune in (("fused", {}), ("planner", {"noplanfuse": 1})):
+        ctx = P.Srtp(1, key)
+        res = []
+        f0 = P.counter("fused")
+        with P.tune(**tune):
+            for k, part in enumerate(parts):
+                if mode == "fused" and k == 3:
+                    P.lib().srtp_gpu_tune(b"fzepoch", 0xfffe)
+                ar, pos, end, cap, _ = to_arena(part)
+                res.append(run_dev(torch, "srtp_encrypt", [ctx], ar, pos,
+                                   end, cap, None))
+        outs[mode] = (res, states([ctx], [SSRC]), P.counter("fused") - f0)
+        ctx.close()
+    assert outs["fused"][2] == len(sizes)
+    assert outs["planner"][2] == 0
+    assert outs["fused"][1] == outs["planner"][1]
+    for x, y in zip(outs["fused"][0], outs["planner"][0]):
+        for u, v in zip(x, y):
+            assert (u == v).all()

@@ -241,7 +241,12 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * launch waited for by a stream synchronisation, not its completion
  * word), "pcrunners" (per-packet runners at once, 1-4, default 4),
  * "pcspin" (pause loops a waiting per-packet caller spins before it
- * sleeps, default 1000), "rxseq" (srtp_rx_index* and srtp_rx_fold walk
+ * sleeps, default 1000), "pchold" (us a new per-packet runner holds its
+ * launch to gather more calls while other runners are in flight, default
+ * 0), "noplanfuse" (single-stream AES-CM device batches take the separate
+ * planner launches, not the plan inside the crypto launch), "fzepoch"
+ * (test hook: the calling thread's next fused launch's look-back epoch),
+ * "rxseq" (srtp_rx_index* and srtp_rx_fold walk
  * in one sequential pass, not in parallel parts), "freshmulti" (the
  * planner's first-batch hint: 1 sends a session's first batch to the
  * per-stream planner, 0 to the one-stream plan; the library sets it when a

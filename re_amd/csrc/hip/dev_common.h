@@ -120,6 +120,25 @@ __device__ __forceinline__ void tt_fill(uint8_t *smem, const uint32_t *T0g)
 	}
 }
 
+/* tt_fill for 1024-thread blocks: thread t's 16 words are entries
+ * (t >> 6) + 16 j of T0 (uniform per wave), loads issued together, then
+ * the stores (see tt4_fill_b1024) */
+__device__ __forceinline__ void tt_fill_b1024(uint8_t *smem,
+					      const uint32_t *T0g)
+{
+	uint32_t *s = (uint32_t *)smem;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const bool rot = (tid & 63u) >= 32u;
+	uint32_t t[16];
+#pragma unroll
+	for (int j = 0; j < 16; j++)
+		t[j] = T0g[wv + 16u * (uint32_t)j];
+#pragma unroll
+	for (int j = 0; j < 16; j++)
+		s[tid + 1024u * (uint32_t)j] = rot ? rotl32(t[j], 8) : t[j];
+}
+
 /* one middle round r (1 <= r < NR) on (s0..s3); k = rk + 4r (rot16'd) */
 __device__ __forceinline__ void aes_round(const uint8_t *smem, uint32_t lo,
 					  const uint32_t *k, uint32_t &s0,
@@ -242,6 +261,31 @@ __device__ __forceinline__ void tt4_fill(uint8_t *smem, const uint32_t *T0g)
 		const uint32_t k = ((i >> 13) & 2u) | ((i >> 5) & 1u);
 		const uint32_t t = T0g[e];
 		s[i] = k ? __builtin_amdgcn_alignbit(t, t, 32 - 8 * k) : t;
+	}
+}
+
+/* tt4_fill for 1024-thread blocks: thread t's 32 words are entries
+ * (t >> 6) + 16 m of T0 (m < 16, each twice: rotations k and k + 2), the
+ * same for its whole wave -- 16 uniform loads issued together, then the
+ * 32 conflict-free LDS stores, instead of a load and its wait per word
+ * (the loop form: ~11 us of the fused kernel's ~15-us plan) */
+__device__ __forceinline__ void tt4_fill_b1024(uint8_t *smem,
+					       const uint32_t *T0g)
+{
+	uint32_t *s = (uint32_t *)smem;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const uint32_t klo = (tid >> 5) & 1u;
+	uint32_t t[16];
+#pragma unroll
+	for (int m = 0; m < 16; m++)
+		t[m] = T0g[wv + 16u * (uint32_t)m];
+#pragma unroll
+	for (int j = 0; j < 32; j++) {
+		const uint32_t k = (((uint32_t)j >> 4) & 1u) << 1 | klo;
+		const uint32_t v = t[j & 15];
+		s[tid + 1024u * (uint32_t)j] =
+			k ? __builtin_amdgcn_alignbit(v, v, 32u - 8u * k) : v;
 	}
 }
 

@@ -24,8 +24,8 @@ kfn_f sgpu_pick_fused(int nr, int prot, int undo)
 extern "C" __attribute__((visibility("default"))) int
 sgpu_fz_wtime(uint64_t *out, size_t n)
 {
-	if (n > 20u * FZ_WTIME_MAX)
-		n = 20u * FZ_WTIME_MAX;
+	if (n > FZ_WREC * FZ_WTIME_MAX)
+		n = FZ_WREC * FZ_WTIME_MAX;
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fzw), n * 8, 0,
 				   hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }

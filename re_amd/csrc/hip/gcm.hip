@@ -423,6 +423,35 @@ __device__ __forceinline__ void gh8_fill(uint8_t *img, const uint32_t (*ht)[4])
 	}
 }
 
+/* gh8_fill for 1024-thread blocks: thread t's 4 entries b = (t >> 4) +
+ * 64 j share L = ht[(t >> 4) & 15]; the 5 table loads issued together */
+__device__ __forceinline__ void gh8_fill_b1024(uint8_t *img,
+					       const uint32_t (*ht)[4])
+{
+	const uint32_t tid = threadIdx.x, r = tid & 15u;
+	const uint4 L = *(const uint4 *)ht[(tid >> 4) & 15u];
+	uint4 H[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++)
+		H[j] = *(const uint4 *)ht[(tid >> 8) + 4u * (uint32_t)j];
+	const uint32_t m = L.w & 15u;
+	const uint32_t red = (m ^ (m << 5) ^ (m << 6) ^ (m << 7)) << 21;
+	const uint32_t lx = (L.x >> 4) ^ red;
+	const uint32_t ly = __builtin_amdgcn_alignbit(L.x, L.y, 4);
+	const uint32_t lz = __builtin_amdgcn_alignbit(L.y, L.z, 4);
+	const uint32_t lw = __builtin_amdgcn_alignbit(L.z, L.w, 4);
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const uint32_t b = (tid >> 4) + 64u * (uint32_t)j;
+		*(uint4 *)(img + b * 256u + r * 16u) = make_uint4(
+			lx ^ H[j].x, ly ^ H[j].y, lz ^ H[j].z, lw ^ H[j].w);
+	}
+}
+
+#ifndef GCM_FILL_LOOP
+#define GCM_FILL_LOOP 0
+#endif
+
 /*
  * X = X * H (SP 800-38D 6.3) with the 8-bit table and one deferred
  * reduction.  With X_i the byte i of X and i = 4w + q:
@@ -915,7 +944,11 @@ k_gcmu(const KArgs a)
 	prof_guard(a);
 	if (a.c.guard && *a.c.guard)          /* rejected plan */
 		return;
-	tt_fill(smem, a.t0);
+	static_assert(GCMU_BLOCK == 1024u, "tt_fill_b1024 / gh8_fill_b1024");
+	if (GCM_FILL_LOOP || blockDim.x != 1024u)
+		tt_fill(smem, a.t0);
+	else
+		tt_fill_b1024(smem, a.t0);
 	uint8_t *__restrict__ verdict = a.verdict;
 	const bool undo = a.c.undo;
 	const uint32_t lane = threadIdx.x & 63u;
@@ -935,8 +968,12 @@ k_gcmu(const KArgs a)
 		atomicMin(&blk_comp, j.comp);
 	__syncthreads();
 	const uint32_t bc = blk_comp;
-	if (bc != 0xffffffffu)
-		gh8_fill(smem + GH8_OFF, a.comps[bc].htab);
+	if (bc != 0xffffffffu) {
+		if (GCM_FILL_LOOP || blockDim.x != 1024u)
+			gh8_fill(smem + GH8_OFF, a.comps[bc].htab);
+		else
+			gh8_fill_b1024(smem + GH8_OFF, a.comps[bc].htab);
+	}
 	__syncthreads();
 	if (!live)
 		return;

@@ -488,10 +488,16 @@ __device__ __forceinline__ void ctr_fast_pkt(const KArgs &a, uint8_t *smem,
 		a.verdict[f.p] = vd;
 }
 
+#ifndef CTRF_FILL_LOOP
+#define CTRF_FILL_LOOP 0
+#endif
 template <int NR, int SHIFT, bool PROT, bool MK = false, bool RTCP = false>
 __device__ __forceinline__ void ctr_fast_body(const KArgs &a, uint8_t *smem)
 {
-	tt4_fill(smem, a.t0);
+	if (CTRF_FILL_LOOP || blockDim.x != 1024u)
+		tt4_fill(smem, a.t0);
+	else
+		tt4_fill_b1024(smem, a.t0);
 	__syncthreads();
 	FastPkt f;
 	if (!fast_pkt<RTCP>(a.c, blockIdx.x * blockDim.x + threadIdx.x, f))

@@ -88,6 +88,22 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v)
 	return v;
 }
 
+#ifdef FZ_WTIME
+#define FZ_WTIME_MAX 4096u
+#define FZ_WREC 24u
+/* per ticket: [0] start (thread 0), [1] CU id, [2 + w] wave w's end,
+ * [18 + k] thread 0 at the plan's k-th barrier */
+__device__ uint64_t g_fzw[FZ_WREC * FZ_WTIME_MAX];
+#define FZ_STAMP(k)                                                          \
+	do {                                                                 \
+		if (threadIdx.x == 0 && S.t < FZ_WTIME_MAX)                  \
+			g_fzw[FZ_WREC * S.t + 18u + (k)] =                   \
+				__builtin_amdgcn_s_memrealtime();            \
+	} while (0)
+#else
+#define FZ_STAMP(k) do { } while (0)
+#endif
+
 /*
  * Steps 1-4 of the header comment for the calling workgroup (packets
  * base + tid).  Returns the header class (0..3) if the lane has a packet
@@ -111,6 +127,7 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 		S.fail = 0;
 	}
 	__syncthreads();
+	FZ_STAMP(0);
 	const uint32_t t = S.t;
 	const uint32_t base = t * B, i = base + tid;
 	const bool live = i < n;
@@ -159,13 +176,20 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 			S.seq[2 - tid] = sv;
 		}
 	}
+#ifndef FZ_FILL_LOOP
+	static_assert(FZ_BLOCK == 1024, "tt4_fill_b1024");
+	tt4_fill_b1024(smem, a.t0);
+#else
 	tt4_fill(smem, a.t0);
+#endif
+	FZ_STAMP(4);
 	if (live) {
 		P.hdr[i] = h;
 		P.es[i] = e;
 		S.seq[tid + 2] = h.seq;
 	}
 	__syncthreads();
+	FZ_STAMP(1);
 
 	/* k_plan_count's checks (srtp_kernels.hip) */
 	const uint32_t hl0 = S.hl0;
@@ -210,6 +234,7 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	if (lane == 0)
 		S.wsum[wv] = (uint32_t)__popcll(m);
 	__syncthreads();
+	FZ_STAMP(2);
 
 	if (wv == 0) {
 		/* step 3: aggregate, look-back, inclusive prefix */
@@ -267,6 +292,7 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 		}
 	}
 	__syncthreads();
+	FZ_STAMP(3);
 	if (!live)
 		return -1;
 	if (S.xfail) {
@@ -335,12 +361,6 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	return (int)((hl0 >> 2) & 3u);
 }
 
-#ifdef FZ_WTIME
-#define FZ_WTIME_MAX 4096u
-/* per ticket: [0] start (thread 0), [1] CU id, [2 + w] wave w's end */
-__device__ uint64_t g_fzw[20u * FZ_WTIME_MAX];
-#endif
-
 template <int NR, bool PROT>
 __global__ void
 __attribute__((amdgpu_flat_work_group_size(1, CTRF_BLK(PROT))))
@@ -360,8 +380,8 @@ k_ctr_fused(const FArgs fa)
 	if (threadIdx.x == 0 && S.t < FZ_WTIME_MAX) {
 		uint32_t hw;
 		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-		g_fzw[20u * S.t] = t_start;
-		g_fzw[20u * S.t + 1u] = hw;
+		g_fzw[FZ_WREC * S.t] = t_start;
+		g_fzw[FZ_WREC * S.t + 1u] = hw;
 	}
 #endif
 	if (cls < 0)
@@ -382,7 +402,7 @@ k_ctr_fused(const FArgs fa)
 	if ((threadIdx.x & 63u) == 0) {
 		const uint32_t t = S.t;
 		if (t < FZ_WTIME_MAX)
-			g_fzw[20u * t + 2u + threadIdx.x / 64u] =
+			g_fzw[FZ_WREC * t + 2u + threadIdx.x / 64u] =
 				__builtin_amdgcn_s_memrealtime();
 	}
 #endif

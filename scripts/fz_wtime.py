@@ -21,10 +21,10 @@ import bench  # noqa: E402
 bench.main()
 lib = ctypes.CDLL(os.environ["RE_SRTP_LIB"])
 n = 1024
-buf = np.zeros(20 * n, dtype=np.uint64)
+buf = np.zeros(24 * n, dtype=np.uint64)
 assert lib.sgpu_fz_wtime(buf.ctypes.data_as(ctypes.c_void_p),
                          ctypes.c_size_t(buf.size)) == 0
-a = buf.reshape(n, 20).astype(np.int64)
+a = buf.reshape(n, 24).astype(np.int64)
 t0 = a[:, 0].min()
 st = (a[:, 0] - t0) / 100.0
 we = (a[:, 2:18] - t0) / 100.0
@@ -51,5 +51,15 @@ gaps = np.array(gaps)
 print("hardware CU ids %d; gap between a CU's workgroups: mean %.2f p50 %.2f "
       "max %.2f us (%d gaps)" % (len(np.unique(cu)), gaps.mean(),
                                  np.median(gaps), gaps.max(), len(gaps)))
+# the plan's barriers (thread 0): 0 ticket, 4 after the image fill, 1 the
+# header writes, 2 the checks' ballot, 3 the look-back
+pb = (a[:, [18, 22, 19, 20, 21]] - t0) / 100.0
+names = ("ticket", "image fill", "headers", "checks", "look-back")
+prev = st
+for k, nm in enumerate(names):
+    d = pb[:, k] - prev
+    print("  plan %-10s mean %6.2f p50 %6.2f p90 %6.2f us" % (
+        nm, d.mean(), np.median(d), np.percentile(d, 90)))
+    prev = pb[:, k]
 for t in np.linspace(0, end.max(), 11):
     print("  %7.1f us: running %4d" % (t, ((st <= t) & (end > t)).sum()))

@@ -102,12 +102,15 @@ def oracle_backend(suite, key):
                                                                0)[0])
 
 
-@pytest.mark.parametrize("suites,fuse,runners", [
-    (SUITES, 1, 0), (SUITES, 0, 0), (SUITES, 1, 1),
+@pytest.mark.parametrize("suites,fuse,runners,hold", [
+    (SUITES, 1, 0, 0), (SUITES, 0, 0, 0), (SUITES, 1, 1, 0),
     # CTR suites only, one runner (its queue gathers every thread's next
     # call): lists mixing operations run as one fused launch
-    ([1, 0, 3, 2], 1, 1), ([1, 0, 3, 2], 0, 1), ([1, 0, 3, 2], 1, 0)])
-def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners):
+    ([1, 0, 3, 2], 1, 1, 0), ([1, 0, 3, 2], 0, 1, 0), ([1, 0, 3, 2], 1, 0, 0),
+    # a new runner holding its launch 20 us while others run (pchold)
+    (SUITES, 1, 0, 20)])
+def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners,
+                                        hold):
     T = 16
     keys = [bytes((13 * t + i) & 0xff for i in range(46)) for t in range(T)]
     want, got = {}, {}
@@ -123,7 +126,7 @@ def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners):
         k = keys[t][:P.key_len(s) + P.salt_len(s)]
         ths.append(threading.Thread(target=run_thread,
                                     args=(t, s, k, dev_backend, got)))
-    with P.tune(nofuse=0 if fuse else 1, pcrunners=runners):
+    with P.tune(nofuse=0 if fuse else 1, pcrunners=runners, pchold=hold):
         for th in ths:
             th.start()
         for th in ths:

@@ -245,7 +245,8 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * launch to gather more calls while other runners are in flight, default
  * 0), "noplanfuse" (single-stream AES-CM device batches take the separate
  * planner launches, not the plan inside the crypto launch), "fzepoch"
- * (test hook: the calling thread's next fused launch's look-back epoch),
+ * (test hook, process-wide and one-shot: the next fused launch of any
+ * thread takes this look-back epoch, its look-back words zeroed first),
  * "rxseq" (srtp_rx_index* and srtp_rx_fold walk
  * in one sequential pass, not in parallel parts), "freshmulti" (the
  * planner's first-batch hint: 1 sends a session's first batch to the

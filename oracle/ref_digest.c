@@ -25,6 +25,13 @@
  *      flipped (^ 0x40) -- 1048 EAUTH verdicts, the receiver states and the
  *      post-error bytes (ciphertext kept, ROC over the tag) pinned
  *  10  config 4 (64K sessions, mixed lengths) with the same forgeries
+ *  11  config 3 (AEAD_AES_256_GCM) with the same forgeries -- the GCM
+ *      EAUTH side effects (payload left decrypted in place, end not
+ *      trimmed: srtp.c:394-411) pinned at full size
+ *  12  shape 7 (SRTCP, CM128/HMAC80) with the same forgeries, and every
+ *      packet i with i % 1000 == 499 replaced after protect by a copy of
+ *      packet i - 1's protected bytes (same SRTCP index: EALREADY after a
+ *      good tag, the tag trimmed, srtcp.c:199-209)
  *
  *   ref_digest <config> [npkts]
  *
@@ -88,9 +95,11 @@ struct cfg {
 	unsigned nssrc;         /* SSRCs of session 0: packet i -> i mod nssrc */
 	int rtcp;               /* SRTCP (workload.make_rtcp_arena) */
 	unsigned forge;         /* forge packet i when i % forge == forge-1 */
+	unsigned replay;        /* packet i when i % replay == replay/2 - 1:
+				   a copy of protected packet i - 1 */
 };
 
-#define NCFG 11
+#define NCFG 13
 static const struct cfg CFG[NCFG] = {
 	{0, 0, 0, 0, 0, 0, 1, 0},
 	{1, 1024, 160, 1, 1, 1, 1, 0},
@@ -103,6 +112,8 @@ static const struct cfg CFG[NCFG] = {
 	{5, 1u << 20, 1200, 1, 65000, 0, 1, 1},
 	{1, 1u << 20, 1200, 1, 65000, 0, 1, 0, 1000},
 	{1, 1u << 20, 0, 1u << 16, 65000, 0, 1, 0, 1000},
+	{5, 1u << 20, 1200, 1, 65000, 0, 1, 0, 1000},
+	{1, 1u << 20, 1200, 1, 65000, 0, 1, 1, 1000, 1000},
 };
 
 static void hex(const uint8_t *p, size_t n)
@@ -431,8 +442,8 @@ int main(int argc, char **argv)
 
 	printf("{\"config\":%d,\"suite\":%d,\"n\":%zu,\"slot\":%zu,"
 	       "\"nsess\":%zu,\"nssrc\":%u,\"rtcp\":%d,\"forge\":%u,"
-	       "\"plain\":", c, cf.suite, n, slot, cf.nsess, cf.nssrc, cf.rtcp,
-	       cf.forge);
+	       "\"replay\":%u,\"plain\":", c, cf.suite, n, slot, cf.nsess,
+	       cf.nssrc, cf.rtcp, cf.forge, cf.replay);
 	sha(arena, n * slot);
 
 	/* protect every packet in array order, in place (the slot has room
@@ -453,6 +464,12 @@ int main(int argc, char **argv)
 		for (i = 0; i < n; i++)
 			if (i % cf.forge == cf.forge - 1)
 				arena[pos[i] + 32] ^= 0x40;
+	if (cf.replay)
+		for (i = 1; i < n; i++)
+			if (i % cf.replay == cf.replay / 2 - 1) {
+				memcpy(arena + pos[i], arena + pos[i - 1], slot);
+				end[i] = pos[i] + (end[i - 1] - pos[i - 1]);
+			}
 
 	for (i = 0; i < n; i++) {
 		struct mbuf mb;

@@ -54,11 +54,15 @@ struct FShared {
 	uint32_t seq[FZ_BLOCK + 2];     /* seq of packets base-2 .. base+B-1 */
 };
 
+/* SPF_* bits a look-back word carries (bits 32..45) */
+#define FZ_FMASK 0x3fffu
+static_assert((SPF_SLOW | SPF_SEG | SPF_PRED | 0x1ffu) <= FZ_FMASK, "fz_word");
+
 __device__ __forceinline__ uint64_t fz_word(uint32_t epoch, uint32_t st,
 					    uint32_t fail, uint32_t wraps)
 {
 	return (uint64_t)epoch << 48 | (uint64_t)st << 46 |
-	       (uint64_t)(fail & 0x7ffu) << 32 | wraps;
+	       (uint64_t)(fail & FZ_FMASK) << 32 | wraps;
 }
 
 __device__ __forceinline__ void fz_store(unsigned long long *w, uint64_t v)
@@ -252,10 +256,14 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 				if (k >= 0) {
 					/* every workgroup below t is running or
 					 * done and publishes before it waits; the
-					 * bound only turns a broken ticket count
-					 * into a rejected plan (SPF_BAD: the host
-					 * re-plans and resets the counters)
-					 * instead of a wave that never ends */
+					 * bound (2^18 polls of s_sleep 1, ~64
+					 * clocks each: ~7 ms at 2.4 GHz) only
+					 * turns a stalled predecessor or a broken
+					 * ticket count into a rejected plan
+					 * (SPF_SLOW: the host re-plans, resets
+					 * the counters and counts it apart from
+					 * a bad window, "lbtimeouts") instead of
+					 * a wave that never ends */
 					for (uint32_t spin = 0;; spin++) {
 						w = fz_load(&P.agg[k]);
 						st = (uint32_t)(w >> 46) & 3u;
@@ -263,7 +271,7 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 						    st != 0)
 							break;
 						if (spin > (1u << 18)) {
-							w = fz_word(0, 2, SPF_BAD, 0);
+							w = fz_word(0, 2, SPF_SLOW, 0);
 							st = 2;
 							break;
 						}
@@ -275,7 +283,7 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 					(uint32_t)__ffsll((long long)inc) - 1u : 64u;
 				const bool take = lane <= first;
 				excl += wave_sum(take ? (uint32_t)w : 0u);
-				xf |= wave_or(take ? (uint32_t)(w >> 32) & 0x7ffu
+				xf |= wave_or(take ? (uint32_t)(w >> 32) & FZ_FMASK
 						   : 0u);
 				if (inc)
 					break;
@@ -287,8 +295,9 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 						    excl + tot));
 			S.excl = excl;
 			S.xfail = lf | xf;
-			if (lf | (xf & SPF_BAD))
-				atomicOr(&P.out->fail, lf | (xf & SPF_BAD));
+			if (lf | (xf & (SPF_BAD | SPF_SLOW)))
+				atomicOr(&P.out->fail,
+					 lf | (xf & (SPF_BAD | SPF_SLOW)));
 		}
 	}
 	__syncthreads();
@@ -361,10 +370,14 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	return (int)((hl0 >> 2) & 3u);
 }
 
+/* sgpu_run_fused always launches FZ_BLOCK threads (one packet per lane,
+ * both directions), so the attributes name FZ_BLOCK, not the lean
+ * kernel's per-direction CTRF_BLK(PROT) (a build with CTRF_BLOCK_U below
+ * CTRF_BLOCK would otherwise fail every fused unprotect launch) */
 template <int NR, bool PROT>
 __global__ void
-__attribute__((amdgpu_flat_work_group_size(1, CTRF_BLK(PROT))))
-__attribute__((amdgpu_waves_per_eu(CTRF_BLK(PROT) / 256, 8)))
+__attribute__((amdgpu_flat_work_group_size(1, FZ_BLOCK)))
+__attribute__((amdgpu_waves_per_eu(FZ_BLOCK / 256, 8)))
 k_ctr_fused(const FArgs fa)
 {
 #ifdef FZ_WTIME

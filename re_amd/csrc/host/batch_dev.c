@@ -182,6 +182,7 @@ int dev_planned_finish(struct dcall *k)
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
+	count(&g_cnt_dplans, 1);
 	if (nfail)
 		count(&g_cnt_misses, nfail);
 	plan_apply(s, po, prot, n, &old);
@@ -286,20 +287,27 @@ static int fz_issue(struct dcall *k, int sync)
 	if (err)
 		return err;
 	fz = w->fz.d;
-	if (w->fz_d != fz || w->fz_epoch == 0 || w->fz_epoch > 0xffffu) {
-		/* a new pool (or the look-back epoch wrapped): counters,
-		 * plan outs and look-back words from zero */
-		err = sgpu_memset(fz, 0, w->fz.cap, stream);
-		if (err)
-			return err;
-		w->fz_d = fz;
-		w->fz_epoch = 1;
-		w->fz_tbase = 0;
-		w->fz_par = 0;
-	}
 	{
+		/* srtp_gpu_tune fzepoch (a test hook, one-shot for whichever
+		 * thread's fused launch comes next): the look-back words are
+		 * zeroed with it, so words of an epoch used since the last
+		 * zeroing can never match */
 		const long e = __atomic_exchange_n(&g_env.fzepoch, 0,
 						   __ATOMIC_RELAXED);
+		if (e > 0 && e <= 0xffff)
+			w->fz_d = NULL;
+		if (w->fz_d != fz || w->fz_epoch == 0 ||
+		    w->fz_epoch > 0xffffu) {
+			/* a new pool (or the look-back epoch wrapped):
+			 * counters, plan outs and look-back words from zero */
+			err = sgpu_memset(fz, 0, w->fz.cap, stream);
+			if (err)
+				return err;
+			w->fz_d = fz;
+			w->fz_epoch = 1;
+			w->fz_tbase = 0;
+			w->fz_par = 0;
+		}
 		if (e > 0 && e <= 0xffff)
 			w->fz_epoch = (uint32_t)e;
 	}
@@ -405,8 +413,10 @@ static int fz_finish(struct dcall *k, int sync)
 		sgpu_prof_void(F->prof_id);
 		if (po->fail & SPF_PRED)
 			return -2;      /* every workgroup did nothing */
-		if (po->fail & SPF_BAD)
+		if (po->fail & (SPF_BAD | SPF_SLOW))
 			w->fz_d = NULL; /* ticket / look-back state from zero */
+		if (po->fail & SPF_SLOW)
+			count(&g_cnt_lbtimeout, 1);
 		if ((po->fail & SPF_SSRC) && !ns0)
 			__atomic_store_n(&g_fresh_multi, 1, __ATOMIC_RELAXED);
 		count(&g_cnt_rejects, 1);
@@ -829,6 +839,7 @@ int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
+	count(&g_cnt_rplans, 1);
 	/* the stream (stream.c:45-67) and its SRTCP state after the batch */
 	if (!s->nstreams) {
 		memset(&s->streams[0], 0, sizeof(s->streams[0]));
@@ -1135,6 +1146,7 @@ int dev_mplanned_finish(struct dcall *k)
 		count(&g_cnt_rejects, 1);
 		return -1;
 	}
+	count(&g_cnt_mplans, 1);
 	if (!nfail)
 		return 0;
 	count(&g_cnt_misses, nfail);

@@ -123,6 +123,12 @@ uint64_t g_cnt_devfolds; /* verdicts folded on the device */
 uint64_t g_cnt_splans;   /* per-stream device plans accepted */
 uint64_t g_cnt_fused;    /* batches planned inside the crypto launch
 				   (dev_fused), accepted */
+uint64_t g_cnt_dplans;   /* single-stream planner launches (k_plan_*,
+				   GCM and noplanfuse), accepted */
+uint64_t g_cnt_mplans;   /* multi-session device plans accepted */
+uint64_t g_cnt_rplans;   /* SRTCP device plans (k_plan_rtcp) accepted */
+uint64_t g_cnt_lbtimeout; /* fused launches rejected by a look-back
+				   wait past its bound (SPF_SLOW) */
 /* a session's first batch (no stream yet) goes to the per-stream planner
  * while the last first batch planned showed several SSRCs: a one-stream
  * plan for it is rejected at completion and the batch planned again, a
@@ -171,6 +177,14 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_splans, __ATOMIC_RELAXED);
 	if (!strcmp(name, "fused"))
 		return __atomic_load_n(&g_cnt_fused, __ATOMIC_RELAXED);
+	if (!strcmp(name, "dplans"))
+		return __atomic_load_n(&g_cnt_dplans, __ATOMIC_RELAXED);
+	if (!strcmp(name, "mplans"))
+		return __atomic_load_n(&g_cnt_mplans, __ATOMIC_RELAXED);
+	if (!strcmp(name, "rplans"))
+		return __atomic_load_n(&g_cnt_rplans, __ATOMIC_RELAXED);
+	if (!strcmp(name, "lbtimeouts"))
+		return __atomic_load_n(&g_cnt_lbtimeout, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcbatches"))
 		return __atomic_load_n(&g_cnt_pcbatch, __ATOMIC_RELAXED);
 	if (!strcmp(name, "pcpackets"))
@@ -1239,11 +1253,19 @@ struct ws *ws_get(void)
  */
 /* after a failed small launch: the workgroup count (0 between launches)
  * may be left part-way, so it is zeroed again on the idle stream before the
- * workspace's next launch counts on it */
+ * workspace's next launch counts on it -- or, when the stream does not
+ * synchronise cleanly (the fault case) or the zeroing fails, the pair is
+ * dropped and the next small_run allocates and zeroes a fresh one */
 static int small_reset(struct ws *w, int err)
 {
-	if (w->sm_cnt && !sgpu_stream_sync(w->stream))
-		(void)sgpu_memset(w->sm_cnt, 0, 4, w->stream);
+	if (!w->sm_cnt)
+		return err;
+	if (!sgpu_stream_sync(w->stream) &&
+	    !sgpu_memset(w->sm_cnt, 0, 4, w->stream))
+		return err;
+	sgpu_free(w->sm_cnt);
+	sgpu_host_free(w->sm_flag);
+	w->sm_cnt = w->sm_flag = NULL;
 	return err;
 }
 

@@ -242,6 +242,7 @@ enum { SEL_RUN = 0, SEL_UNDO = 1 };
 extern uint64_t g_cnt_pcbatch, g_cnt_pcpkts, g_cnt_pcfused, g_cnt_rxw_redo;
 extern uint64_t g_cnt_misses, g_cnt_folds, g_cnt_rejects, g_cnt_devfolds;
 extern uint64_t g_cnt_splans, g_cnt_fused, g_cnt_gated;
+extern uint64_t g_cnt_dplans, g_cnt_mplans, g_cnt_rplans, g_cnt_lbtimeout;
 extern int g_fresh_multi;       /* srtp.c: the last first batch of a session
 				   showed several SSRCs (see there) */
 extern __thread struct tk_owner *t_own; /* srtp.c: this thread's async

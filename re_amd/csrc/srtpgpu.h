@@ -251,6 +251,9 @@ enum {
 	SPF_SEG     = 1u << 10, /* multi-session counting grouping: a session
 				   with more than SGPU_MP_SEGMAX packets (the
 				   host re-plans with the radix sort) */
+	SPF_SLOW    = 1u << 11, /* fused launch: a look-back wait ran past its
+				   bound (a stalled predecessor, not a bad
+				   window: counted as "lbtimeouts") */
 };
 #define SGPU_MP_SEGMAX 1024
 

@@ -175,9 +175,21 @@ def random_sessions(npkts, nsess, seed=SEED_PAYLOAD + 2):
 #   5  the config-5 stream, 2M packets (two 1M shards of it)
 #   6  config 2 over 2 SSRCs of one session (packet i -> SSRC i mod 2)
 #   7  SRTCP in the config-2 shape, 8  SRTCP in the config-3 shape
-#   9  config 2, 10 config 4, with the packets i % 1000 == 999 forged
-#      between protect and unprotect (FORGE_AT: payload byte 20 ^ 0x40)
+#   9  config 2, 10 config 4, 11 config 3, with the packets
+#      i % 1000 == 999 forged between protect and unprotect (FORGE_AT:
+#      payload byte 20 ^ 0x40)
+#  12  shape 7 (SRTCP) with the same forgeries, and every packet
+#      i % 1000 == 499 replaced after protect by a copy of protected packet
+#      i - 1 (replay_targets: a replayed SRTCP index)
 FORGE_AT = 32
+
+
+def replay_targets(n, replay):
+    """packets overwritten by a copy of their predecessor (ref_digest.c:
+    i % replay == replay / 2 - 1, i >= 1)"""
+    i = np.arange(1, n)
+    return i[i % replay == replay // 2 - 1]
+
 CONFIGS = {
     1: dict(suite=1, n=1024, length=160, nsess=1, s0=1, key=CONFIG1_KEY),
     2: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000),
@@ -190,6 +202,9 @@ CONFIGS = {
     9: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, forge=1000),
     10: dict(suite=1, n=1 << 20, length=None, nsess=1 << 16, s0=65000,
              forge=1000),
+    11: dict(suite=5, n=1 << 20, length=1200, nsess=1, s0=65000, forge=1000),
+    12: dict(suite=1, n=1 << 20, length=1200, nsess=1, s0=65000, rtcp=True,
+             forge=1000, replay=1000),
 }
 
 KEY_LEN = {0: 30, 1: 30, 2: 46, 3: 46, 4: 28, 5: 44}

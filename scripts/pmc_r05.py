@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Round-5 per-kernel PMC summary (profiles/r05_pmc.json): scripts/
 pmc_r03.py's traffic and VALU / LDS issue floors, plus the co-issue
-corrected floor the bench reports.
+corrected issue-time estimate the bench reports.  The
+estimate is not a hard floor: the GCM kernels run up to ~4 % under it.
 
     python scripts/pmc_r05.py OUT.json WORKLOAD FETCH_DIR WRITE_DIR SQ_DIR
 

@@ -10,6 +10,9 @@ reference src/srtp compiled from its sources, oracle/ref_digest.c):
             sessions
   shape 7/8 SRTCP (srtcp_*_batch_dev) over 1M x 1200-B RTCP packets,
             AES_CM_128_HMAC_SHA1_80 / AEAD_AES_256_GCM
+  shape 9-11 configs 2 / 4 / 3 with 0.1 % of the packets forged
+  shape 12  shape 7 with the same forgeries and 0.1 % replayed SRTCP
+            indices (srtcp.c:199-209)
 
 For each config: protect every packet, then unprotect the whole protected
 arena with fresh receivers; after each direction the SHA-256 of the whole
@@ -18,6 +21,11 @@ the tag included -- srtp.c:342-344), of the end array, of the per-packet
 errnos and of every session's final stream state (ROC, s_l, replay window)
 must equal the reference's.  A mismatch names the 64K-packet blocks that
 differ.
+
+Each call also asserts WHICH path produced those bytes (srtp_gpu_counter
+deltas, PATHS below): every planner rejects into an exact host re-plan, so
+without this a digest could pass on the host engine while the bench times
+the device path.
 """
 import numpy as np
 import pytest
@@ -79,6 +87,45 @@ def session_states(ctxs, rtcp=False):
     return F.state_bytes(rows)
 
 
+# per (config, direction): the counters that must move by exactly the
+# given amount in that call ("rejects" and "folds" -- a host re-plan or a
+# host fold -- must stay 0 unless listed).  fused: the in-launch plan
+# (k_ctr_fused); dplans: the single-stream planner launches (GCM);
+# mplans: the multi-session planner; rplans: the SRTCP planner; devfolds:
+# forged packets' verdicts folded on the device.
+COUNTERS = ("fused", "dplans", "mplans", "rplans", "rejects", "folds",
+            "devfolds")
+PATHS = {
+    (1, "protect"): {"fused": 1}, (1, "unprotect"): {"fused": 1},
+    (2, "protect"): {"fused": 1}, (2, "unprotect"): {"fused": 1},
+    (3, "protect"): {"dplans": 1}, (3, "unprotect"): {"dplans": 1},
+    (4, "protect"): {"mplans": 1}, (4, "unprotect"): {"mplans": 1},
+    (7, "protect"): {"rplans": 1}, (7, "unprotect"): {"rplans": 1},
+    (8, "protect"): {"rplans": 1}, (8, "unprotect"): {"rplans": 1},
+    (9, "protect"): {"fused": 1},
+    (9, "unprotect"): {"fused": 1, "devfolds": 1},
+    (10, "protect"): {"mplans": 1},
+    (10, "unprotect"): {"mplans": 1, "devfolds": 1},
+    (11, "protect"): {"dplans": 1},
+    (11, "unprotect"): {"dplans": 1, "devfolds": 1},
+    (12, "protect"): {"rplans": 1},
+    # replayed indices: the SRTCP planner's replay speculation fails
+    # (SPF_REPLAY) and the batch runs on the exact host engine
+    (12, "unprotect"): {"rejects": 1},
+}
+
+
+def counters():
+    return {c: P.counter(c) for c in COUNTERS}
+
+
+def check_path(cfg, direction, before, after):
+    want = PATHS[(cfg, direction)]
+    got = {c: after[c] - before[c] for c in COUNTERS}
+    exp = {c: want.get(c, 0) for c in COUNTERS}
+    assert got == exp, (cfg, direction, got, exp)
+
+
 def check_config(torch, ref, cfg):
     arena, pos, end, cap, sess, keys = W.build_config(cfg)
     suite, n, slot, nsess = ref["suite"], ref["n"], ref["slot"], ref["nsess"]
@@ -100,12 +147,22 @@ def check_config(torch, ref, cfg):
     for direction, op, ctxs in (("protect", pfx + "_encrypt", tx),
                                 ("unprotect", pfx + "_decrypt", rx)):
         if direction == "unprotect" and ref.get("forge"):
-            # shapes 9, 10: forge packets i % f == f - 1 (ref_digest.c)
+            # shapes 9-12: forge packets i % f == f - 1 (ref_digest.c)
             f = ref["forge"]
             idx = torch.from_numpy(pos[f - 1::f].astype(np.int64) +
                                    W.FORGE_AT).cuda()
             dev[idx] ^= 0x40
+        if direction == "unprotect" and ref.get("replay"):
+            # shape 12: packet i a copy of protected packet i - 1
+            ri = torch.from_numpy(W.replay_targets(n, ref["replay"])).cuda()
+            slots = dev.view(n, slot)
+            slots[ri] = slots[ri - 1]
+            pos_t = pos_d.long()
+            end_d[ri] = (pos_t[ri] + end_d[ri - 1].long() -
+                         pos_t[ri - 1]).int()
+        before = counters()
         err = run_dev(torch, op, ctxs, dev, pos_d, end_d, cap_d, sess_d, n)
+        check_path(cfg, direction, before, counters())
         m = F.compare(ref[direction], dev.cpu().numpy(), n, slot,
                       end_d.cpu().numpy().view(np.uint32),
                       err.cpu().numpy(), session_states(ctxs, rtcp))
@@ -116,13 +173,16 @@ def check_config(torch, ref, cfg):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 7, 8, 9, 10])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 7, 8, 9, 10, 11, 12])
 def test_fullsize_vs_reference(torch_cuda, digests, cfg):
     """configs 1-4, SRTCP arenas of the config-2 / config-3 shape (7, 8:
-    1M x 1200-B RTCP packets through srtcp_*_batch_dev), and configs 2 / 4
-    with 0.1 % of the packets forged between protect and unprotect (9, 10:
-    the EAUTH verdicts, the post-error bytes -- ciphertext kept, the ROC
-    over the tag -- and every receiver state against the reference)"""
+    1M x 1200-B RTCP packets through srtcp_*_batch_dev), configs 2 / 4 / 3
+    with 0.1 % of the packets forged between protect and unprotect (9, 10,
+    11: the EAUTH verdicts, the post-error bytes -- HMAC: ciphertext kept,
+    the ROC over the tag; GCM: the payload decrypted in place, end not
+    trimmed, srtp.c:394-411 -- and every receiver state against the
+    reference), and SRTCP with forgeries and replayed indices (12: EALREADY
+    after a good tag, srtcp.c:199-209); each through the path PATHS names"""
     check_config(torch_cuda, digests[cfg], cfg)
 
 

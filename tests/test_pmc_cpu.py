@@ -1,9 +1,13 @@
 """The bench's integer roofline (profiles/r05_pmc.json, scripts/pmc_r05.py)
-is a floor: a kernel cannot run faster than the issue time of its measured
-VALU and LDS instructions, corrected for the partial co-issue measured on
-gfx950 (profiles/r04_ubench_coissue.txt).  issue_floor_frac = max(V, L) +
-c x min(V, L) of the launch must therefore stay at or below ~1; the plain
-sum V + L (round 4's issue_frac) did not (1.21 for the headline kernel)."""
+is an ESTIMATE of the issue time of a kernel's measured VALU and LDS
+instructions, corrected for the partial co-issue measured on gfx950
+(profiles/r04_ubench_coissue.txt): issue_floor_frac = max(V, L) +
+c x min(V, L) of the launch.  It is not a hard floor: the GCM kernels run up
+to ~4 % faster than it (k_gcmu issue_floor_frac 1.026 / 1.041 -- their b128
+LDS reads and VALU co-issue better than the microbenchmark's rows), so the
+test bounds the model's error (<= 1.08) and holds the CTR kernels, where the
+rows fit, to <= 1.0.  The plain sum V + L (round 4's issue_frac) was far off
+(1.21 for the headline kernel)."""
 import json
 import os
 import sys
@@ -18,7 +22,7 @@ def entries():
                 if e.get("issue_floor_frac") is not None]
 
 
-def test_coissue_floor_is_a_floor():
+def test_coissue_estimate_bounds():
     es = entries()
     # the bench's dominant kernels of configs 2, 3 (RTP and SRTCP) and 4
     names = {(e["kernel"], e["workload"]) for e in es}
@@ -33,7 +37,7 @@ def test_coissue_floor_is_a_floor():
         assert abs(e["issue_floor_frac"] - (max(v, l) + c * min(v, l))) \
             < 1e-4
         assert e["issue_sum_frac"] >= e["issue_floor_frac"]
-        # the model's error: GCM protect runs ~5 % under it
+        # the estimate's error: the GCM kernels run up to ~4 % faster
         assert e["issue_floor_frac"] <= 1.08, e
         if e["workload"] in ("config2", "config4", "config2_rtcp"):
             assert e["issue_floor_frac"] <= 1.0, e

@@ -237,6 +237,23 @@ def test_bench_spawns_its_own_ranks():
     assert ln["rank0_state"]["roc"] == 0
 
 
+def test_bench_eight_ranks_gloo():
+    """world 8, the driver's SCALE shape, on the CPU's gloo path: bench.py
+    spawns 8 ranks itself, all rendezvous, the counters and the max time
+    reduce over 8, and every rank's boundary states at the real shard size
+    (1M packets) equal the reference's over the whole 8M-packet stream
+    (tests/golden/config5_shards.json tx_in / rx_in)"""
+    rc, lines, err = _bench(["--gpus", "8", "--same-device", "--packets",
+                             "2048", "--dry-run"], timeout=300)
+    assert rc == 0, err
+    assert len(lines) == 1, (lines, err)
+    ln = lines[0]
+    assert ln["n_gpus"] == 8 and ln["dist_world"] == 8, ln
+    assert ln["packets_total"] == 8 * 2048
+    assert ln["tmax"] == 0.008                      # max over the ranks
+    assert ln["boundary_states_ok"] == 8, ln
+
+
 def test_bench_world_size_mismatch_fails():
     rc, lines, err = _bench(["--gpus", "4", "--dry-run"],
                             {"WORLD_SIZE": "2", "RANK": "0"})

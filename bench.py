@@ -516,10 +516,14 @@ def main():
         assert nsess == 1 and cfg["length"], "--rtcp: configs 2 and 3"
         arena_h, pos, end, cap = W.make_rtcp_arena(n, lengths)
     else:
+        # config 5: rank r holds packets r*n .. (r+1)*n-1 of the one 8M
+        # stream (payload generators and timestamps continue it), exactly
+        # the shard the reference digests pin (config5_shards.json)
         arena_h, pos, end, cap = W.make_arena(
             n, lengths, s0=s0 & 0xffff,
             sess=(gsess if gsess is not None else sess) if K == 1 else
             np.arange(n, dtype=np.uint32) % K, idx=gidx,
+            first=rank * n if cfg_id == 5 else 0,
             room=args.room or 16)
     OPS = ("srtcp_encrypt", "srtcp_decrypt") if args.rtcp else \
         ("srtp_encrypt", "srtp_decrypt")

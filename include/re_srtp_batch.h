@@ -233,6 +233,8 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * CTR kernels for device-planned batches), "nocoop" (small host-planned
  * CTR launches keep the cipher in the one-packet-per-lane kernel),
  * "mpradix" (multi-session plans group packets by the radix sort),
+ * "nobucket" (multi-session plans by the counting grouping of
+ * plan_multi.hip instead of the four-launch bucket planner),
  * "nodevfold" (forged packets
  * of a device-planned batch fold on the host), "nocombine" (per-packet
  * calls of different threads do not share launches), "nosmall" (the

@@ -1,0 +1,957 @@
+/*
+ * plan_buckets.hip -- multi-session RTP batches planned on the device in
+ * three launches around the crypto (srtpgpu.h struct sgpu_bplan).
+ *
+ * The reference keeps one sequential state machine per stream
+ * (srtp_encrypt srtp.c:203-215, 279-280; srtp_decrypt srtp.c:310-321,
+ * 426-427; srtp_get_index misc.c:22-41; srtp_replay_check replay.c:32-62),
+ * and streams of different sessions are independent.  The counting
+ * grouping of plan_multi.hip needs a global scan between its passes (17
+ * launches per call with the plan and the launch order); here the sessions
+ * are cut into buckets of 2^bshift consecutive ids, each with a fixed
+ * region of `cap` entries, so a packet is placed in the launch that parses
+ * it, and every later step of a session happens inside the one workgroup
+ * that owns its bucket:
+ *
+ *   k_bp_scatter  per packet: parse + window checks (k_parse), end copy,
+ *                 its slot in its bucket (LDS count per workgroup, one
+ *                 global atomic per (workgroup, bucket) for the base)
+ *   k_bp_plan     per bucket, in LDS: the sessions' resident states, the
+ *                 entries grouped by session (counting) and ranked by
+ *                 packet index inside each session, the single-stream
+ *                 speculation per session segment (k_mp_count / desc /
+ *                 final of plan_multi.hip), the launch order; the last
+ *                 workgroup folds every fail word and re-zeroes the bucket
+ *                 counters
+ *   k_bp_finish   results, the touched states committed; with speculation
+ *                 misses the verdict fold per bucket (k_mf_* of
+ *                 plan_multi.hip) and, in the last workgroup, the forged
+ *                 packets' EAUTH results and the commit
+ *
+ * A batch the buckets cannot hold (a bucket over cap, a session over
+ * SGPU_BP_SEGMAX packets in it) fails with SPF_SEG and is re-planned by the
+ * radix-sort grouping; any other failed check rejects the plan exactly as
+ * the other planners do (nothing modified, the host plans).
+ */
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdio.h>
+#include "../srtpgpu.h"
+#include "plan_common.h"
+
+#ifndef EAUTH
+#define EAUTH 217               /* include/re_types.h:215-217 */
+#endif
+
+#define BPB SGPU_BP_BLOCK
+#define BP_IMASK 0x3ffffffu     /* entry: packet index | length bin << 26 */
+#define BP_OBINS 64
+
+/* ---- block-wide scans (1024 threads, 16 waves) ------------------------ */
+
+__device__ __forceinline__ uint32_t bp_excl_sum(uint32_t v, uint32_t *wsum,
+						uint32_t *total)
+{
+	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	uint32_t x = v;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t u = (uint32_t)__shfl_up((int)x, d);
+		if (lane >= (uint32_t)d)
+			x += u;
+	}
+	if (lane == 63)
+		wsum[wv] = x;
+	__syncthreads();
+	uint32_t pre = 0, tot = 0;
+	for (uint32_t q = 0; q < BPB / 64u; q++) {
+		const uint32_t w = wsum[q];
+		pre += q < wv ? w : 0u;
+		tot += w;
+	}
+	__syncthreads();
+	if (total)
+		*total = tot;
+	return pre + x - v;
+}
+
+/* exclusive prefix maximum of v (-1: none) */
+__device__ __forceinline__ int32_t bp_excl_max(int32_t v, int32_t *wmax)
+{
+	const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	int32_t x = v;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const int32_t u = __shfl_up(x, d);
+		if (lane >= (uint32_t)d)
+			x = max(x, u);
+	}
+	if (lane == 63)
+		wmax[wv] = x;
+	int32_t below = __shfl_up(x, 1);
+	if (lane == 0)
+		below = -1;
+	__syncthreads();
+	int32_t pre = -1;
+	for (uint32_t q = 0; q < wv; q++)
+		pre = max(pre, wmax[q]);
+	__syncthreads();
+	return max(pre, below);
+}
+
+/* the last-workgroup hand-off (cdna_hip_programming.md, the split-K
+ * reducer recipe): every wave's stores drained, then one release fence and
+ * one agent-scope ticket per workgroup; the workgroup drawing the last
+ * ticket acquires before it reads the others' words */
+__device__ __forceinline__ bool bp_last(uint32_t *ticket, uint32_t tbase,
+					uint32_t nblk, uint32_t *flag)
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		const uint32_t t = __hip_atomic_fetch_add(ticket, 1u,
+							  __ATOMIC_RELAXED,
+							  __HIP_MEMORY_SCOPE_AGENT);
+		*flag = (t - tbase) == nblk - 1u;
+		if (*flag) {
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+	}
+	__syncthreads();
+	return *flag != 0;
+}
+
+static_assert(sizeof(struct sgpu_sstate) == 32 &&
+	      offsetof(struct sgpu_sstate, flags) == 12,
+	      "bp_ld/bp_st move the state as two 16-byte words");
+
+__device__ __forceinline__ struct sgpu_sstate bp_ld(const struct sgpu_sstate *p)
+{
+	const uint4 a = ((const uint4 *)p)[0], b = ((const uint4 *)p)[1];
+	struct sgpu_sstate s;
+	s.ssrc = a.x; s.roc = a.y; s.s_l = a.z; s.flags = a.w;
+	s.lix = (uint64_t)b.y << 32 | b.x;
+	s.bitmap = (uint64_t)b.w << 32 | b.z;
+	return s;
+}
+
+__device__ __forceinline__ void bp_st(struct sgpu_sstate *p,
+				      const struct sgpu_sstate &s)
+{
+	((uint4 *)p)[0] = make_uint4(s.ssrc, s.roc, s.s_l, s.flags);
+	((uint4 *)p)[1] = make_uint4((uint32_t)s.lix, (uint32_t)(s.lix >> 32),
+				     (uint32_t)s.bitmap,
+				     (uint32_t)(s.bitmap >> 32));
+}
+
+/* ---- 1: parse, checks, bucket scatter --------------------------------- */
+
+__global__ void __launch_bounds__(BPB)
+k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
+	     const struct sgpu_bplan P)
+{
+	__shared__ uint32_t hist[SGPU_BP_NBMAX], base[SGPU_BP_NBMAX];
+	__shared__ uint32_t bf;
+	const uint32_t tid = threadIdx.x, nb = P.nb;
+	for (uint32_t k = tid; k < nb; k += BPB)
+		hist[k] = 0;
+	if (tid == 0) {
+		bf = 0;
+		if (blockIdx.x == 0)
+			*P.nfail = 0;   /* the crypto launch's miss counter */
+	}
+	__syncthreads();
+	uint32_t bk[SGPU_BP_PPT], rk[SGPU_BP_PPT], wd[SGPU_BP_PPT];
+	uint32_t f = 0;
+#pragma unroll
+	for (int j = 0; j < SGPU_BP_PPT; j++) {
+		const uint32_t i = blockIdx.x * (BPB * SGPU_BP_PPT) + j * BPB + tid;
+		bk[j] = 0xffffffffu;
+		rk[j] = wd[j] = 0;
+		if (i >= P.n)
+			continue;
+		const uint32_t p = P.pos[i], e = P.end[i];
+		const uint32_t c = P.capv ? P.capv[i] : 0u;
+		uint32_t s = P.sess[i];
+		P.es[i] = e;
+		/* a window outside the arena is never read */
+		const uint32_t left = (e > p && e <= asz) ? e - p : 0u;
+		const struct sgpu_hdr h = parse_rtp_hdr(arena + p, p, left);
+		P.hdr[i] = h;
+		/* the window checks of k_mp_count (via k_parse_rtp_checked) */
+		if (h.hdr_len == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (!P.prot && e - p - h.hdr_len < P.tag)
+			f |= SPF_PARSE;
+		if (e - p >= P.maxlen)
+			f |= SPF_SIZE;
+		if ((p & 3u) || p > e || e > asz ||
+		    (P.capv && (e > c || c > asz)))
+			f |= SPF_BAD;
+		if (P.prot && P.capv && (uint64_t)e + P.need > (uint64_t)c)
+			f |= SPF_CAP;
+		if (s >= P.nsess) {
+			f |= SPF_BAD;
+			s = P.nsess - 1u;
+		}
+		/* the crypto launch order's class: descending 64-B chunks */
+		const uint32_t L = e >= p ? e - p : 0u, ch = (L + 63u) >> 6;
+		const uint32_t bin = (BP_OBINS - 1u) -
+				     (ch < BP_OBINS - 1u ? ch : BP_OBINS - 1u);
+		bk[j] = s >> P.bshift;
+		rk[j] = atomicAdd(&hist[bk[j]], 1u);
+		wd[j] = i | bin << 26;
+	}
+	if (blockIdx.x == 0 && tid == 0 && P.pred && *P.pred)
+		f |= SPF_PRED;          /* sgpu_gate_pred */
+	__syncthreads();
+	for (uint32_t k = tid; k < nb; k += BPB)
+		base[k] = hist[k] ? atomicAdd(&P.bcount[k], hist[k]) : 0u;
+	__syncthreads();
+#pragma unroll
+	for (int j = 0; j < SGPU_BP_PPT; j++) {
+		if (bk[j] == 0xffffffffu)
+			continue;
+		const uint32_t slot = base[bk[j]] + rk[j];
+		if (slot < P.cap)
+			P.tmp[(size_t)bk[j] * P.cap + slot] = wd[j];
+		else
+			f |= SPF_SEG;   /* the bucket overflows: radix re-plan */
+	}
+	if (f)
+		atomicOr(&bf, f);
+	__syncthreads();
+	if (tid == 0)
+		P.afail[blockIdx.x] = bf;
+}
+
+/* ---- 2: per bucket, the plan ------------------------------------------ */
+
+struct BpPlanLds {
+	uint32_t ent[SGPU_BP_CAPMAX];   /* entry word, arrival order in bucket */
+	uint16_t sq[SGPU_BP_CAPMAX];    /* seq */
+	uint16_t srt[SGPU_BP_CAPMAX];   /* rank in session, then: entries by
+					   (session, packet index) */
+	uint16_t un[SGPU_BP_CAPMAX];    /* entries by session (unstable) */
+	uint16_t pw[SGPU_BP_CAPMAX];    /* rank in length bin, then: rollovers
+					   up to and including position k */
+	uint8_t sl[SGPU_BP_CAPMAX];     /* session in bucket */
+	struct sgpu_sstate st[SGPU_BP_NSB];
+	uint32_t cnt[SGPU_BP_NSB], start[SGPU_BP_NSB];
+	uint32_t smin[SGPU_BP_NSB], smax[SGPU_BP_NSB];
+	uint32_t bh[BP_OBINS], bb[BP_OBINS];
+	uint32_t wsum[BPB / 64];
+	uint32_t bf, hl0, flag, fail;
+};
+
+/* speculated s_l seen by sorted position k (its segment starting at f):
+ * the previous packet's seq, or the session's stored s_l (a new stream:
+ * its first packet's seq, stream.c:87-109) */
+__device__ __forceinline__ uint32_t bp_sb(const BpPlanLds &S, uint32_t k,
+					  uint32_t f, uint32_t l)
+{
+	if (k != f)
+		return S.sq[S.srt[k - 1]];
+	return (S.st[l].flags & SST_SL_SET) ? S.st[l].s_l : S.sq[S.srt[k]];
+}
+
+/* index of sorted position k (mp_ix of plan_multi.hip) */
+__device__ __forceinline__ uint64_t bp_ix(const BpPlanLds &S, uint32_t prot,
+					  uint32_t k, uint32_t f, uint32_t l,
+					  uint32_t *flp, uint32_t *rocp,
+					  bool *wrapp, uint32_t *sbp)
+{
+	const uint32_t seq = S.sq[S.srt[k]];
+	const uint32_t sb = bp_sb(S, k, f, l);
+	const bool wrap = plan_wrap(seq, sb);
+	const bool wf = plan_wrap(S.sq[S.srt[f]], bp_sb(S, f, f, l));
+	/* ROC after this packet's own rollover */
+	const uint32_t roc = S.st[l].roc + S.pw[k] - (S.pw[f] - (wf ? 1u : 0u));
+	uint64_t ix;
+	uint32_t fl = SD_RUN | SD_CIPHER;
+	if (prot) {
+		ix = 65536ull * roc + seq;                   /* srtp.c:215 */
+	}
+	else {
+		const int32_t v = plan_v(roc, wrap ? 0u : sb, seq);
+		ix = seq + (uint64_t)(int64_t)v * 65536ull;
+		if ((uint32_t)v != roc)
+			fl |= (uint32_t)v + 1u == roc ? SD_ROC_P1 : SD_ROC_M1;
+	}
+	if (flp)
+		*flp = fl;
+	if (rocp)
+		*rocp = roc;
+	if (wrapp)
+		*wrapp = wrap;
+	if (sbp)
+		*sbp = sb;
+	return ix;
+}
+
+__global__ void __launch_bounds__(BPB)
+k_bp_plan(const struct sgpu_bplan P)
+{
+	__shared__ BpPlanLds S;
+	const uint32_t tid = threadIdx.x, b = blockIdx.x;
+	const uint32_t s0 = b << P.bshift;
+	const uint32_t ns = min(1u << P.bshift, P.nsess - s0);
+	const uint32_t EPT = P.cap / BPB;
+	uint32_t m = P.bcount[b];
+	uint32_t f = 0;
+	if (m > P.cap) {
+		f |= SPF_SEG;           /* (the scatter flagged it too) */
+		m = 0;
+	}
+	/* the bucket's place in the launch order: the entries before it */
+	uint32_t acc = 0;
+	for (uint32_t k = tid; k < b; k += BPB)
+		acc += min(P.bcount[k], P.cap);
+	if (tid == 0) {
+		S.bf = 0;
+		S.hl0 = P.hdr[0].hdr_len;
+	}
+	if (tid < BP_OBINS)
+		S.bh[tid] = 0;
+	if (tid < ns) {
+		/* the session's resident state (k_sst_load): the host's upload
+		 * first where the device copy is stale */
+		const uint32_t s = s0 + tid, slot = P.cm[s] >> 1;
+		struct sgpu_sstate x;
+		if (P.upneed && P.upneed[s]) {
+			x = bp_ld(P.up + s);
+			bp_st(P.sst + slot, x);
+		}
+		else {
+			x = bp_ld(P.sst + slot);
+		}
+		S.st[tid] = x;
+		S.cnt[tid] = 0;
+		S.smin[tid] = 0xffffffffu;
+		S.smax[tid] = 0;
+	}
+	/* (the sum's barriers also publish the LDS writes above) */
+	uint32_t bucket_base;
+	(void)bp_excl_sum(acc, S.wsum, &bucket_base);
+	const uint32_t hl0 = S.hl0;
+	/* the entries: header, session, rank in session and length bin */
+	for (uint32_t k = tid; k < m; k += BPB) {
+		const uint32_t w = P.tmp[(size_t)b * P.cap + k];
+		const uint32_t i = w & BP_IMASK;
+		const struct sgpu_hdr h = P.hdr[i];
+		uint32_t s = P.sess[i];
+		if (s >= P.nsess)
+			s = P.nsess - 1u;       /* SPF_BAD from the scatter */
+		const uint32_t l = s - s0;
+		S.ent[k] = w;
+		S.sq[k] = h.seq;
+		S.sl[k] = (uint8_t)l;
+		S.srt[k] = (uint16_t)atomicAdd(&S.cnt[l], 1u);
+		S.pw[k] = (uint16_t)atomicAdd(&S.bh[w >> 26], 1u);
+		atomicMin(&S.smin[l], h.ssrc);
+		atomicMax(&S.smax[l], h.ssrc);
+		if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (((h.hdr_len ^ hl0) >> 2) & 3u)
+			f |= SPF_CLASS;
+	}
+	__syncthreads();
+	/* segment starts (sessions, <= 256: wave 0) and length-bin starts
+	 * (64: wave 1) */
+	if (tid < 64) {
+		uint32_t c4[4], v = 0;
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t l = 4 * tid + q;
+			c4[q] = l < ns ? S.cnt[l] : 0u;
+			v += c4[q];
+		}
+		uint32_t x = v;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t u = (uint32_t)__shfl_up((int)x, d);
+			if (tid >= (uint32_t)d)
+				x += u;
+		}
+		uint32_t run = x - v;
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const uint32_t l = 4 * tid + q;
+			if (l < SGPU_BP_NSB)
+				S.start[l] = run;
+			run += c4[q];
+		}
+	}
+	else if (tid < 128) {
+		const uint32_t lane = tid - 64, v = S.bh[lane];
+		uint32_t x = v;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t u = (uint32_t)__shfl_up((int)x, d);
+			if (lane >= (uint32_t)d)
+				x += u;
+		}
+		S.bb[lane] = x - v;
+	}
+	/* one SSRC per session: the stored one, or the segment's
+	 * (k_mp_count's SPF_SSRC, order-free) */
+	if (tid < ns && S.cnt[tid]) {
+		const struct sgpu_sstate &x = S.st[tid];
+		if (S.smin[tid] != S.smax[tid] ||
+		    ((x.flags & SST_EXISTS) && S.smin[tid] != x.ssrc))
+			f |= SPF_SSRC;
+		if (S.cnt[tid] > SGPU_BP_SEGMAX)
+			f |= SPF_SEG;
+	}
+	if (f)
+		atomicOr(&S.bf, f);
+	__syncthreads();
+	const bool dead = S.bf != 0;    /* the plan fails: nothing more */
+	if (!dead) {
+		/* grouped by session; the crypto launch order (bucket-major,
+		 * descending length bins inside the bucket) */
+		for (uint32_t k = tid; k < m; k += BPB) {
+			S.un[S.start[S.sl[k]] + S.srt[k]] = (uint16_t)k;
+			P.order[bucket_base + S.bb[S.ent[k] >> 26] + S.pw[k]] =
+				S.ent[k] & BP_IMASK;
+		}
+	}
+	__syncthreads();
+	if (!dead) {
+		/* inside a session by packet index: the stable order the
+		 * reference processes them in */
+		for (uint32_t q = tid; q < m; q += BPB) {
+			const uint32_t e = S.un[q], l = S.sl[e];
+			const uint32_t f0 = S.start[l], c = S.cnt[l];
+			const uint32_t ie = S.ent[e] & BP_IMASK;
+			uint32_t r = 0;
+			for (uint32_t t = f0; t < f0 + c; t++)
+				r += (S.ent[S.un[t]] & BP_IMASK) < ie ? 1u : 0u;
+			S.srt[f0 + r] = (uint16_t)e;
+		}
+	}
+	__syncthreads();
+	/* rollovers up to each sorted position (EPT consecutive positions per
+	 * thread; the sum runs across segments, bp_ix takes differences) */
+	uint32_t loc = 0, wbits = 0;
+	if (!dead) {
+		for (uint32_t j = 0; j < EPT; j++) {
+			const uint32_t k = tid * EPT + j;
+			if (k >= m)
+				break;
+			const uint32_t l = S.sl[S.srt[k]];
+			const bool w = plan_wrap(S.sq[S.srt[k]],
+						 bp_sb(S, k, S.start[l], l));
+			wbits |= (w ? 1u : 0u) << j;
+			loc += w ? 1u : 0u;
+		}
+	}
+	{
+		uint32_t run = bp_excl_sum(loc, S.wsum, NULL);
+		if (!dead)
+			for (uint32_t j = 0; j < EPT; j++) {
+				const uint32_t k = tid * EPT + j;
+				if (k >= m)
+					break;
+				run += (wbits >> j) & 1u;
+				S.pw[k] = (uint16_t)run;
+			}
+	}
+	__syncthreads();
+	if (!dead) {
+		/* per packet: the checks of k_mp_count that need the order,
+		 * the index, the replay speculation, desc (k_mp_desc) */
+		for (uint32_t k = tid; k < m; k += BPB) {
+			const uint32_t e = S.srt[k], l = S.sl[e];
+			const uint32_t f0 = S.start[l];
+			const bool last = k + 1 == f0 + S.cnt[l];
+			const uint32_t i = S.ent[e] & BP_IMASK;
+			const uint32_t seq = S.sq[e];
+			uint32_t fl, sb;
+			bool wrap;
+			const uint64_t ix = bp_ix(S, P.prot, k, f0, l, &fl, NULL,
+						  &wrap, &sb);
+			if (!P.prot && (int)seq - (int)sb > 32768)
+				f |= SPF_TIMEOUT;
+			if (!last && !wrap && seq < sb)
+				f |= SPF_ORDER;
+			if (!P.prot) {
+				/* replay: every packet new (replay.c:32-62),
+				 * above the session's pre-batch lix as well */
+				const struct sgpu_sstate &x = S.st[l];
+				bool ok;
+				if (k == f0) {
+					if (ix > x.lix) {
+						ok = true;
+					}
+					else {
+						const uint64_t d = x.lix - ix;
+						ok = d < 64 && !(x.bitmap & (1ull << d));
+					}
+				}
+				else {
+					ok = ix > bp_ix(S, 0, k - 1, f0, l, NULL, NULL,
+							NULL, NULL) && ix > x.lix;
+				}
+				if (!ok)
+					f |= SPF_REPLAY;
+			}
+			P.desc[i] = d_desc(ix, fl);
+			P.sorted[(size_t)b * P.cap + k] = i;
+		}
+	}
+	/* every session's state after the batch (k_mp_final) */
+	if (tid < ns) {
+		const uint32_t s = s0 + tid, c = S.cnt[tid];
+		struct sgpu_sstate o = S.st[tid];
+		o.flags &= ~(uint32_t)SST_TOUCHED;
+		if (c && !dead) {
+			const uint32_t f0 = S.start[tid], l = f0 + c - 1u;
+			uint32_t roc, sb;
+			bool wrap;
+			(void)bp_ix(S, P.prot, l, f0, tid, NULL, &roc, &wrap, &sb);
+			const uint32_t seq = S.sq[S.srt[l]];
+			const struct sgpu_sstate &x = S.st[tid];
+			o.ssrc = (x.flags & SST_EXISTS) ? x.ssrc : S.smin[tid];
+			o.roc = roc;
+			o.s_l = wrap ? seq : (seq > sb ? seq : sb);
+			o.flags = SST_EXISTS | SST_SL_SET | SST_TOUCHED;
+			if (!P.prot) {
+				/* the window over the last <= 65 indices (older
+				 * bits have shifted out: every index is new and
+				 * increasing) */
+				uint64_t lix = x.lix, bm = x.bitmap;
+				uint32_t k = f0;
+				if (l - f0 + 1u > 65u) {
+					k = l - 64u;
+					lix = bp_ix(S, 0, k - 1u, f0, tid, NULL, NULL,
+						    NULL, NULL);
+					bm = 1;
+				}
+				for (; k <= l; k++) {
+					const uint64_t ix = bp_ix(S, 0, k, f0, tid,
+								  NULL, NULL, NULL,
+								  NULL);
+					if (ix > lix) {
+						const uint64_t d = ix - lix;
+						bm = d < 64 ? (bm << d) | 1ull : 1ull;
+						lix = ix;
+					}
+					else {
+						bm |= 1ull << (lix - ix);
+					}
+				}
+				o.lix = lix;
+				o.bitmap = bm;
+			}
+			P.sseg[s] = f0 | c << 16;
+		}
+		else {
+			P.sseg[s] = 0;
+		}
+		bp_st(P.sout + s, o);
+	}
+	if (f)
+		atomicOr(&S.bf, f);
+	__syncthreads();
+	if (tid == 0)
+		P.bfail[b] = S.bf;
+	if (!bp_last(&P.tickets[0], P.tb, P.nb, &S.flag))
+		return;
+	/* the last workgroup: every fail word into the plan out, the guards
+	 * of the crypto launches, the bucket counters back to zero */
+	if (tid == 0)
+		S.fail = 0;
+	__syncthreads();
+	{
+		const uint32_t na = (P.n + BPB * SGPU_BP_PPT - 1) /
+				    (BPB * SGPU_BP_PPT);
+		uint32_t x = 0;
+		for (uint32_t k = tid; k < na; k += BPB)
+			x |= __hip_atomic_load(&P.afail[k], __ATOMIC_RELAXED,
+					       __HIP_MEMORY_SCOPE_AGENT);
+		for (uint32_t k = tid; k < P.nb; k += BPB)
+			x |= __hip_atomic_load(&P.bfail[k], __ATOMIC_RELAXED,
+					       __HIP_MEMORY_SCOPE_AGENT);
+		if (x)
+			atomicOr(&S.fail, x);
+	}
+	for (uint32_t k = tid; k < P.nb; k += BPB)
+		P.bcount[k] = 0;
+	__syncthreads();
+	if (tid == 0) {
+		const uint32_t fl = S.fail, h0 = S.hl0;
+		struct sgpu_plan_out *o = P.out;
+		o->fail = fl;
+		o->wraps = 0;
+		o->ssrc0 = 0;
+		o->hl0 = h0;
+		o->s_l_last = 0;
+		o->nfail = 0;
+		for (int q = 0; q < 4; q++)
+			o->skip[q] = fl || (((h0 >> 2) & 3u) != (uint32_t)q);
+	}
+}
+
+/* ---- 3: results, commit, verdict fold --------------------------------- */
+
+struct BpFoldLds {
+	uint32_t idx[SGPU_BP_CAPMAX];   /* packet of sorted position k */
+	uint16_t sq[SGPU_BP_CAPMAX];
+	int16_t ev[SGPU_BP_CAPMAX];     /* last event position <= k, or -1 */
+	uint8_t au[SGPU_BP_CAPMAX];     /* tag verified */
+	uint8_t sl[SGPU_BP_CAPMAX];     /* session in bucket */
+	struct sgpu_sstate st[SGPU_BP_NSB];     /* before the batch */
+	uint32_t f0[SGPU_BP_NSB], cnt[SGPU_BP_NSB];
+	int32_t wmax[BPB / 64];
+	uint32_t m, cf, flag, ff;
+};
+
+/* the s_l a segment starts from (stream_get_seq, stream.c:87-109) */
+__device__ __forceinline__ uint32_t bf_sl0(const BpFoldLds &S, uint32_t l)
+{
+	return (S.st[l].flags & SST_SL_SET) ? S.st[l].s_l : S.sq[S.f0[l]];
+}
+
+/* speculated s_l of position k */
+__device__ __forceinline__ uint32_t bf_sb(const BpFoldLds &S, uint32_t k,
+					  uint32_t l)
+{
+	return k == S.f0[l] ? bf_sl0(S, l) : S.sq[k - 1];
+}
+
+/* true s_l after event position e (before the segment: its start) */
+__device__ __forceinline__ uint32_t bf_slv(const BpFoldLds &S, int32_t e,
+					   uint32_t l)
+{
+	if (e < (int32_t)S.f0[l])
+		return bf_sl0(S, l);
+	return S.au[e] ? S.sq[e] : 0u;
+}
+
+/* forged packet i: srtp_decrypt's EAUTH (srtp.c:342-359: HMAC, end at
+ * the tag; 404-411: GCM, end as it was) */
+__device__ __forceinline__ void bp_forged(const struct sgpu_bplan &P,
+					  uint32_t i)
+{
+	P.err[i] = EAUTH;
+	P.posw[i] += P.hdr[i].hdr_len;
+	P.endw[i] = P.gcm ? P.es[i] : P.es[i] + (uint32_t)P.delta;
+}
+
+__global__ void __launch_bounds__(BPB)
+k_bp_finish(const struct sgpu_bplan P)
+{
+	__shared__ BpFoldLds S;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t fail = P.out->fail;
+	const uint32_t nf = *(volatile const uint32_t *)P.nfail;
+	if (blockIdx.x >= P.nb) {
+		/* per packet (coalesced): every authentic packet's results
+		 * (k_plan_finish); forged ones wait for the fold */
+		if (fail)
+			return;
+		const uint32_t i0 = (blockIdx.x - P.nb) * (BPB * SGPU_BP_PPT);
+#pragma unroll
+		for (int j = 0; j < SGPU_BP_PPT; j++) {
+			const uint32_t i = i0 + j * BPB + tid;
+			if (i >= P.n)
+				break;
+			if (P.prot || !nf || (P.verdict[i] & SV_TAG_OK)) {
+				P.endw[i] = P.es[i] + (uint32_t)P.delta;
+				P.err[i] = 0;
+			}
+		}
+		return;
+	}
+	const uint32_t b = blockIdx.x;
+	const uint32_t s0 = b << P.bshift;
+	const uint32_t ns = min(1u << P.bshift, P.nsess - s0);
+	const uint32_t EPT = P.cap / BPB;
+	if (tid == 0) {
+		S.cf = 0;
+		S.m = 0;
+	}
+	__syncthreads();
+	if (!fail && !nf) {
+		/* every tag verified: the touched states replace the resident
+		 * ones (k_sst_commit) */
+		if (tid < ns) {
+			const uint32_t s = s0 + tid;
+			struct sgpu_sstate o = bp_ld(P.sout + s);
+			if (o.flags & SST_TOUCHED) {
+				o.flags &= ~(uint32_t)SST_TOUCHED;
+				bp_st(P.sst + (P.cm[s] >> 1), o);
+			}
+		}
+	}
+	else if (!fail) {
+		/* the verdict fold of this bucket's sessions (k_mf_count /
+		 * scan / check / final): a forged packet still bumps the ROC
+		 * on a rollover but never sets s_l (srtp.c:310-321, 342-359,
+		 * 426-427), so later packets of its session may see another
+		 * s_l than the plan assumed */
+		if (tid < ns) {
+			const uint32_t s = s0 + tid, v = P.sseg[s];
+			S.st[tid] = bp_ld(P.sst + (P.cm[s] >> 1));
+			S.f0[tid] = v & 0xffffu;
+			S.cnt[tid] = v >> 16;
+			if (v >> 16)
+				atomicMax(&S.m, (v & 0xffffu) + (v >> 16));
+			for (uint32_t k = v & 0xffffu; k < (v & 0xffffu) + (v >> 16);
+			     k++)
+				S.sl[k] = (uint8_t)tid;
+		}
+		__syncthreads();
+		const uint32_t m = S.m;
+		for (uint32_t k = tid; k < m; k += BPB) {
+			const uint32_t i = P.sorted[(size_t)b * P.cap + k];
+			S.idx[k] = i;
+			S.sq[k] = P.hdr[i].seq;
+			S.au[k] = (P.verdict[i] & SV_TAG_OK) ? 1 : 0;
+		}
+		__syncthreads();
+		/* events: an authentic packet (s_l = seq) or a rollover (s_l =
+		 * 0 when forged); the last one at or before each position */
+		int32_t loc = -1;
+		for (uint32_t j = 0; j < EPT; j++) {
+			const uint32_t k = tid * EPT + j;
+			if (k >= m)
+				break;
+			const uint32_t l = S.sl[k];
+			if (S.au[k] || plan_wrap(S.sq[k], bf_sb(S, k, l)))
+				loc = (int32_t)k;
+		}
+		{
+			int32_t run = bp_excl_max(loc, S.wmax);
+			for (uint32_t j = 0; j < EPT; j++) {
+				const uint32_t k = tid * EPT + j;
+				if (k >= m)
+					break;
+				const uint32_t l = S.sl[k];
+				if (S.au[k] || plan_wrap(S.sq[k], bf_sb(S, k, l)))
+					run = (int32_t)k;
+				S.ev[k] = (int16_t)run;
+			}
+		}
+		__syncthreads();
+		uint32_t cf = 0;
+		for (uint32_t k = tid; k < m; k += BPB) {
+			const uint32_t l = S.sl[k];
+			const int32_t e = k ? S.ev[k - 1] : -1;
+			const uint32_t seq = S.sq[k];
+			const uint32_t sb = bf_sb(S, k, l);     /* speculated */
+			const uint32_t sv = bf_slv(S, e, l);    /* true */
+			const bool wrap = plan_wrap(seq, sb);
+			bool bad = plan_wrap(seq, sv) != wrap ||
+				   (int)seq - (int)sv > 32768;  /* ETIMEDOUT */
+			if (!bad && !wrap) {
+				/* the same index estimate (misc.c:22-41) */
+				bad = plan_v(65536u, sv, seq) !=
+				      plan_v(65536u, sb, seq);
+				/* an authentic packet sets s_l = seq only if
+				 * seq > s_l (srtp.c:426-427) */
+				if (S.au[k] && seq < sv)
+					bad = true;
+			}
+			if (bad)
+				cf = 1;
+		}
+		if (P.nofold)
+			cf = 1;         /* srtp_gpu_tune nodevfold */
+		/* each touched session's s_l and replay window after the batch
+		 * (the authentic packets only) */
+		if (tid < ns && S.cnt[tid]) {
+			const uint32_t s = s0 + tid, f0 = S.f0[tid];
+			const uint32_t l = f0 + S.cnt[tid] - 1u;
+			struct sgpu_sstate o = bp_ld(P.sout + s);
+			o.s_l = bf_slv(S, S.ev[l], tid);
+			const struct sgpu_sstate &x = S.st[tid];
+			int32_t j = (int32_t)l;
+			while (j >= (int32_t)f0 && !S.au[j])
+				j--;
+			uint64_t lix = x.lix, bm = x.bitmap;
+			if (j >= (int32_t)f0) {
+				uint32_t q = f0;
+				if ((uint32_t)j - f0 >= 64u) {
+					q = (uint32_t)j - 63u;
+					const uint64_t d = P.desc[S.idx[q - 1]];
+					lix = (d & 0xffffull) |
+					      ((d >> 16) & 0xffffffffull) << 16;
+					bm = 0;
+				}
+				for (; q <= (uint32_t)j; q++) {
+					if (!S.au[q])
+						continue;
+					const uint64_t d = P.desc[S.idx[q]];
+					const uint64_t ix = (d & 0xffffull) |
+						((d >> 16) & 0xffffffffull) << 16;
+					if (ix > lix) {
+						const uint64_t dl = ix - lix;
+						bm = dl < 64 ? (bm << dl) | 1ull : 1ull;
+						lix = ix;
+					}
+					else {
+						bm |= 1ull << (lix - ix);
+					}
+				}
+			}
+			o.lix = lix;
+			o.bitmap = bm;
+			bp_st(P.sout + s, o);
+		}
+		if (cf)
+			atomicOr(&S.cf, 1u);
+		__syncthreads();
+		if (tid == 0)
+			P.cfail[b] = S.cf;
+	}
+	if (!bp_last(&P.tickets[1], P.tc, P.nb, &S.flag))
+		return;
+	/* the last workgroup: the call's outcome */
+	if (tid == 0)
+		S.ff = 0;
+	__syncthreads();
+	if (!fail && nf) {
+		uint32_t x = 0;
+		for (uint32_t k = tid; k < P.nb; k += BPB)
+			x |= __hip_atomic_load(&P.cfail[k], __ATOMIC_RELAXED,
+					       __HIP_MEMORY_SCOPE_AGENT);
+		if (x)
+			atomicOr(&S.ff, 1u);
+		__syncthreads();
+		if (!S.ff) {
+			/* the fold holds: the states and the forged packets'
+			 * results (a fold that fails leaves all to the host) */
+			for (uint32_t s = tid; s < P.nsess; s += BPB) {
+				struct sgpu_sstate o = bp_ld(P.sout + s);
+				if (o.flags & SST_TOUCHED) {
+					o.flags &= ~(uint32_t)SST_TOUCHED;
+					bp_st(P.sst + (P.cm[s] >> 1), o);
+				}
+			}
+			if (P.flist) {
+				for (uint32_t q = tid; q < nf; q += BPB)
+					bp_forged(P, P.flist[q]);
+			}
+			else {
+				for (uint32_t i = tid; i < P.n; i += BPB)
+					if (!(P.verdict[i] & SV_TAG_OK))
+						bp_forged(P, i);
+			}
+		}
+	}
+	if (tid == 0) {
+		const uint32_t ff = S.ff;
+		struct sgpu_fold_out *fo = P.fo;
+		fo->fail = ff;
+		fo->nok = 0;
+		fo->first_ok = 0xffffffffu;
+		fo->last_ok = 0xffffffffu;
+		fo->s_l = 0;
+		fo->pad = 0;
+		fo->lix = 0;
+		fo->bitmap = 0;
+		P.out->nfail = nf;
+		if (P.gate)     /* sgpu_gate_set: completed here, or not */
+			*P.gate = (fail || (nf && ff)) ? 1u : 0u;
+	}
+}
+
+/* ---- host side ------------------------------------------------------ */
+
+static size_t bp_align(size_t x)
+{
+	return (x + 255) & ~(size_t)255;
+}
+
+extern "C" int sgpu_bplan_geometry(uint32_t n, uint32_t nsess,
+				   uint32_t *bshift, uint32_t *nb,
+				   uint32_t *cap)
+{
+	if (n == 0 || n > SGPU_BP_NMAX || nsess < 2)
+		return -1;
+	/* the most sessions per bucket (<= 256) that keep the expected
+	 * entries per bucket <= 4096; at most SGPU_BP_NBMAX buckets */
+	for (int sh = 8; sh >= 0; sh--) {
+		const uint64_t nbk = ((uint64_t)nsess + (1ull << sh) - 1) >> sh;
+		const uint64_t exp = ((uint64_t)n << sh) / nsess + 1;
+		if (nbk > SGPU_BP_NBMAX)
+			return -1;      /* fewer sessions per bucket: more */
+		if (exp > 4096)
+			continue;
+		uint64_t c = 2 * exp + 1024;
+		c = (c + BPB - 1) / BPB * BPB;
+		if (c > SGPU_BP_CAPMAX)
+			c = SGPU_BP_CAPMAX;
+		*bshift = (uint32_t)sh;
+		*nb = (uint32_t)nbk;
+		*cap = (uint32_t)c;
+		return 0;
+	}
+	return -1;
+}
+
+extern "C" size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
+				     uint32_t cap)
+{
+	const size_t na = (n + BPB * SGPU_BP_PPT - 1) / (BPB * SGPU_BP_PPT);
+	return 2 * bp_align((size_t)nb * cap * 4) + /* tmp, sorted */
+	       bp_align((size_t)nb * 4) + 256 +      /* bcount, tickets */
+	       bp_align(na * 4) + 2 * bp_align((size_t)nb * 4) + /* fails */
+	       bp_align((size_t)nsess * 4) +         /* sseg */
+	       bp_align((size_t)nsess * 32);         /* sout */
+}
+
+static int bp_check(const struct sgpu_bplan *b)
+{
+	if (!b->n || b->n > SGPU_BP_NMAX || b->nsess < 2 || !b->nb ||
+	    b->nb > SGPU_BP_NBMAX || b->bshift > 8 || !b->cap ||
+	    b->cap > SGPU_BP_CAPMAX || b->cap % BPB ||
+	    ((uint64_t)b->nb << b->bshift) < b->nsess ||
+	    ((uint64_t)(b->nb - 1) << b->bshift) >= b->nsess)
+		return EINVAL;
+	return 0;
+}
+
+static int bp_err(const char *what)
+{
+	const hipError_t e = hipGetLastError();
+	if (e == hipSuccess)
+		return 0;
+	fprintf(stderr, "re_srtp: %s launch: %s\n", what, hipGetErrorString(e));
+	return EIO;
+}
+
+extern "C" int sgpu_bplan_scatter(const uint8_t *arena, uint64_t arena_size,
+				  const struct sgpu_bplan *b, void *stream)
+{
+	if (bp_check(b))
+		return EINVAL;
+	const uint32_t g = (b->n + BPB * SGPU_BP_PPT - 1) / (BPB * SGPU_BP_PPT);
+	hipLaunchKernelGGL(k_bp_scatter, dim3(g), dim3(BPB), 0,
+			   (hipStream_t)stream, arena, arena_size, *b);
+	return bp_err("k_bp_scatter");
+}
+
+extern "C" int sgpu_bplan_plan(const struct sgpu_bplan *b, void *stream)
+{
+	if (bp_check(b))
+		return EINVAL;
+	hipLaunchKernelGGL(k_bp_plan, dim3(b->nb), dim3(BPB), 0,
+			   (hipStream_t)stream, *b);
+	return bp_err("k_bp_plan");
+}
+
+extern "C" int sgpu_bplan_finish(const struct sgpu_bplan *b, void *stream)
+{
+	if (bp_check(b))
+		return EINVAL;
+	const uint32_t g = (b->n + BPB * SGPU_BP_PPT - 1) / (BPB * SGPU_BP_PPT);
+	hipLaunchKernelGGL(k_bp_finish, dim3(b->nb + g), dim3(BPB), 0,
+			   (hipStream_t)stream, *b);
+	return bp_err("k_bp_finish");
+}

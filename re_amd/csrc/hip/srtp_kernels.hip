@@ -651,6 +651,11 @@ static struct sgpu_sstate *g_sst;       /* per slot: RTP stream 0 state of
 					   resident multi-session batches */
 static uint32_t g_table_cap;
 static struct sgpu_keyreq *g_req_dev;
+
+extern "C" struct sgpu_sstate *sgpu_sst_table(void)
+{
+	return g_sst;
+}
 static uint32_t *g_slot_dev;
 static uint32_t g_req_cap;
 

@@ -910,8 +910,213 @@ static int mfold(struct dcall *k, int phase, const uint32_t *nfail,
 			      d->stream);
 }
 
+/*
+ * The bucket planner (plan_buckets.hip, srtpgpu.h struct sgpu_bplan): the
+ * same plan, verdict fold and resident states as below, in three launches
+ * around the crypto instead of ~17 plus the fold's five.
+ *
+ * w->bp: ticket words | bucket counters (BP_HEAD, zero between calls) |
+ * bucket entries | sorted | fail words | sseg | sout | launch order
+ */
+#define BP_HEAD (256u + 4u * SGPU_BP_NBMAX)
+
+static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
+			      uint32_t cap)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp **sessv = k->sessv;
+	const size_t nsess = k->nsess;
+	struct srtp_batch_dev *d = &k->d;
+	struct ws *w = k->w;
+	const struct comp *c0 = &sessv[0]->rtp;
+	const size_t n = d->n;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const uint32_t T = gcm ? 16u : c0->tag_len;
+	const size_t na = (n + SGPU_BP_BLOCK * SGPU_BP_PPT - 1) /
+			  (SGPU_BP_BLOCK * SGPU_BP_PPT);
+	struct sgpu_bplan *B = &k->bp;
+	struct sgpu_sstate *up_h, *up_d;
+	uint8_t *need_h, *need_d, *p;
+	uint32_t *cm_h;
+	void *stream = d->stream;
+	const int times = g_env.times;
+	int err;
+
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 8);
+	if (!err)   /* nfail | save | verdict | forged list */
+		err = pool_reserve(w, &w->vs, n * 9 + 72);
+	if (!err)
+		err = pool_reserve(w, &w->cm, nsess * 4);
+	k->foff = (sizeof(struct sgpu_plan_out) + 63) & ~(size_t)63;
+	if (!err)   /* plan out | fold out */
+		err = pool_reserve(w, &w->pl, k->foff + 64);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)   /* uploads | need */
+		err = pool_reserve(w, &w->ms,
+				   nsess * (sizeof(struct sgpu_sstate) + 1));
+	if (!err)
+		err = pool_reserve(w, &w->bp, BP_HEAD +
+				   sgpu_bplan_scratch((uint32_t)n,
+						      (uint32_t)nsess, nb, cap) +
+				   n * 4 + 256);
+	if (err)
+		return err;
+	if (w->bp_d != w->bp.d) {
+		/* a new pool (or a call that did not finish): counters and
+		 * tickets from zero */
+		err = sgpu_memset(w->bp.d, 0, BP_HEAD, stream);
+		if (err)
+			return err;
+		w->bp_d = w->bp.d;
+		w->bp_tb = w->bp_tc = 0;
+	}
+	memset(B, 0, sizeof(*B));
+	B->n = (uint32_t)n;
+	B->nsess = (uint32_t)nsess;
+	B->prot = (uint32_t)prot;
+	B->tag = T;
+	B->need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
+	B->maxlen = SGPU_CACHED_MAX(c0->mode);
+	B->bshift = bshift;
+	B->nb = nb;
+	B->cap = cap;
+	B->tb = w->bp_tb;
+	B->tc = w->bp_tc;
+	B->delta = prot ? (int32_t)T : -(int32_t)T;
+	B->gcm = (uint32_t)gcm;
+	k->devfold = !prot && !g_env.nodevfold;
+	B->nofold = (uint32_t)!k->devfold;
+	B->pos = d->pos;
+	B->end = d->end;
+	B->capv = d->cap;
+	B->sess = d->sess;
+	B->posw = d->pos;
+	B->endw = d->end;
+	B->err = d->err;
+	B->es = (uint32_t *)w->es.d;
+	B->hdr = (struct sgpu_hdr *)w->hd.d;
+	B->desc = (uint64_t *)w->dsc.d;
+	p = w->bp.d;
+	B->tickets = (uint32_t *)p;
+	B->bcount = (uint32_t *)(p + 256);
+	p += BP_HEAD;
+#define BP_TAKE(ptr, bytes)                                                  \
+	do {                                                                 \
+		(ptr) = (void *)p;                                           \
+		p += ((size_t)(bytes) + 255) & ~(size_t)255;                 \
+	} while (0)
+	BP_TAKE(B->tmp, (size_t)nb * cap * 4);
+	BP_TAKE(B->sorted, (size_t)nb * cap * 4);
+	BP_TAKE(B->afail, na * 4);
+	BP_TAKE(B->bfail, (size_t)nb * 4);
+	BP_TAKE(B->cfail, (size_t)nb * 4);
+	BP_TAKE(B->sseg, nsess * 4);
+	BP_TAKE(B->sout, nsess * sizeof(struct sgpu_sstate));
+	BP_TAKE(B->order, n * 4);
+#undef BP_TAKE
+	B->sst = sgpu_sst_table();
+	B->out = (struct sgpu_plan_out *)w->pl.d;
+	B->fo = (struct sgpu_fold_out *)(w->pl.d + k->foff);
+	B->pred = k->pred;
+	B->gate = k->gate;
+	B->nfail = (uint32_t *)w->vs.d;
+	B->verdict = w->vs.d + 64 + n * 4;
+	B->flist = !prot && !gcm && k->devfold ?
+		   (uint32_t *)(w->vs.d + ((64 + n * 5 + 3) & ~(size_t)3)) : NULL;
+	/* parse, checks, bucket slots: no session state needed, so it runs
+	 * while the host walks the sessions */
+	err = sgpu_bplan_scatter(d->arena, d->arena_size, B, stream);
+	if (err) {
+		w->bp_d = NULL;
+		return err;
+	}
+	cm_h = (uint32_t *)w->cm.h;
+	up_h = (struct sgpu_sstate *)w->ms.h;
+	need_h = (uint8_t *)(up_h + nsess);
+	up_d = (struct sgpu_sstate *)w->ms.d;
+	need_d = (uint8_t *)(up_d + nsess);
+	k->t[0] = times ? now_ms() : 0;
+	if (mplan_gather_res(sessv, nsess, up_h, cm_h, need_h, &k->nup,
+			     k->pend, k->done)) {
+		/* the scatter only wrote scratch -- and the bucket counters,
+		 * zeroed again before the workspace's next call */
+		w->bp_d = NULL;
+		err = sgpu_stream_sync(stream);
+		return err ? err : -1;
+	}
+	k->t[1] = times ? now_ms() : 0;
+	/* the slot map and the states the device lacks go up on the
+	 * workspace's own stream (overlapping the kernels queued before on the
+	 * call's stream); the call's stream waits for them before the plan */
+	if (!w->upev)
+		w->upev = sgpu_event_create();
+	if (!w->upev) {
+		w->bp_d = NULL;
+		sgpu_stream_sync(stream);
+		return ENOMEM;
+	}
+	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->stream);
+	if (!err && k->nup)
+		err = sgpu_memcpy_h2d(up_d, up_h,
+				      nsess * (sizeof(struct sgpu_sstate) + 1),
+				      w->stream);
+	if (!err)
+		err = sgpu_event_record(w->upev, w->stream);
+	if (!err)
+		err = sgpu_stream_wait(stream, w->upev);
+	if (err) {
+		/* no copy may still read the host buffers */
+		sgpu_stream_sync(w->stream);
+		w->bp_d = NULL;
+		return err;
+	}
+	B->cm = (const uint32_t *)w->cm.d;
+	B->upneed = k->nup ? need_d : NULL;
+	B->up = up_d;
+	err = sgpu_bplan_plan(B, stream);
+	if (!err) {
+		w->bp_tb += nb;
+		/* the crypto launches behind the plan's guards, in its order */
+		struct sgpu_compact C = {
+			d->pos, B->es, B->hdr, B->desc, d->sess,
+			(const uint32_t *)w->cm.d, B->order, 0, (uint32_t)n,
+			(uint8_t *)B->verdict, (uint32_t *)(w->vs.d + 64),
+			B->nfail, 0, 0, NULL, 0, (uint32_t *)B->flist};
+		err = run_classes(d->arena, d->arena_size, C, c0,
+				  B->out, prot, stream);
+	}
+	if (!err) {
+		err = sgpu_bplan_finish(B, stream);
+		if (!err)
+			w->bp_tc += nb;
+	}
+	if (err) {
+		w->bp_d = NULL;
+		return err;
+	}
+	/* plan out and fold out in one copy */
+	err = sgpu_memcpy_d2h(w->pl.h, w->pl.d, k->foff + sizeof(struct sgpu_fold_out),
+			      stream);
+	k->t[2] = times ? now_ms() : 0;
+	return err;
+}
+
 int dev_mplanned_issue(struct dcall *k)
 {
+	{
+		uint32_t bsh, nb, cap;
+		if (!k->radix && !g_env.mpradix && !g_env.nobucket &&
+		    !sgpu_bplan_geometry((uint32_t)k->d.n, (uint32_t)k->nsess,
+					 &bsh, &nb, &cap)) {
+			k->bucket = 1;
+			return dev_bplanned_issue(k, bsh, nb, cap);
+		}
+		k->bucket = 0;
+	}
+
 	const int prot = k->op == OP_RTP_ENC;
 	struct srtp **sessv = k->sessv;
 	const size_t nsess = k->nsess;

@@ -240,6 +240,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.splan = value > 0;
 	else if (!strcmp(name, "nomk"))
 		g_env.nomk = value > 0;
+	else if (!strcmp(name, "nobucket"))
+		g_env.nobucket = value > 0;
 	else if (!strcmp(name, "mpradix"))
 		g_env.mpradix = value > 0;
 	else if (!strcmp(name, "nocoop"))

@@ -92,6 +92,9 @@ struct srtp_env {
 				   the general per-lane-key kernel */
 	int splan;              /* srtp_gpu_tune splan: single-session RTP
 				   batches through the per-stream planner */
+	int nobucket;           /* srtp_gpu_tune nobucket: multi-session plans
+				   by the counting grouping (plan_multi.hip),
+				   not the bucket planner (plan_buckets.hip) */
 	int mpradix;            /* srtp_gpu_tune mpradix: multi-session plans
 				   group by the radix sort (not counting) */
 	int nodevfold;          /* RE_SRTP_NODEVFOLD: forged packets in a
@@ -218,6 +221,13 @@ struct ws {
 	uint32_t *sm_cnt;       /* device */
 	uint32_t *sm_flag;      /* pinned host */
 	uint32_t sm_seq;
+	/* multi-session batches of the bucket planner (plan_buckets.hip):
+	 * bucket entries | sorted | counters | tickets | fail words | sseg |
+	 * sout; the counters and tickets are zero between calls */
+	struct pool bp;
+	uint8_t *bp_d;          /* bp.d the ticket bases below belong to */
+	uint32_t bp_nb;         /* ... and the geometry they were laid out for */
+	uint32_t bp_tb, bp_tc;  /* the next launches' first tickets */
 };
 
 struct mbc {
@@ -322,6 +332,8 @@ struct dcall {
 	int fused;              /* single stream planned inside the crypto
 				   launch (fz_issue / fz_finish) */
 	struct sgpu_fused fz;   /* ... its launch */
+	int bucket;             /* many sessions: the bucket planner */
+	struct sgpu_bplan bp;   /* ... its launches */
 };
 
 /* srtp.c */

@@ -494,6 +494,94 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 		     void *stream);
 
 /*
+ * Multi-session device planning in four launches (plan_buckets.hip): the
+ * sessions are cut into nb buckets of 2^bshift consecutive session ids,
+ * each bucket has a fixed region of cap entries, so no global scan is
+ * needed before a packet is placed:
+ *   sgpu_bplan_scatter  per packet: header parse (rtp_hdr_decode), window
+ *                       checks, end copy; its bucket slot by an atomic per
+ *                       (workgroup, bucket), the entry packed as
+ *                       index | length bin << 26 (SPF_SEG past cap)
+ *   sgpu_bplan_plan     per bucket (one workgroup): the sessions' resident
+ *                       states (+ uploads), the entries sorted by session
+ *                       and packet index in LDS, the speculation of
+ *                       sgpu_plan_rtp per session segment (srtp.c:203-215,
+ *                       310-321, misc.c:22-41, replay.c:32-62), desc, the
+ *                       crypto launch order (bucket-major, descending
+ *                       length bins), each session's state after the
+ *                       batch; the last workgroup folds every fail word
+ *                       into out (fail, hl0, skip[]) and re-zeroes the
+ *                       bucket counters
+ *   (crypto, in `order`; unprotect CTR: the forged-packet restore)
+ *   sgpu_bplan_finish   the results (end, err) per packet, the commit of
+ *                       the touched sessions' states; with speculation
+ *                       misses the verdict fold per bucket (the fold of
+ *                       sgpu_mfold_rtp), the last workgroup then writes
+ *                       the forged packets' EAUTH results and commits --
+ *                       or leaves everything for the host (fo->fail);
+ *                       gate word, out->nfail
+ * bcount / tickets must be zero before the first launch of a workspace
+ * (each launch pair leaves them so); tb / tc: the ticket bases (+ nb per
+ * launch).
+ */
+#define SGPU_BP_BLOCK 1024
+#define SGPU_BP_PPT 4           /* scatter: packets per thread */
+#define SGPU_BP_CAPMAX 8192     /* entries per bucket */
+#define SGPU_BP_NSB 256         /* sessions per bucket, at most */
+#define SGPU_BP_NBMAX 4096      /* buckets, at most */
+#define SGPU_BP_NMAX (1u << 26) /* packets per call, at most */
+#define SGPU_BP_SEGMAX 1024     /* packets of one session per bucket pass */
+struct sgpu_bplan {
+	uint32_t n, nsess, prot, tag, need, maxlen;
+	uint32_t bshift, nb, cap;       /* bucket geometry */
+	uint32_t tb, tc;                /* ticket bases of plan / finish */
+	int32_t delta;                  /* end change of a processed packet */
+	uint32_t gcm;
+	uint32_t nofold;                /* misses are left to the host fold */
+	const uint32_t *pos, *end, *capv, *sess;
+	uint32_t *posw;                 /* = pos (EAUTH: pos += header) */
+	uint32_t *endw;                 /* = end (results) */
+	int32_t *err;
+	uint32_t *es;                   /* end before the call */
+	struct sgpu_hdr *hdr;
+	uint64_t *desc;
+	uint32_t *order;                /* crypto launch order (n) */
+	uint32_t *tmp;                  /* nb x cap bucket entries */
+	uint32_t *sorted;               /* nb x cap: packet index by session */
+	uint32_t *bcount;               /* nb: entries per bucket (zeroed) */
+	uint32_t *tickets;              /* 2: plan, finish (zeroed once) */
+	uint32_t *afail;                /* per scatter workgroup */
+	uint32_t *bfail;                /* per bucket (plan) */
+	uint32_t *cfail;                /* per bucket (fold) */
+	uint32_t *sseg;                 /* per session: start | count << 16 */
+	const uint32_t *cm;             /* session -> comp index (2 slot) */
+	const uint8_t *upneed;          /* or NULL: upload up[s] first */
+	const struct sgpu_sstate *up;
+	struct sgpu_sstate *sst;        /* resident states by slot */
+	struct sgpu_sstate *sout;       /* per session, after the batch */
+	struct sgpu_plan_out *out;
+	struct sgpu_fold_out *fo;
+	const uint32_t *pred;           /* async chain: the call before's gate */
+	uint32_t *gate;                 /* or NULL */
+	uint32_t *nfail;                /* the crypto launch's miss counter
+					   (zeroed by the scatter) */
+	const uint8_t *verdict;
+	const uint32_t *flist;          /* CTR: forged packets, or NULL */
+};
+size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
+			  uint32_t cap);
+/* geometry for n packets over nsess sessions: 0 and bshift/nb/cap, or -1
+ * (the bucket planner does not take the batch) */
+int   sgpu_bplan_geometry(uint32_t n, uint32_t nsess, uint32_t *bshift,
+			  uint32_t *nb, uint32_t *cap);
+/* the resident state table (sgpu_sst_*) */
+struct sgpu_sstate *sgpu_sst_table(void);
+int   sgpu_bplan_scatter(const uint8_t *arena, uint64_t arena_size,
+			 const struct sgpu_bplan *b, void *stream);
+int   sgpu_bplan_plan(const struct sgpu_bplan *b, void *stream);
+int   sgpu_bplan_finish(const struct sgpu_bplan *b, void *stream);
+
+/*
  * Device-side planning of a single-stream SRTCP batch (srtcp_encrypt
  * srtcp.c:31-140, srtcp_decrypt srtcp.c:143-287): protect numbers the
  * packets rtcp_index + 1, + 2, ...; unprotect reads E || index from each

@@ -915,10 +915,11 @@ static int mfold(struct dcall *k, int phase, const uint32_t *nfail,
  * same plan, verdict fold and resident states as below, in three launches
  * around the crypto instead of ~17 plus the fold's five.
  *
- * w->bp: ticket words | bucket counters (BP_HEAD, zero between calls) |
- * bucket entries | sorted | fail words | sseg | sout | launch order
+ * w->bp: ticket words | bin counters | bucket counters (BP_HEAD, zero
+ * between calls) | bucket entries | sorted | fail words | sseg | sout |
+ * launch order | bin places
  */
-#define BP_HEAD (256u + 4u * SGPU_BP_NBMAX)
+#define BP_HEAD (512u + 4u * SGPU_BP_NBMAX)
 
 static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 			      uint32_t cap)
@@ -961,7 +962,7 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		err = pool_reserve(w, &w->bp, BP_HEAD +
 				   sgpu_bplan_scratch((uint32_t)n,
 						      (uint32_t)nsess, nb, cap) +
-				   n * 4 + 256);
+				   2 * (n * 4 + 256));
 	if (err)
 		return err;
 	if (w->bp_d != w->bp.d) {
@@ -1001,7 +1002,8 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	B->desc = (uint64_t *)w->dsc.d;
 	p = w->bp.d;
 	B->tickets = (uint32_t *)p;
-	B->bcount = (uint32_t *)(p + 256);
+	B->obins = (uint32_t *)(p + 64);
+	B->bcount = (uint32_t *)(p + 512);
 	p += BP_HEAD;
 #define BP_TAKE(ptr, bytes)                                                  \
 	do {                                                                 \
@@ -1016,6 +1018,7 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	BP_TAKE(B->sseg, nsess * 4);
 	BP_TAKE(B->sout, nsess * sizeof(struct sgpu_sstate));
 	BP_TAKE(B->order, n * 4);
+	BP_TAKE(B->ooff, n * 4);
 #undef BP_TAKE
 	B->sst = sgpu_sst_table();
 	B->out = (struct sgpu_plan_out *)w->pl.d;

@@ -501,17 +501,19 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  *   sgpu_bplan_scatter  per packet: header parse (rtp_hdr_decode), window
  *                       checks, end copy; its bucket slot by an atomic per
  *                       (workgroup, bucket), the entry packed as
- *                       index | length bin << 26 (SPF_SEG past cap)
+ *                       index | length bin << 26 (SPF_SEG past cap); its
+ *                       place in its length bin likewise (ooff)
  *   sgpu_bplan_plan     per bucket (one workgroup): the sessions' resident
  *                       states (+ uploads), the entries sorted by session
  *                       and packet index in LDS, the speculation of
  *                       sgpu_plan_rtp per session segment (srtp.c:203-215,
  *                       310-321, misc.c:22-41, replay.c:32-62), desc, the
- *                       crypto launch order (bucket-major, descending
- *                       length bins), each session's state after the
- *                       batch; the last workgroup folds every fail word
- *                       into out (fail, hl0, skip[]) and re-zeroes the
- *                       bucket counters
+ *                       crypto launch order (descending length bins, the
+ *                       packets of a scatter workgroup together), each
+ *                       session's state after the batch; the last
+ *                       workgroup folds every fail word into out (fail,
+ *                       hl0, skip[]) and re-zeroes the bucket and bin
+ *                       counters
  *   (crypto, in `order`; unprotect CTR: the forged-packet restore)
  *   sgpu_bplan_finish   the results (end, err) per packet, the commit of
  *                       the touched sessions' states; with speculation
@@ -520,7 +522,7 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  *                       the forged packets' EAUTH results and commits --
  *                       or leaves everything for the host (fo->fail);
  *                       gate word, out->nfail
- * bcount / tickets must be zero before the first launch of a workspace
+ * bcount / obins / tickets must be zero before the first launch of a workspace
  * (each launch pair leaves them so); tb / tc: the ticket bases (+ nb per
  * launch).
  */
@@ -549,6 +551,8 @@ struct sgpu_bplan {
 	uint32_t *tmp;                  /* nb x cap bucket entries */
 	uint32_t *sorted;               /* nb x cap: packet index by session */
 	uint32_t *bcount;               /* nb: entries per bucket (zeroed) */
+	uint32_t *obins;                /* 64: packets per length bin (zeroed) */
+	uint32_t *ooff;                 /* n: a packet's place in its bin */
 	uint32_t *tickets;              /* 2: plan, finish (zeroed once) */
 	uint32_t *afail;                /* per scatter workgroup */
 	uint32_t *bfail;                /* per bucket (plan) */

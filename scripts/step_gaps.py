@@ -16,7 +16,8 @@ CRYPTO = ('k_ctr_fast_any', 'k_ctr_fused', 'k_gcmu', 'k_ctr_fast_mk',
 def is_start(name):
     return ('k_ctr_fast_any<10, true>' in name or
             'k_ctr_fused<10, true>' in name or 'k_gcmu<14, true>' in name or
-            'k_ctr_fast_rtcp<10, true>' in name)
+            'k_ctr_fast_rtcp<10, true>' in name or
+            'k_ctr_fast_mk<10, true>' in name)
 
 
 starts = [k for k, r in enumerate(rows) if is_start(r['Kernel_Name'])]

@@ -166,24 +166,62 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		if (blockIdx.x == 0)
 			*P.nfail = 0;   /* the crypto launch's miss counter */
 	}
-	__syncthreads();
 	uint32_t bk[SGPU_BP_PPT], rk[SGPU_BP_PPT], wd[SGPU_BP_PPT];
 	uint32_t orank[SGPU_BP_PPT];
+	uint32_t pv[SGPU_BP_PPT], ev[SGPU_BP_PPT], cv[SGPU_BP_PPT];
+	uint32_t sv[SGPU_BP_PPT], w0[SGPU_BP_PPT], w2[SGPU_BP_PPT];
 	uint32_t f = 0;
+	const uint32_t i0 = blockIdx.x * (BPB * SGPU_BP_PPT) + tid;
+	/* every window first, then every header's two words: all of a
+	 * thread's loads in flight together */
 #pragma unroll
 	for (int j = 0; j < SGPU_BP_PPT; j++) {
-		const uint32_t i = blockIdx.x * (BPB * SGPU_BP_PPT) + j * BPB + tid;
+		const uint32_t i = i0 + j * BPB;
+		pv[j] = ev[j] = cv[j] = sv[j] = 0;
+		if (i < P.n) {
+			pv[j] = P.pos[i];
+			ev[j] = P.end[i];
+			cv[j] = P.capv ? P.capv[i] : 0u;
+			sv[j] = P.sess[i];
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < SGPU_BP_PPT; j++) {
+		const uint32_t p = pv[j], e = ev[j];
+		w0[j] = w2[j] = 0;
+		/* the batch APIs' 4-byte aligned windows (parse_rtp_hdr's fast
+		 * load); anything else parses byte by byte below */
+		if (i0 + j * BPB < P.n && e > p && e <= asz && e - p >= 12 &&
+		    !(p & 3u)) {
+			w0[j] = *(const uint32_t *)(arena + p);
+			w2[j] = *(const uint32_t *)(arena + p + 8);
+		}
+	}
+	__syncthreads();
+#pragma unroll
+	for (int j = 0; j < SGPU_BP_PPT; j++) {
+		const uint32_t i = i0 + j * BPB;
 		bk[j] = 0xffffffffu;
-		rk[j] = wd[j] = 0;
+		rk[j] = wd[j] = orank[j] = 0;
 		if (i >= P.n)
 			continue;
-		const uint32_t p = P.pos[i], e = P.end[i];
-		const uint32_t c = P.capv ? P.capv[i] : 0u;
-		uint32_t s = P.sess[i];
+		const uint32_t p = pv[j], e = ev[j], c = cv[j];
+		uint32_t s = sv[j];
 		P.es[i] = e;
 		/* a window outside the arena is never read */
 		const uint32_t left = (e > p && e <= asz) ? e - p : 0u;
-		const struct sgpu_hdr h = parse_rtp_hdr(arena + p, p, left);
+		struct sgpu_hdr h;
+		const uint32_t b0 = w0[j] & 0xffu;
+		if (left >= 12 && !(p & 3u) && !(b0 & 0x1fu)) {
+			/* no CSRC, no extension: the header is the two words */
+			h.seq = (uint16_t)((w0[j] >> 8 & 0xff00u) | (w0[j] >> 24));
+			h.ssrc = __builtin_bswap32(w2[j]);
+			h.err_pos = 0;
+			h.hdr_len = 12;
+		}
+		else {
+			h = parse_rtp_hdr(arena + p, p, left);
+		}
 		P.hdr[i] = h;
 		/* the window checks of k_mp_count (via k_parse_rtp_checked) */
 		if (h.hdr_len == 0xffffffffu)
@@ -242,6 +280,8 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 
 /* ---- 2: per bucket, the plan ------------------------------------------ */
 
+#define BP_EPT (SGPU_BP_CAPMAX / BPB)   /* entries per thread, at most */
+
 struct BpPlanLds {
 	uint32_t ent[SGPU_BP_CAPMAX];   /* entry word, arrival order in bucket */
 	uint16_t sq[SGPU_BP_CAPMAX];    /* seq */
@@ -252,22 +292,25 @@ struct BpPlanLds {
 					   sorted position k */
 	uint8_t sl[SGPU_BP_CAPMAX];     /* session in bucket */
 	struct sgpu_sstate st[SGPU_BP_NSB];
+	uint64_t lixl[SGPU_BP_NSB];     /* index of the segment's last packet */
 	uint32_t cnt[SGPU_BP_NSB], start[SGPU_BP_NSB];
 	uint32_t smin[SGPU_BP_NSB], smax[SGPU_BP_NSB];
-	uint32_t bh[BP_OBINS], bb[BP_OBINS];
+	uint32_t sl0[SGPU_BP_NSB];      /* s_l the segment starts from */
+	uint32_t rbase[SGPU_BP_NSB];    /* ROC of position k: rbase + pw[k] */
+	uint32_t froc[SGPU_BP_NSB], fsl[SGPU_BP_NSB];   /* after the batch */
+	uint32_t wlo[SGPU_BP_NSB], whi[SGPU_BP_NSB];    /* replay bits */
+	uint32_t bb[BP_OBINS];
 	uint32_t wsum[BPB / 64];
 	uint32_t bf, hl0, flag, fail;
 };
 
-/* speculated s_l seen by sorted position k (its segment starting at f):
+/* speculated s_l seen by sorted position k (its segment l starting at f):
  * the previous packet's seq, or the session's stored s_l (a new stream:
  * its first packet's seq, stream.c:87-109) */
 __device__ __forceinline__ uint32_t bp_sb(const BpPlanLds &S, uint32_t k,
 					  uint32_t f, uint32_t l)
 {
-	if (k != f)
-		return S.sq[S.srt[k - 1]];
-	return (S.st[l].flags & SST_SL_SET) ? S.st[l].s_l : S.sq[S.srt[k]];
+	return k != f ? S.sq[S.srt[k - 1]] : S.sl0[l];
 }
 
 /* index of sorted position k (mp_ix of plan_multi.hip) */
@@ -279,9 +322,8 @@ __device__ __forceinline__ uint64_t bp_ix(const BpPlanLds &S, uint32_t prot,
 	const uint32_t seq = S.sq[S.srt[k]];
 	const uint32_t sb = bp_sb(S, k, f, l);
 	const bool wrap = plan_wrap(seq, sb);
-	const bool wf = plan_wrap(S.sq[S.srt[f]], bp_sb(S, f, f, l));
 	/* ROC after this packet's own rollover */
-	const uint32_t roc = S.st[l].roc + S.pw[k] - (S.pw[f] - (wf ? 1u : 0u));
+	const uint32_t roc = S.rbase[l] + S.pw[k];
 	uint64_t ix;
 	uint32_t fl = SD_RUN | SD_CIPHER;
 	if (prot) {
@@ -318,12 +360,34 @@ k_bp_plan(const struct sgpu_bplan P)
 		f |= SPF_SEG;           /* (the scatter flagged it too) */
 		m = 0;
 	}
+	/* the entries' loads first (EPT per thread, all in flight), then
+	 * their headers and sessions */
+	uint32_t wv[BP_EPT], seqv[BP_EPT], ssv[BP_EPT], hlv[BP_EPT],
+		 sesv[BP_EPT];
+#pragma unroll
+	for (int j = 0; j < BP_EPT; j++) {
+		const uint32_t k = tid + j * BPB;
+		wv[j] = k < m ? P.tmp[(size_t)b * P.cap + k] : 0u;
+	}
+#pragma unroll
+	for (int j = 0; j < BP_EPT; j++) {
+		const uint32_t k = tid + j * BPB;
+		seqv[j] = ssv[j] = hlv[j] = sesv[j] = 0;
+		if (k < m) {
+			const uint32_t i = wv[j] & BP_IMASK;
+			const uint32_t *hw = (const uint32_t *)(P.hdr + i);
+			ssv[j] = hw[0];
+			seqv[j] = hw[1] & 0xffffu;
+			hlv[j] = hw[2];
+			sesv[j] = P.sess[i];
+		}
+	}
 	if (tid == 0) {
 		S.bf = 0;
 		S.hl0 = P.hdr[0].hdr_len;
 	}
 	if (tid < BP_OBINS)
-		S.bh[tid] = P.obins[tid];       /* the bins' totals */
+		S.bb[tid] = P.obins[tid];       /* the bins' totals */
 	if (tid < ns) {
 		/* the session's resident state (k_sst_load): the host's upload
 		 * first where the device copy is stale */
@@ -340,27 +404,29 @@ k_bp_plan(const struct sgpu_bplan P)
 		S.cnt[tid] = 0;
 		S.smin[tid] = 0xffffffffu;
 		S.smax[tid] = 0;
+		S.wlo[tid] = S.whi[tid] = 0;
 	}
 	__syncthreads();
 	const uint32_t hl0 = S.hl0;
-	/* the entries: header, session, rank in session and length bin */
-	for (uint32_t k = tid; k < m; k += BPB) {
-		const uint32_t w = P.tmp[(size_t)b * P.cap + k];
-		const uint32_t i = w & BP_IMASK;
-		const struct sgpu_hdr h = P.hdr[i];
-		uint32_t s = P.sess[i];
+	/* the entries: seq, session, rank in session */
+#pragma unroll
+	for (int j = 0; j < BP_EPT; j++) {
+		const uint32_t k = tid + j * BPB;
+		if (k >= m)
+			continue;
+		uint32_t s = sesv[j];
 		if (s >= P.nsess)
 			s = P.nsess - 1u;       /* SPF_BAD from the scatter */
 		const uint32_t l = s - s0;
-		S.ent[k] = w;
-		S.sq[k] = h.seq;
+		S.ent[k] = wv[j];
+		S.sq[k] = (uint16_t)seqv[j];
 		S.sl[k] = (uint8_t)l;
 		S.srt[k] = (uint16_t)atomicAdd(&S.cnt[l], 1u);
-		atomicMin(&S.smin[l], h.ssrc);
-		atomicMax(&S.smax[l], h.ssrc);
-		if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
+		atomicMin(&S.smin[l], ssv[j]);
+		atomicMax(&S.smax[l], ssv[j]);
+		if (hlv[j] == 0xffffffffu || hl0 == 0xffffffffu)
 			f |= SPF_PARSE;
-		else if (((h.hdr_len ^ hl0) >> 2) & 3u)
+		else if (((hlv[j] ^ hl0) >> 2) & 3u)
 			f |= SPF_CLASS;
 	}
 	__syncthreads();
@@ -391,7 +457,7 @@ k_bp_plan(const struct sgpu_bplan P)
 		}
 	}
 	else if (tid < 128) {
-		const uint32_t lane = tid - 64, v = S.bh[lane];
+		const uint32_t lane = tid - 64, v = S.bb[lane];
 		uint32_t x = v;
 #pragma unroll
 		for (int d = 1; d < 64; d <<= 1) {
@@ -418,10 +484,14 @@ k_bp_plan(const struct sgpu_bplan P)
 	if (!dead) {
 		/* grouped by session; the crypto launch order (descending
 		 * length bins, each scatter workgroup's packets together) */
-		for (uint32_t k = tid; k < m; k += BPB) {
-			const uint32_t i = S.ent[k] & BP_IMASK;
+#pragma unroll
+		for (int j = 0; j < BP_EPT; j++) {
+			const uint32_t k = tid + j * BPB;
+			if (k >= m)
+				continue;
+			const uint32_t i = wv[j] & BP_IMASK;
 			S.un[S.start[S.sl[k]] + S.srt[k]] = (uint16_t)k;
-			P.order[S.bb[S.ent[k] >> 26] + P.ooff[i]] = i;
+			P.order[S.bb[wv[j] >> 26] + P.ooff[i]] = i;
 		}
 	}
 	__syncthreads();
@@ -439,8 +509,12 @@ k_bp_plan(const struct sgpu_bplan P)
 		}
 	}
 	__syncthreads();
+	if (tid < ns && !dead)
+		S.sl0[tid] = (S.st[tid].flags & SST_SL_SET) ? S.st[tid].s_l
+			     : S.cnt[tid] ? S.sq[S.srt[S.start[tid]]] : 0u;
+	__syncthreads();
 	/* rollovers up to each sorted position (EPT consecutive positions per
-	 * thread; the sum runs across segments, bp_ix takes differences) */
+	 * thread; the sum runs across segments, rbase takes it off) */
 	uint32_t loc = 0, wbits = 0;
 	if (!dead) {
 		for (uint32_t j = 0; j < EPT; j++) {
@@ -466,6 +540,13 @@ k_bp_plan(const struct sgpu_bplan P)
 			}
 	}
 	__syncthreads();
+	if (tid < ns && !dead && S.cnt[tid]) {
+		/* roc(k) = stored ROC + rollovers of positions f..k */
+		const uint32_t f0 = S.start[tid];
+		const bool wf = plan_wrap(S.sq[S.srt[f0]], S.sl0[tid]);
+		S.rbase[tid] = S.st[tid].roc - S.pw[f0] + (wf ? 1u : 0u);
+	}
+	__syncthreads();
 	if (!dead) {
 		/* per packet: the checks of k_mp_count that need the order,
 		 * the index, the replay speculation, desc (k_mp_desc) */
@@ -475,9 +556,9 @@ k_bp_plan(const struct sgpu_bplan P)
 			const bool last = k + 1 == f0 + S.cnt[l];
 			const uint32_t i = S.ent[e] & BP_IMASK;
 			const uint32_t seq = S.sq[e];
-			uint32_t fl, sb;
+			uint32_t fl, sb, roc;
 			bool wrap;
-			const uint64_t ix = bp_ix(S, P.prot, k, f0, l, &fl, NULL,
+			const uint64_t ix = bp_ix(S, P.prot, k, f0, l, &fl, &roc,
 						  &wrap, &sb);
 			if (!P.prot && (int)seq - (int)sb > 32768)
 				f |= SPF_TIMEOUT;
@@ -504,55 +585,60 @@ k_bp_plan(const struct sgpu_bplan P)
 				if (!ok)
 					f |= SPF_REPLAY;
 			}
+			if (last) {
+				/* the session after the batch (k_mp_final) */
+				S.froc[l] = roc;
+				S.fsl[l] = wrap ? seq : (seq > sb ? seq : sb);
+				S.lixl[l] = ix;
+			}
 			P.desc[i] = d_desc(ix, fl);
 			P.sorted[(size_t)b * P.cap + k] = i;
 		}
 	}
-	/* every session's state after the batch (k_mp_final) */
+	__syncthreads();
+	if (!dead && !P.prot) {
+		/* the replay window after the batch (replay.c:32-62): every
+		 * index is new and increasing (checked above), so it holds the
+		 * batch's indices within 64 of the last one and the stored
+		 * window shifted up to it -- each packet sets its own bit */
+		for (uint32_t k = tid; k < m; k += BPB) {
+			const uint32_t e = S.srt[k], l = S.sl[e];
+			const uint32_t f0 = S.start[l];
+			if (k + 64u < f0 + S.cnt[l])
+				continue;       /* 64 or more packets before the
+						   last: shifted out */
+			const uint64_t top = S.lixl[l] > S.st[l].lix ?
+					     S.lixl[l] : S.st[l].lix;
+			const uint64_t d = top - bp_ix(S, 0, k, f0, l, NULL, NULL,
+						       NULL, NULL);
+			if (d < 32)
+				atomicOr(&S.wlo[l], 1u << d);
+			else if (d < 64)
+				atomicOr(&S.whi[l], 1u << (d - 32));
+		}
+	}
+	__syncthreads();
+	/* every session's state after the batch */
 	if (tid < ns) {
 		const uint32_t s = s0 + tid, c = S.cnt[tid];
 		struct sgpu_sstate o = S.st[tid];
 		o.flags &= ~(uint32_t)SST_TOUCHED;
 		if (c && !dead) {
-			const uint32_t f0 = S.start[tid], l = f0 + c - 1u;
-			uint32_t roc, sb;
-			bool wrap;
-			(void)bp_ix(S, P.prot, l, f0, tid, NULL, &roc, &wrap, &sb);
-			const uint32_t seq = S.sq[S.srt[l]];
 			const struct sgpu_sstate &x = S.st[tid];
 			o.ssrc = (x.flags & SST_EXISTS) ? x.ssrc : S.smin[tid];
-			o.roc = roc;
-			o.s_l = wrap ? seq : (seq > sb ? seq : sb);
+			o.roc = S.froc[tid];
+			o.s_l = S.fsl[tid];
 			o.flags = SST_EXISTS | SST_SL_SET | SST_TOUCHED;
 			if (!P.prot) {
-				/* the window over the last <= 65 indices (older
-				 * bits have shifted out: every index is new and
-				 * increasing) */
-				uint64_t lix = x.lix, bm = x.bitmap;
-				uint32_t k = f0;
-				if (l - f0 + 1u > 65u) {
-					k = l - 64u;
-					lix = bp_ix(S, 0, k - 1u, f0, tid, NULL, NULL,
-						    NULL, NULL);
-					bm = 1;
-				}
-				for (; k <= l; k++) {
-					const uint64_t ix = bp_ix(S, 0, k, f0, tid,
-								  NULL, NULL, NULL,
-								  NULL);
-					if (ix > lix) {
-						const uint64_t d = ix - lix;
-						bm = d < 64 ? (bm << d) | 1ull : 1ull;
-						lix = ix;
-					}
-					else {
-						bm |= 1ull << (lix - ix);
-					}
-				}
-				o.lix = lix;
+				const uint64_t top = S.lixl[tid] > x.lix ?
+						     S.lixl[tid] : x.lix;
+				uint64_t bm = (uint64_t)S.whi[tid] << 32 | S.wlo[tid];
+				if (top - x.lix < 64)
+					bm |= x.bitmap << (top - x.lix);
+				o.lix = top;
 				o.bitmap = bm;
 			}
-			P.sseg[s] = f0 | c << 16;
+			P.sseg[s] = S.start[tid] | c << 16;
 		}
 		else {
 			P.sseg[s] = 0;
@@ -567,7 +653,7 @@ k_bp_plan(const struct sgpu_bplan P)
 	if (!bp_last(&P.tickets[0], P.tb, P.nb, &S.flag))
 		return;
 	/* the last workgroup: every fail word into the plan out, the guards
-	 * of the crypto launches, the bucket counters back to zero */
+	 * of the crypto launches, the bucket and bin counters back to zero */
 	if (tid == 0)
 		S.fail = 0;
 	__syncthreads();
@@ -882,13 +968,14 @@ extern "C" int sgpu_bplan_geometry(uint32_t n, uint32_t nsess,
 	if (n == 0 || n > SGPU_BP_NMAX || nsess < 2)
 		return -1;
 	/* the most sessions per bucket (<= 256) that keep the expected
-	 * entries per bucket <= 4096; at most SGPU_BP_NBMAX buckets */
+	 * entries per bucket <= SGPU_BP_EXP (a workgroup of 1024 lanes: ~one
+	 * packet each, two workgroups per CU); at most SGPU_BP_NBMAX buckets */
 	for (int sh = 8; sh >= 0; sh--) {
 		const uint64_t nbk = ((uint64_t)nsess + (1ull << sh) - 1) >> sh;
 		const uint64_t exp = ((uint64_t)n << sh) / nsess + 1;
 		if (nbk > SGPU_BP_NBMAX)
 			return -1;      /* fewer sessions per bucket: more */
-		if (exp > 4096)
+		if (exp > SGPU_BP_EXP)
 			continue;
 		uint64_t c = 2 * exp + 1024;
 		c = (c + BPB - 1) / BPB * BPB;

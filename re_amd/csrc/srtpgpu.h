@@ -528,7 +528,10 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  */
 #define SGPU_BP_BLOCK 1024
 #define SGPU_BP_PPT 4           /* scatter: packets per thread */
-#define SGPU_BP_CAPMAX 8192     /* entries per bucket */
+#define SGPU_BP_CAPMAX 4096     /* entries per bucket */
+#define SGPU_BP_EXP 1088        /* expected entries per bucket, at most
+				   (64K sessions x 1M packets: 64 sessions,
+				   ~1025 entries per bucket) */
 #define SGPU_BP_NSB 256         /* sessions per bucket, at most */
 #define SGPU_BP_NBMAX 4096      /* buckets, at most */
 #define SGPU_BP_NMAX (1u << 26) /* packets per call, at most */

@@ -660,6 +660,8 @@ __device__ __forceinline__ void ctr_refix_body(const KArgs &a, uint8_t *smem)
 __device__ __forceinline__ int fast_class(const KArgs &a)
 {
 	prof_guard(a);
+	if (a.c.gfail && *a.c.gfail)
+		return -1;              /* the bucket planner's plan failed */
 	const uint32_t *g = a.c.guard;
 	return !g[3] ? 3 : !g[0] ? 0 : !g[1] ? 1 : !g[2] ? 2 : -1;
 }

@@ -316,9 +316,12 @@ struct KArgs {
  * behind every launch */
 __device__ __forceinline__ void prof_guard(const KArgs &a)
 {
-	if (a.pguard && a.c.guard && blockIdx.x == 0 && threadIdx.x == 0)
+	if (a.pguard && a.c.guard && blockIdx.x == 0 && threadIdx.x == 0) {
+		/* a set second guard word voids every class */
+		const bool gf = a.c.gfail && *a.c.gfail;
 		for (uint32_t q = 0; q < a.pguard_n; q++)
-			a.pguard[q] = a.c.guard[q];
+			a.pguard[q] = gf ? 1u : a.c.guard[q];
+	}
 }
 
 /*

@@ -163,8 +163,17 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		oh[tid] = 0;
 	if (tid == 0) {
 		bf = 0;
-		if (blockIdx.x == 0)
-			*P.nfail = 0;   /* the crypto launch's miss counter */
+		if (blockIdx.x == 0) {
+			/* the call's outs: nothing else writes them before the
+			 * plan kernel (the crypto launch's miss counter too) */
+			*P.nfail = 0;
+			P.out->fail = 0;
+			P.out->wraps = 0;
+			P.out->ssrc0 = 0;
+			P.out->s_l_last = 0;
+			P.out->nfail = 0;
+			P.fo->fail = 0;
+		}
 	}
 	uint32_t bk[SGPU_BP_PPT], rk[SGPU_BP_PPT], wd[SGPU_BP_PPT];
 	uint32_t orank[SGPU_BP_PPT];
@@ -223,6 +232,14 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 			h = parse_rtp_hdr(arena + p, p, left);
 		}
 		P.hdr[i] = h;
+		if (i == 0) {
+			/* the crypto launches' class guards (out->fail is their
+			 * second guard word, final after the plan kernel) */
+			P.out->hl0 = h.hdr_len;
+			for (uint32_t q = 0; q < 4; q++)
+				P.out->skip[q] = h.hdr_len == 0xffffffffu ||
+						 ((h.hdr_len >> 2) & 3u) != q;
+		}
 		/* the window checks of k_mp_count (via k_parse_rtp_checked) */
 		if (h.hdr_len == 0xffffffffu)
 			f |= SPF_PARSE;
@@ -301,7 +318,7 @@ struct BpPlanLds {
 	uint32_t wlo[SGPU_BP_NSB], whi[SGPU_BP_NSB];    /* replay bits */
 	uint32_t bb[BP_OBINS];
 	uint32_t wsum[BPB / 64];
-	uint32_t bf, hl0, flag, fail;
+	uint32_t bf, hl0;
 };
 
 /* speculated s_l seen by sorted position k (its segment l starting at f):
@@ -356,6 +373,14 @@ k_bp_plan(const struct sgpu_bplan P)
 	const uint32_t EPT = P.cap / BPB;
 	uint32_t m = P.bcount[b];
 	uint32_t f = 0;
+	{
+		/* the scatter workgroups' fail words, spread over the buckets
+		 * (no workgroup waits for another) */
+		const uint32_t na = (P.n + BPB * SGPU_BP_PPT - 1) /
+				    (BPB * SGPU_BP_PPT);
+		for (uint32_t k = b + tid * P.nb; k < na; k += BPB * P.nb)
+			f |= P.afail[k];
+	}
 	if (m > P.cap) {
 		f |= SPF_SEG;           /* (the scatter flagged it too) */
 		m = 0;
@@ -648,45 +673,8 @@ k_bp_plan(const struct sgpu_bplan P)
 	if (f)
 		atomicOr(&S.bf, f);
 	__syncthreads();
-	if (tid == 0)
-		P.bfail[b] = S.bf;
-	if (!bp_last(&P.tickets[0], P.tb, P.nb, &S.flag))
-		return;
-	/* the last workgroup: every fail word into the plan out, the guards
-	 * of the crypto launches, the bucket and bin counters back to zero */
-	if (tid == 0)
-		S.fail = 0;
-	__syncthreads();
-	{
-		const uint32_t na = (P.n + BPB * SGPU_BP_PPT - 1) /
-				    (BPB * SGPU_BP_PPT);
-		uint32_t x = 0;
-		for (uint32_t k = tid; k < na; k += BPB)
-			x |= __hip_atomic_load(&P.afail[k], __ATOMIC_RELAXED,
-					       __HIP_MEMORY_SCOPE_AGENT);
-		for (uint32_t k = tid; k < P.nb; k += BPB)
-			x |= __hip_atomic_load(&P.bfail[k], __ATOMIC_RELAXED,
-					       __HIP_MEMORY_SCOPE_AGENT);
-		if (x)
-			atomicOr(&S.fail, x);
-	}
-	for (uint32_t k = tid; k < P.nb; k += BPB)
-		P.bcount[k] = 0;
-	if (tid < BP_OBINS)
-		P.obins[tid] = 0;
-	__syncthreads();
-	if (tid == 0) {
-		const uint32_t fl = S.fail, h0 = S.hl0;
-		struct sgpu_plan_out *o = P.out;
-		o->fail = fl;
-		o->wraps = 0;
-		o->ssrc0 = 0;
-		o->hl0 = h0;
-		o->s_l_last = 0;
-		o->nfail = 0;
-		for (int q = 0; q < 4; q++)
-			o->skip[q] = fl || (((h0 >> 2) & 3u) != (uint32_t)q);
-	}
+	if (tid == 0 && S.bf)
+		atomicOr(&P.out->fail, S.bf);
 }
 
 /* ---- 3: results, commit, verdict fold --------------------------------- */
@@ -767,12 +755,32 @@ k_bp_finish(const struct sgpu_bplan P)
 	if (tid == 0) {
 		S.cf = 0;
 		S.m = 0;
+		/* the scatter's counters back to zero for the next call (the
+		 * plan kernel, their last reader, is done) */
+		P.bcount[b] = 0;
+	}
+	if (b == 0 && tid < BP_OBINS)
+		P.obins[tid] = 0;
+	if (b == 0 && tid == 0 && (fail || !nf)) {
+		/* nothing to fold: the call's outcome is known */
+		struct sgpu_fold_out *fo = P.fo;
+		fo->fail = 0;
+		fo->nok = 0;
+		fo->first_ok = 0xffffffffu;
+		fo->last_ok = 0xffffffffu;
+		fo->s_l = 0;
+		fo->pad = 0;
+		fo->lix = 0;
+		fo->bitmap = 0;
+		P.out->nfail = nf;
+		if (P.gate)     /* sgpu_gate_set */
+			*P.gate = fail ? 1u : 0u;
 	}
 	__syncthreads();
-	if (!fail && !nf) {
+	if (fail || !nf) {
 		/* every tag verified: the touched states replace the resident
 		 * ones (k_sst_commit) */
-		if (tid < ns) {
+		if (!fail && tid < ns) {
 			const uint32_t s = s0 + tid;
 			struct sgpu_sstate o = bp_ld(P.sout + s);
 			if (o.flags & SST_TOUCHED) {
@@ -780,8 +788,9 @@ k_bp_finish(const struct sgpu_bplan P)
 				bp_st(P.sst + (P.cm[s] >> 1), o);
 			}
 		}
+		return;
 	}
-	else if (!fail) {
+	{
 		/* the verdict fold of this bucket's sessions (k_mf_count /
 		 * scan / check / final): a forged packet still bumps the ROC
 		 * on a rollover but never sets s_l (srtp.c:310-321, 342-359,
@@ -899,23 +908,20 @@ k_bp_finish(const struct sgpu_bplan P)
 		if (cf)
 			atomicOr(&S.cf, 1u);
 		__syncthreads();
-		if (tid == 0)
-			P.cfail[b] = S.cf;
+		if (tid == 0 && S.cf)
+			atomicOr(&P.fo->fail, 1u);
 	}
-	if (!bp_last(&P.tickets[1], P.tc, P.nb, &S.flag))
+	/* the last bucket workgroup: the fold's outcome (the ticket is taken
+	 * only on this path, and reset by the last taker) */
+	if (!bp_last(P.ticket, 0u, P.nb, &S.flag))
 		return;
-	/* the last workgroup: the call's outcome */
-	if (tid == 0)
-		S.ff = 0;
+	if (tid == 0) {
+		S.ff = __hip_atomic_load(&P.fo->fail, __ATOMIC_RELAXED,
+					 __HIP_MEMORY_SCOPE_AGENT);
+		*P.ticket = 0;
+	}
 	__syncthreads();
-	if (!fail && nf) {
-		uint32_t x = 0;
-		for (uint32_t k = tid; k < P.nb; k += BPB)
-			x |= __hip_atomic_load(&P.cfail[k], __ATOMIC_RELAXED,
-					       __HIP_MEMORY_SCOPE_AGENT);
-		if (x)
-			atomicOr(&S.ff, 1u);
-		__syncthreads();
+	{
 		if (!S.ff) {
 			/* the fold holds: the states and the forged packets'
 			 * results (a fold that fails leaves all to the host) */
@@ -940,7 +946,7 @@ k_bp_finish(const struct sgpu_bplan P)
 	if (tid == 0) {
 		const uint32_t ff = S.ff;
 		struct sgpu_fold_out *fo = P.fo;
-		fo->fail = ff;
+		fo->fail = ff ? 1u : 0u;
 		fo->nok = 0;
 		fo->first_ok = 0xffffffffu;
 		fo->last_ok = 0xffffffffu;
@@ -950,7 +956,7 @@ k_bp_finish(const struct sgpu_bplan P)
 		fo->bitmap = 0;
 		P.out->nfail = nf;
 		if (P.gate)     /* sgpu_gate_set: completed here, or not */
-			*P.gate = (fail || (nf && ff)) ? 1u : 0u;
+			*P.gate = ff ? 1u : 0u;
 	}
 }
 
@@ -994,8 +1000,7 @@ extern "C" size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
 {
 	const size_t na = (n + BPB * SGPU_BP_PPT - 1) / (BPB * SGPU_BP_PPT);
 	return 2 * bp_align((size_t)nb * cap * 4) + /* tmp, sorted */
-	       bp_align((size_t)nb * 4) + 256 +      /* bcount, tickets */
-	       bp_align(na * 4) + 2 * bp_align((size_t)nb * 4) + /* fails */
+	       bp_align(na * 4) +                    /* afail */
 	       bp_align((size_t)nsess * 4) +         /* sseg */
 	       bp_align((size_t)nsess * 32);         /* sout */
 }

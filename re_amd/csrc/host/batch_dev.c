@@ -108,7 +108,7 @@ int dev_planned_issue(struct dcall *k)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1, NULL, 0, flist_d};
+			save_d, nfail_d, 0, 1, NULL, 0, flist_d, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -214,7 +214,7 @@ int dev_planned_finish(struct dcall *k)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 1, NULL, 0, NULL};
+			save_d, nfail_d, 1, 1, NULL, 0, NULL, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -646,7 +646,7 @@ int dev_splanned_issue(struct dcall *k)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 0, 1, NULL, 0, NULL};
+			save_d, nfail_d, 0, 1, NULL, 0, NULL, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  &po_d->base, prot, stream);
 	}
@@ -699,7 +699,7 @@ int dev_splanned_finish(struct dcall *k)
 			(uint64_t *)w->dsc.d, NULL, (const uint32_t *)w->cm.d,
 			NULL, 0, (uint32_t)n, w->vs.d + 64 + n * 4,
 			(uint32_t *)(w->vs.d + 64), (uint32_t *)w->vs.d, 1, 1,
-			NULL, 0, NULL};
+			NULL, 0, NULL, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0, &po_d->base,
 				  prot, d->stream);
 	}
@@ -819,7 +819,7 @@ int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
 			save_d, nfail_d, 0, gcm || g_env.nolean ? 1 : 4,
-			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL};
+			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL, NULL};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
 	}
@@ -863,7 +863,7 @@ int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 			d->pos, es_d, hd_d, desc_d, NULL,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
 			save_d, nfail_d, 1, gcm ? 0 : 1,
-			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL};
+			gcm ? &po_d->fail : &po_d->skip[2], 1, NULL, NULL};
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, 0, stream);
 	}
@@ -972,7 +972,6 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		if (err)
 			return err;
 		w->bp_d = w->bp.d;
-		w->bp_tb = w->bp_tc = 0;
 	}
 	memset(B, 0, sizeof(*B));
 	B->n = (uint32_t)n;
@@ -984,8 +983,6 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	B->bshift = bshift;
 	B->nb = nb;
 	B->cap = cap;
-	B->tb = w->bp_tb;
-	B->tc = w->bp_tc;
 	B->delta = prot ? (int32_t)T : -(int32_t)T;
 	B->gcm = (uint32_t)gcm;
 	k->devfold = !prot && !g_env.nodevfold;
@@ -1001,7 +998,7 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	B->hdr = (struct sgpu_hdr *)w->hd.d;
 	B->desc = (uint64_t *)w->dsc.d;
 	p = w->bp.d;
-	B->tickets = (uint32_t *)p;
+	B->ticket = (uint32_t *)p;
 	B->obins = (uint32_t *)(p + 64);
 	B->bcount = (uint32_t *)(p + 512);
 	p += BP_HEAD;
@@ -1013,8 +1010,6 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	BP_TAKE(B->tmp, (size_t)nb * cap * 4);
 	BP_TAKE(B->sorted, (size_t)nb * cap * 4);
 	BP_TAKE(B->afail, na * 4);
-	BP_TAKE(B->bfail, (size_t)nb * 4);
-	BP_TAKE(B->cfail, (size_t)nb * 4);
 	BP_TAKE(B->sseg, nsess * 4);
 	BP_TAKE(B->sout, nsess * sizeof(struct sgpu_sstate));
 	BP_TAKE(B->order, n * 4);
@@ -1081,21 +1076,19 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 	B->up = up_d;
 	err = sgpu_bplan_plan(B, stream);
 	if (!err) {
-		w->bp_tb += nb;
-		/* the crypto launches behind the plan's guards, in its order */
+		/* the crypto launches behind the plan's guards (the class
+		 * guards skip[] and the fail word), in its order */
 		struct sgpu_compact C = {
 			d->pos, B->es, B->hdr, B->desc, d->sess,
 			(const uint32_t *)w->cm.d, B->order, 0, (uint32_t)n,
 			(uint8_t *)B->verdict, (uint32_t *)(w->vs.d + 64),
-			B->nfail, 0, 0, NULL, 0, (uint32_t *)B->flist};
+			B->nfail, 0, 0, NULL, 0, (uint32_t *)B->flist,
+			&B->out->fail};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  B->out, prot, stream);
 	}
-	if (!err) {
+	if (!err)
 		err = sgpu_bplan_finish(B, stream);
-		if (!err)
-			w->bp_tc += nb;
-	}
 	if (err) {
 		w->bp_d = NULL;
 		return err;
@@ -1285,7 +1278,7 @@ int dev_mplanned_issue(struct dcall *k)
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
 			vd_d, save_d, nfail_d, 0, 0, NULL, 0,
-			!prot && !gcm && !g_env.nodevfold ? flist_d : NULL};
+			!prot && !gcm && !g_env.nodevfold ? flist_d : NULL, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -1380,7 +1373,7 @@ int dev_mplanned_finish(struct dcall *k)
 		struct sgpu_compact C = {
 			d->pos, es_d, hd_d, desc_d, d->sess,
 			(const uint32_t *)w->cm.d, NULL, 0, (uint32_t)n, vd_d,
-			save_d, nfail_d, 1, 0, NULL, 0, NULL};
+			save_d, nfail_d, 1, 0, NULL, 0, NULL, NULL};
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  po_d, prot, stream);
 	}

@@ -880,7 +880,7 @@ static int run_mplanned(int op, struct srtp **sessv, size_t nsess,
 		struct sgpu_compact C = {
 			up_d, up_d + n, hd_d, desc_d, up_d + 2 * n,
 			(const uint32_t *)w->cm.d, order_d, 0, (uint32_t)n,
-			vd_d, save_d, nfail_d, 0, 0, NULL, 0, NULL};
+			vd_d, save_d, nfail_d, 0, 0, NULL, 0, NULL, NULL};
 		err = run_classes(b->arena, b->arena_size, C, c0,
 				  po_d, prot, stream);
 	}
@@ -1096,7 +1096,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 			struct sgpu_compact C = {
 				up_d, up_d + n, hd_d, desc_d, NULL,
 				(const uint32_t *)w->cm.d, NULL, 0,
-				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL, 0, NULL};
+				(uint32_t)n, vd_d, save_d, nfail_d, 0, 1, NULL, 0, NULL, NULL};
 			err = run_classes(b->arena, b->arena_size, C, c0,
 					  po_d, prot, stream);
 		}
@@ -1292,7 +1292,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				(const uint32_t *)w->cm.d,
 				fl[q].has_idx ? idx_d : NULL, fl[q].base,
 				fl[q].n, vd_d, save_d, nfail_d, 0, nsess == 1,
-				NULL, 0, NULL};
+				NULL, 0, NULL, NULL};
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,
 					       (int)fl[q].shift, prot, stream);
@@ -1329,7 +1329,7 @@ static int run_fast(int op, struct srtp **sessv, size_t nsess,
 				c0->mode == SGPU_MODE_GCM ?
 				&((struct sgpu_plan_out *)w->pl.d)->fail :
 				&((struct sgpu_plan_out *)w->pl.d)->
-					  skip[fl[k].shift], 0, NULL};
+					  skip[fl[k].shift], 0, NULL, NULL};
 			C.uniform = planned != 2 && nsess == 1;
 			err = sgpu_run_compact(b->arena, b->arena_size, &C,
 					       c0->mode, (int)c0->nr,

@@ -221,13 +221,11 @@ struct ws {
 	uint32_t *sm_cnt;       /* device */
 	uint32_t *sm_flag;      /* pinned host */
 	uint32_t sm_seq;
-	/* multi-session batches of the bucket planner (plan_buckets.hip):
-	 * bucket entries | sorted | counters | tickets | fail words | sseg |
-	 * sout; the counters and tickets are zero between calls */
+	/* multi-session batches of the bucket planner (plan_buckets.hip,
+	 * batch_dev.c dev_bplanned_issue): its counters are zero between
+	 * calls once bp.d has been zeroed (bp_d) */
 	struct pool bp;
-	uint8_t *bp_d;          /* bp.d the ticket bases below belong to */
-	uint32_t bp_nb;         /* ... and the geometry they were laid out for */
-	uint32_t bp_tb, bp_tc;  /* the next launches' first tickets */
+	uint8_t *bp_d;
 };
 
 struct mbc {

@@ -185,6 +185,9 @@ struct sgpu_compact {
 					   the nfail count) and restored by a
 					   packet-per-workgroup pass; NULL: a
 					   full-grid pass finds them */
+	const uint32_t *gfail;          /* or NULL: a second guard word (the
+					   bucket planner's fail word, beside
+					   the class guards in guard[]) */
 };
 
 /* SRTCP descriptor: bits 0..30 SRTCP index, bit 31 E, bits 48..63 SD_* */
@@ -510,21 +513,23 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  *                       310-321, misc.c:22-41, replay.c:32-62), desc, the
  *                       crypto launch order (descending length bins, the
  *                       packets of a scatter workgroup together), each
- *                       session's state after the batch; the last
- *                       workgroup folds every fail word into out (fail,
- *                       hl0, skip[]) and re-zeroes the bucket and bin
- *                       counters
- *   (crypto, in `order`; unprotect CTR: the forged-packet restore)
+ *                       session's state after the batch; its fail bits
+ *                       and the scatter's into out->fail (the scatter's
+ *                       first workgroup zeroed it, wrote hl0 and the
+ *                       class guards skip[])
+ *   (crypto, in `order`, guarded by skip[] and out->fail; unprotect CTR:
+ *   the forged-packet restore)
  *   sgpu_bplan_finish   the results (end, err) per packet, the commit of
- *                       the touched sessions' states; with speculation
- *                       misses the verdict fold per bucket (the fold of
+ *                       the touched sessions' states, the bucket and bin
+ *                       counters back to zero; with speculation misses
+ *                       the verdict fold per bucket (the fold of
  *                       sgpu_mfold_rtp), the last workgroup then writes
  *                       the forged packets' EAUTH results and commits --
  *                       or leaves everything for the host (fo->fail);
  *                       gate word, out->nfail
- * bcount / obins / tickets must be zero before the first launch of a workspace
- * (each launch pair leaves them so); tb / tc: the ticket bases (+ nb per
- * launch).
+ * No workgroup waits for another except the fold's last one (a ticket,
+ * taken only when there are misses).  bcount / obins / ticket must be zero
+ * before the first launch of a workspace; every call leaves them so.
  */
 #define SGPU_BP_BLOCK 1024
 #define SGPU_BP_PPT 4           /* scatter: packets per thread */
@@ -539,7 +544,6 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
 struct sgpu_bplan {
 	uint32_t n, nsess, prot, tag, need, maxlen;
 	uint32_t bshift, nb, cap;       /* bucket geometry */
-	uint32_t tb, tc;                /* ticket bases of plan / finish */
 	int32_t delta;                  /* end change of a processed packet */
 	uint32_t gcm;
 	uint32_t nofold;                /* misses are left to the host fold */
@@ -556,10 +560,9 @@ struct sgpu_bplan {
 	uint32_t *bcount;               /* nb: entries per bucket (zeroed) */
 	uint32_t *obins;                /* 64: packets per length bin (zeroed) */
 	uint32_t *ooff;                 /* n: a packet's place in its bin */
-	uint32_t *tickets;              /* 2: plan, finish (zeroed once) */
+	uint32_t *ticket;               /* the fold's last-workgroup ticket
+					   (zero between calls) */
 	uint32_t *afail;                /* per scatter workgroup */
-	uint32_t *bfail;                /* per bucket (plan) */
-	uint32_t *cfail;                /* per bucket (fold) */
 	uint32_t *sseg;                 /* per session: start | count << 16 */
 	const uint32_t *cm;             /* session -> comp index (2 slot) */
 	const uint8_t *upneed;          /* or NULL: upload up[s] first */

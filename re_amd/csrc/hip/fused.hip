@@ -19,6 +19,11 @@ kfn_f sgpu_pick_fused(int nr, int prot, int undo)
 			: (prot ? k_ctr_fused<14, true> : k_ctr_fused<14, false>);
 }
 
+kfn_f sgpu_pick_fzplan(int prot)
+{
+	return prot ? k_fz_plan<true> : k_fz_plan<false>;
+}
+
 #ifdef FZ_WTIME
 /* the diagnostic stamps of the last launches (scripts/fz_wtime.py) */
 extern "C" __attribute__((visibility("default"))) int

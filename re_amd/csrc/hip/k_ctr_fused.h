@@ -114,7 +114,7 @@ __device__ uint64_t g_fzw[FZ_WREC * FZ_WTIME_MAX];
  * to encrypt / decrypt (fp), -1 if it has none or the workgroup does
  * nothing.
  */
-template <bool PROT>
+template <bool PROT, bool FILL = true>
 __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 				       uint8_t *smem, FastPkt &fp)
 {
@@ -162,11 +162,17 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 			S.seq0 = h0.seq;
 			if (t == 0) {
 				/* the next launch's counters; the context index
-				 * for the launches behind this one */
+				 * for the launches behind this one; the class
+				 * guards of a crypto launch behind the plan-only
+				 * kernel (skip[q] beside out->fail: k_fz_plan) */
 				P.out_next->fail = 0;
 				P.out_next->nfail = 0;
 				if (P.cm_out)
 					*P.cm_out = P.comp;
+				for (uint32_t c = 0; c < 4; c++)
+					P.out->skip[c] =
+						h0.hdr_len == 0xffffffffu ||
+						((h0.hdr_len >> 2) & 3u) != c;
 			}
 		}
 		else if (base >= tid) {
@@ -182,9 +188,11 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	}
 #ifndef FZ_FILL_LOOP
 	static_assert(FZ_BLOCK == 1024, "tt4_fill_b1024");
-	tt4_fill_b1024(smem, a.t0);
+	if (FILL)
+		tt4_fill_b1024(smem, a.t0);
 #else
-	tt4_fill(smem, a.t0);
+	if (FILL)
+		tt4_fill(smem, a.t0);
 #endif
 	FZ_STAMP(4);
 	if (live) {
@@ -419,6 +427,26 @@ k_ctr_fused(const FArgs fa)
 				__builtin_amdgcn_s_memrealtime();
 	}
 #endif
+}
+
+/*
+ * The plan alone, as its own launch in front of the lean crypto kernels
+ * (k_ctr_fast_any, guarded by skip[] and out->fail; k_gcmu, guarded by
+ * out->fail): the one-launch single-stream planner (batch_dev.c lp_issue).
+ * It writes what k_parse, k_plan_count / scan / desc / final and
+ * k_plan_finish wrote (hdr, es, desc, the plan out, the results of every
+ * packet planned), in one launch of many small workgroups instead of six,
+ * and leaves the crypto launch its full LDS and registers (the in-launch
+ * plan of k_ctr_fused costs each crypto workgroup ~15 us of latency, four
+ * workgroups in turn per CU).
+ */
+template <bool PROT>
+__global__ void __launch_bounds__(FZ_BLOCK)
+k_fz_plan(const FArgs fa)
+{
+	__shared__ FShared S;
+	FastPkt f;
+	(void)fz_plan<PROT, false>(fa, S, nullptr, f);
 }
 
 /*

@@ -1128,6 +1128,7 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
  * (k_ctr_fused.h): never voided as a whole (each workgroup plans itself) */
 typedef void (*kfn_f)(const FArgs);
 kfn_f sgpu_pick_fused(int nr, int prot, int undo);      /* fused.hip */
+kfn_f sgpu_pick_fzplan(int prot);                       /* fused.hip */
 
 /* grid = n / block; jobs: the packets it processes (srtp_gpu_prof);
  * *pid: the profiling record of the launch (sgpu_prof_void), or 0 */
@@ -1300,9 +1301,11 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 		int e = launch(ff, a, c->n, prof_slot(mode, nr, 3, prot),
 			       (hipStream_t)stream, sgpu_ctr_fast_block(prot),
 			       "k_ctr_fast_any", nr, prot, 4);
-		if (!e && !prot && c->flist) {
+		if (!e && !prot && c->flist && !c->gfail) {
 			/* one workgroup per listed forged packet (grid-
-			 * strided past 1024); all exit at once if none */
+			 * strided past 1024); all exit at once if none.
+			 * (Behind the one-launch planner -- gfail set -- the
+			 * caller launches it only when there are misses.) */
 			const uint32_t g = c->n < 1024u ? c->n : 1024u;
 			hipLaunchKernelGGL(nr == 10 ? sgpu_pick_ctr10_fast(0, 2)
 						    : sgpu_pick_ctr14_fast(0, 2),
@@ -1452,6 +1455,21 @@ extern "C" int sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
 			    f->in.n, prof_slot(SGPU_MODE_CTR, nr, 3, prot),
 			    (hipStream_t)stream, FZ_BLOCK, "k_ctr_fused", nr,
 			    prot, &f->prof_id);
+}
+
+extern "C" int sgpu_run_fzplan(uint8_t *arena, uint64_t arena_size,
+			       struct sgpu_fused *f, void *stream)
+{
+	FArgs fa;
+	if (!f->in.n)
+		return EINVAL;
+	const uint32_t nwg = (f->in.n + FZ_BLOCK - 1) / FZ_BLOCK;
+	f->ntickets = nwg;
+	f->prof_id = 0;
+	fz_args(fa, arena, arena_size, f);
+	hipLaunchKernelGGL(sgpu_pick_fzplan(f->in.prot != 0), dim3(nwg),
+			   dim3(FZ_BLOCK), 0, (hipStream_t)stream, fa);
+	return herr(hipGetLastError(), "plan launch");
 }
 
 extern "C" int sgpu_fused_undo(uint8_t *arena, uint64_t arena_size,

@@ -35,11 +35,18 @@
 static int fz_issue(struct dcall *k, int sync);
 static int fz_finish(struct dcall *k, int sync);
 
+static int lp_issue(struct dcall *k, int sync);
+static int lp_finish(struct dcall *k, int sync);
+
 int dev_planned_issue(struct dcall *k)
 {
-	if (k->sessv[0]->rtp.mode == SGPU_MODE_CTR && !g_env.noplanfuse) {
-		k->fused = 1;
-		return fz_issue(k, 0);
+	if (!g_env.noplanfuse) {
+		if (k->sessv[0]->rtp.mode == SGPU_MODE_CTR && g_env.fusedplan) {
+			k->fused = 1;
+			return fz_issue(k, 0);
+		}
+		k->fused = 2;
+		return lp_issue(k, 0);
 	}
 	const int prot = k->op == OP_RTP_ENC;
 	struct srtp *s = k->sessv[0];
@@ -149,8 +156,10 @@ int dev_planned_issue(struct dcall *k)
  * chained call before (nothing modified) */
 int dev_planned_finish(struct dcall *k)
 {
-	if (k->fused)
+	if (k->fused == 1)
 		return fz_finish(k, 0);
+	if (k->fused == 2)
+		return lp_finish(k, 0);
 	const int prot = k->op == OP_RTP_ENC;
 	struct srtp *s = k->sessv[0];
 	struct srtp_batch_dev *d = &k->d;
@@ -503,6 +512,284 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 	return err;
 }
 
+/* ---- one stream, the one-launch planner in front of the lean kernels -- */
+
+/*
+ * k_fz_plan (k_ctr_fused.h) plans the batch in one launch -- the in-launch
+ * plan of k_ctr_fused as a kernel of its own: hdr, es, desc, the plan out
+ * with the class guards skip[], the results of every packet planned -- and
+ * the lean crypto kernel runs behind it, guarded by skip[] and out->fail
+ * (AES-CM: k_ctr_fast_any) or by out->fail (GCM: k_gcmu), counting its
+ * tag misses into out->nfail.  A rejected plan wrote no byte of the arena
+ * (the crypto launch did nothing): only the ends are put back.  Forged
+ * packets: as dev_fused (the restore of their ciphertext and the verdict
+ * fold after the synchronisation; queued behind for asynchronous calls).
+ * Same workspace state as fz_issue (w->fz: tickets, epochs, plan outs).
+ */
+static int lp_issue(struct dcall *k, int sync)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	const struct comp *c0 = &s->rtp;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const size_t n = d->n;
+	const uint32_t T = gcm ? 16u : c0->tag_len;
+	const uint32_t need = prot ? (gcm ? 16u : (T > 4 ? T : 4u)) : 0u;
+	const uint32_t B = sgpu_fused_block();
+	const uint32_t nblk = (uint32_t)((n + B - 1) / B);
+	struct ws *w = k->w;
+	struct sgpu_fused *F = &k->fz;
+	void *stream = d->stream;
+	uint8_t *fz;
+	size_t poff;
+	int err;
+
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 8);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 9 + 72);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = pool_reserve(w, &w->pl, 64 + (n / 256 + 4) * 20);
+	if (!err)
+		err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_SLOT +
+				   (size_t)nblk * 8);
+	if (err)
+		return err;
+	fz = w->fz.d;
+	{
+		const long e = __atomic_exchange_n(&g_env.fzepoch, 0,
+						   __ATOMIC_RELAXED);
+		if (e > 0 && e <= 0xffff)
+			w->fz_d = NULL;
+		if (w->fz_d != fz || w->fz_epoch == 0 ||
+		    w->fz_epoch > 0xffffu) {
+			err = sgpu_memset(fz, 0, w->fz.cap, stream);
+			if (err)
+				return err;
+			w->fz_d = fz;
+			w->fz_epoch = 1;
+			w->fz_tbase = 0;
+			w->fz_par = 0;
+		}
+		if (e > 0 && e <= 0xffff)
+			w->fz_epoch = (uint32_t)e;
+	}
+	poff = FZ_HEAD + (size_t)w->fz_par * FZ_SLOT;
+	k->foff = poff;
+
+	memset(F, 0, sizeof(*F));
+	plan_in(&F->in, s, (uint32_t)n, prot, T, need);
+	F->in.zeroed = 1;
+	F->in.pred = k->pred;
+	F->pos = d->pos;
+	F->end = d->end;
+	F->cap = d->cap;
+	F->err = d->err;
+	F->es = (uint32_t *)w->es.d;
+	F->hdr = (struct sgpu_hdr *)w->hd.d;
+	F->desc = (uint64_t *)w->dsc.d;
+	if (!prot) {
+		F->save = (uint32_t *)(w->vs.d + 64);
+		F->verdict = w->vs.d + 64 + n * 4;
+		F->flist = gcm ? NULL : (uint32_t *)(w->vs.d +
+				     ((64 + n * 5 + 3) & ~(size_t)3));
+	}
+	F->out = (struct sgpu_plan_out *)(fz + poff);
+	F->out_next = (struct sgpu_plan_out *)(fz + FZ_HEAD +
+					       (size_t)(w->fz_par ^ 1) * FZ_SLOT);
+	F->cm_out = (uint32_t *)w->cm.d;
+	F->agg = (unsigned long long *)(fz + FZ_HEAD + 2 * FZ_SLOT);
+	F->ticket = (uint32_t *)fz;
+	F->tbase = w->fz_tbase;
+	F->epoch = w->fz_epoch;
+	F->comp = c0->dev;
+	F->delta = prot ? (int32_t)T : -(int32_t)T;
+	err = sgpu_run_fzplan(d->arena, d->arena_size, F, stream);
+	if (err) {
+		w->fz_d = NULL;
+		return err;
+	}
+	w->fz_tbase += F->ntickets;
+	w->fz_epoch++;
+	w->fz_par ^= 1;
+	{
+		/* the crypto launch behind the plan's guards */
+		struct sgpu_compact C = {
+			d->pos, F->es, F->hdr, F->desc, NULL, F->cm_out, NULL, 0,
+			(uint32_t)n, F->verdict, F->save, &F->out->nfail, 0,
+			gcm ? 1 : 2, gcm ? &F->out->fail : F->out->skip, 0,
+			F->flist, gcm ? NULL : &F->out->fail};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, gcm ? 0 : -1, prot, stream);
+		if (err)
+			return err;
+	}
+	k->devfold = !sync && !prot && !g_env.nodevfold;
+	if (!sync) {
+		/* queued behind: forged packets' ciphertext (AES-CM) and the
+		 * verdict fold (unprotect), the chained gate word */
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(fz + poff + FZ_FO_OFF);
+		uint32_t *fscr = (uint32_t *)(w->pl.d + 64);
+		if (k->devfold) {
+			if (!gcm)
+				err = sgpu_fused_refix(d->arena, d->arena_size, F,
+						       (int)c0->nr, stream);
+			if (!err)
+				err = sgpu_fold_rtp(1, &F->out->nfail, &F->in,
+						    F->hdr, F->desc, F->verdict,
+						    F->es, d->pos, d->end, d->err,
+						    gcm, fscr, fo_d, stream);
+		}
+		if (!err && k->gate)
+			err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0,
+					       0, &F->out->nfail, k->gate, NULL,
+					       k->devfold ? &fo_d->fail : NULL,
+					       stream);
+		if (!err && k->devfold)
+			err = sgpu_fold_rtp(2, &F->out->nfail, &F->in, F->hdr,
+					    F->desc, F->verdict, F->es, d->pos,
+					    d->end, d->err, gcm, fscr, fo_d,
+					    stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
+				      k->devfold ? FZ_SLOT
+						 : sizeof(struct sgpu_plan_out),
+				      stream);
+	return err;
+}
+
+static int lp_finish(struct dcall *k, int sync)
+{
+	const int prot = k->op == OP_RTP_ENC;
+	struct srtp *s = k->sessv[0];
+	struct srtp_batch_dev *d = &k->d;
+	const struct comp *c0 = &s->rtp;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const size_t n = d->n;
+	const unsigned ns0 = s->nstreams;
+	struct ws *w = k->w;
+	struct sgpu_fused *F = &k->fz;
+	const size_t poff = k->foff;
+	const struct sgpu_plan_out *po =
+		(const struct sgpu_plan_out *)(w->fz.h + poff);
+	const struct sgpu_fold_out *fo =
+		(const struct sgpu_fold_out *)(w->fz.h + poff + FZ_FO_OFF);
+	void *stream = d->stream;
+	struct srtp_stream old;
+	int err;
+
+	k->pfail = po->fail;
+	if (po->fail) {
+		if (po->fail & SPF_PRED)
+			return -2;      /* every workgroup did nothing */
+		if (po->fail & (SPF_BAD | SPF_SLOW))
+			w->fz_d = NULL;
+		if (po->fail & SPF_SLOW)
+			count(&g_cnt_lbtimeout, 1);
+		if ((po->fail & SPF_SSRC) && !ns0)
+			__atomic_store_n(&g_fresh_multi, 1, __ATOMIC_RELAXED);
+		count(&g_cnt_rejects, 1);
+		/* the crypto launch did nothing: only the ends the plan wrote
+		 * go back */
+		err = sgpu_memcpy_d2d(d->end, F->es, n * 4, stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		return err ? err : -1;
+	}
+	plan_apply(s, po, prot, n, &old);
+	count(&g_cnt_lplans, 1);
+	if (!po->nfail)
+		return 0;
+	count(&g_cnt_misses, po->nfail);
+	if (sync && !g_env.nodevfold) {
+		struct sgpu_fold_out *fo_d =
+			(struct sgpu_fold_out *)(w->fz.d + poff + FZ_FO_OFF);
+		err = 0;
+		if (!gcm)
+			err = sgpu_fused_refix(d->arena, d->arena_size, F,
+					       (int)c0->nr, stream);
+		if (!err)
+			err = sgpu_fold_rtp(0, &F->out->nfail, &F->in, F->hdr,
+					    F->desc, F->verdict, F->es, d->pos,
+					    d->end, d->err, gcm,
+					    (uint32_t *)(w->pl.d + 64), fo_d,
+					    stream);
+		if (!err)
+			err = sgpu_memcpy_d2h(w->fz.h + poff + FZ_FO_OFF, fo_d,
+					      sizeof(*fo), stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		if (err)
+			return err;
+		k->devfold = 1;
+	}
+	if (k->devfold && !fo->fail) {
+		struct srtp_stream *st = &s->streams[0];
+		st->s_l = (uint16_t)fo->s_l;
+		st->replay_rtp.lix = fo->lix;
+		st->replay_rtp.bitmap = fo->bitmap;
+		count(&g_cnt_devfolds, 1);
+		return 0;
+	}
+	/* the fold cannot be settled on the device (or nodevfold): every
+	 * processed packet back to its bytes, the host folds */
+	count(&g_cnt_folds, 1);
+	plan_unapply(s, ns0, &old);
+	if (gcm) {
+		struct sgpu_compact C = {
+			d->pos, F->es, F->hdr, F->desc, NULL, F->cm_out, NULL, 0,
+			(uint32_t)n, F->verdict, F->save, &F->out->nfail, 1, 1,
+			NULL, 0, NULL, NULL};
+		err = run_classes(d->arena, d->arena_size, C, c0, F->out, prot,
+				  stream);
+	}
+	else {
+		F->shift = (po->hl0 >> 2) & 3u;
+		err = sgpu_fused_undo(d->arena, d->arena_size, F, (int)c0->nr,
+				      prot, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, F->es, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	return err ? err : -1;
+}
+
+/* synchronous (dev_planned): -1 not plannable (nothing modified;
+ * *pfail: why, 0 for a forged packet the host must fold), else 0 /
+ * errno */
+static int dev_lplanned(int op, struct srtp *s, struct srtp_batch_dev *d,
+			uint32_t *pfail)
+{
+	struct dcall k;
+	int err;
+	memset(&k, 0, sizeof(k));
+	k.op = op;
+	k.sessv = &s;
+	k.nsess = 1;
+	k.d = *d;
+	k.w = ws_get();
+	*pfail = 0;
+	if (!k.w)
+		return ENOMEM;
+	err = lp_issue(&k, 1);
+	if (!err)
+		err = sgpu_stream_sync(d->stream);
+	if (err)
+		return err;
+	err = lp_finish(&k, 1);
+	*pfail = k.pfail;
+	return err;
+}
+
 /* synchronous: -1 not plannable (nothing modified; *pfail: why, 0 for a
  * forged packet the host must fold), else 0 / errno */
 int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
@@ -510,8 +797,11 @@ int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
 {
 	struct dcall k;
 	int err;
-	if (s->rtp.mode == SGPU_MODE_CTR && !g_env.noplanfuse)
-		return dev_fused(op, s, d, pfail);
+	if (!g_env.noplanfuse) {
+		if (s->rtp.mode == SGPU_MODE_CTR && g_env.fusedplan)
+			return dev_fused(op, s, d, pfail);
+		return dev_lplanned(op, s, d, pfail);
+	}
 	memset(&k, 0, sizeof(k));
 	k.op = op;
 	k.sessv = &s;

@@ -127,6 +127,8 @@ uint64_t g_cnt_dplans;   /* single-stream planner launches (k_plan_*,
 				   GCM and noplanfuse), accepted */
 uint64_t g_cnt_mplans;   /* multi-session device plans accepted */
 uint64_t g_cnt_rplans;   /* SRTCP device plans (k_plan_rtcp) accepted */
+uint64_t g_cnt_lplans;   /* single-stream batches planned by the
+				   one-launch planner (k_fz_plan), accepted */
 uint64_t g_cnt_lbtimeout; /* fused launches rejected by a look-back
 				   wait past its bound (SPF_SLOW) */
 /* a session's first batch (no stream yet) goes to the per-stream planner
@@ -177,6 +179,8 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_cnt_splans, __ATOMIC_RELAXED);
 	if (!strcmp(name, "fused"))
 		return __atomic_load_n(&g_cnt_fused, __ATOMIC_RELAXED);
+	if (!strcmp(name, "lplans"))
+		return __atomic_load_n(&g_cnt_lplans, __ATOMIC_RELAXED);
 	if (!strcmp(name, "dplans"))
 		return __atomic_load_n(&g_cnt_dplans, __ATOMIC_RELAXED);
 	if (!strcmp(name, "mplans"))
@@ -250,6 +254,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "nosmall"))
 		g_env.nosmall = value > 0;
+	else if (!strcmp(name, "fusedplan"))
+		g_env.fusedplan = value > 0;
 	else if (!strcmp(name, "noplanfuse"))
 		g_env.noplanfuse = value > 0;
 	else if (!strcmp(name, "fzepoch"))

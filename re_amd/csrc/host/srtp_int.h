@@ -116,6 +116,10 @@ struct srtp_env {
 	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
 				   launch by a stream synchronisation, not
 				   its completion word */
+	int fusedplan;          /* srtp_gpu_tune fusedplan: single-stream
+				   AES-CM batches planned inside the crypto
+				   launch (k_ctr_fused), not by the one-launch
+				   planner in front of the lean kernel */
 	int noplanfuse;         /* srtp_gpu_tune noplanfuse: single-stream
 				   batches take the separate device planner
 				   (k_parse + k_plan_*), not the plan inside
@@ -251,6 +255,7 @@ extern uint64_t g_cnt_pcbatch, g_cnt_pcpkts, g_cnt_pcfused, g_cnt_rxw_redo;
 extern uint64_t g_cnt_misses, g_cnt_folds, g_cnt_rejects, g_cnt_devfolds;
 extern uint64_t g_cnt_splans, g_cnt_fused, g_cnt_gated;
 extern uint64_t g_cnt_dplans, g_cnt_mplans, g_cnt_rplans, g_cnt_lbtimeout;
+extern uint64_t g_cnt_lplans;
 extern int g_fresh_multi;       /* srtp.c: the last first batch of a session
 				   showed several SSRCs (see there) */
 extern __thread struct tk_owner *t_own; /* srtp.c: this thread's async
@@ -328,7 +333,8 @@ struct dcall {
 	int devfold;            /* fold queued on the device */
 	int radix;              /* ... grouped by the radix sort */
 	int fused;              /* single stream planned inside the crypto
-				   launch (fz_issue / fz_finish) */
+				   launch (fz_issue / fz_finish), 2: by the
+				   one-launch planner (lp_issue / lp_finish) */
 	struct sgpu_fused fz;   /* ... its launch */
 	int bucket;             /* many sessions: the bucket planner */
 	struct sgpu_bplan bp;   /* ... its launches */

@@ -334,6 +334,12 @@ struct sgpu_fused {
 	uint64_t prof_id;               /* (out) its srtp_gpu_prof record */
 };
 unsigned sgpu_fused_block(void);        /* packets per workgroup */
+/* the plan of sgpu_run_fused alone (k_fz_plan), for a lean crypto launch
+ * behind it: the same outputs, plus out->skip[] (the class guards; the
+ * crypto launch's second guard word is out->fail) and the results of
+ * every packet planned; no byte of the arena is written */
+int   sgpu_run_fzplan(uint8_t *arena, uint64_t arena_size,
+		      struct sgpu_fused *f, void *stream);
 int   sgpu_run_fused(uint8_t *arena, uint64_t arena_size,
 		     struct sgpu_fused *f, int nr, void *stream);
 /* after a rejected fused launch (f->shift = class of packet 0's header):

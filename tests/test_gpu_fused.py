@@ -1,14 +1,21 @@
-"""Single-stream AES-CM batches planned inside the crypto launch
-(k_ctr_fused.h, host dev_fused): srtp_*_batch_dev of one session and one
-SSRC runs one launch that parses, plans (decoupled look-back over its
-1024-packet workgroups) and encrypts / decrypts.  It must give exactly the
-separate device planner's results (srtp_gpu_tune noplanfuse: k_parse +
-k_plan_* + the lean kernel, pinned by the reference digests in earlier
-rounds) and the general engine's: arena, pos, end, errno and stream
-state -- for batches the plan accepts and for every rejection, wherever in
-the batch the broken assumption sits (first, middle or last workgroup),
-which the fused path must undo completely before the host re-plans
-(srtp.c:183-432, misc.c:22-41, replay.c:32-62 of the reference).
+"""Single-stream batches planned by the decoupled look-back plan of
+k_ctr_fused.h (parse, every check, the ROC prefix over 1024-packet
+workgroups), in its two forms:
+
+  lplan   the default: the plan as a launch of its own (k_fz_plan, host
+          lp_issue / lp_finish) in front of the lean crypto kernel -- AES-CM
+          (k_ctr_fast_any) and AES-GCM (k_gcmu);
+  fused   srtp_gpu_tune fusedplan (AES-CM only): the plan inside the crypto
+          launch (k_ctr_fused, host dev_fused).
+
+Both must give exactly the separate device planner's results
+(srtp_gpu_tune noplanfuse: k_parse + k_plan_* + the lean kernel, pinned by
+the reference digests in earlier rounds) and the general engine's: arena,
+pos, end, errno and stream state -- for batches the plan accepts and for
+every rejection, wherever in the batch the broken assumption sits (first,
+middle or last workgroup), which each path must leave undone before the
+host re-plans (srtp.c:183-432, misc.c:22-41, replay.c:32-62 of the
+reference).
 """
 import numpy as np
 import pytest
@@ -63,36 +70,62 @@ def cases(s0):
     }
 
 
+GCM = (4, 5)
+
+
+def modes(suite):
+    """(mode, tune knobs, the counter its accepted plans move)"""
+    m = [("lplan", {}, "lplans")]
+    if suite not in GCM:
+        m.append(("fused", {"fusedplan": 1}, "fused"))
+    return m + [("planner", {"noplanfuse": 1}, None),
+                ("general", {"general": 1}, None)]
+
+
+PLANNED = ("lplan", "fused")
+
+
 def run_modes(torch, suite, key, op, pkts, state_from=None, cap_short=()):
-    """the batch through the fused path, the separate planner and the
-    general engine; returns {mode: (outputs, state, counters)}"""
+    """the batch through the one-launch plan, the fused path, the separate
+    planner and the general engine; returns {mode: (outputs, state,
+    (accepted plans of the mode's kind, rejects))}"""
     arena, pos, end, cap, _ = to_arena(pkts, short_cap=cap_short)
     res = {}
-    for mode, tune in (("fused", {}), ("planner", {"noplanfuse": 1}),
-                       ("general", {"general": 1})):
+    for mode, tune, cname in modes(suite):
         ctx = P.Srtp(suite, key)
         if state_from is not None:
             assert ctx.import_(state_from) == 0
-        f0, r0 = P.counter("fused"), P.counter("rejects")
+        f0 = P.counter(cname) if cname else 0
+        r0 = P.counter("rejects")
         with P.tune(**tune):
             out = run_dev(torch, op, [ctx], arena, pos, end, cap, None)
         res[mode] = (out, states([ctx], [SSRC]),
-                     (P.counter("fused") - f0, P.counter("rejects") - r0))
+                     ((P.counter(cname) - f0) if cname else 0,
+                      P.counter("rejects") - r0))
         ctx.close()
     return res
 
 
 def same(res, name):
-    A = res["fused"]
-    for mode in ("planner", "general"):
-        B = res[mode]
-        for k, (x, y) in enumerate(zip(A[0], B[0])):
-            assert (x == y).all(), (name, mode, ("arena", "pos", "end",
-                                                 "err")[k])
-        assert A[1] == B[1], (name, mode, A[1], B[1])
+    for a in PLANNED:
+        if a not in res:
+            continue
+        A = res[a]
+        for mode in ("planner", "general"):
+            B = res[mode]
+            for k, (x, y) in enumerate(zip(A[0], B[0])):
+                assert (x == y).all(), (name, a, mode,
+                                        ("arena", "pos", "end", "err")[k])
+            assert A[1] == B[1], (name, a, mode, A[1], B[1])
 
 
-@pytest.mark.parametrize("suite", [1, 0, 2])
+def planned(res, want, name):
+    for a in PLANNED:
+        if a in res:
+            assert res[a][2] == want, (name, a, res[a][2])
+
+
+@pytest.mark.parametrize("suite", [1, 0, 2, 4, 5])
 @pytest.mark.parametrize("s0", [65000, 100])
 def test_fused_equals_planner_and_general(suite, s0, torch_cuda):
     torch = torch_cuda
@@ -104,11 +137,10 @@ def test_fused_equals_planner_and_general(suite, s0, torch_cuda):
         same(res, name + "/protect")
         # a forward jump of 40000 is only ETIMEDOUT for the receiver
         accepted = name in ("inorder", "jump_last")
-        assert res["fused"][2] == ((1, 0) if accepted else (0, 1)), \
-            (name, res["fused"][2])
+        planned(res, (1, 0) if accepted else (0, 1), name)
         # receive what the accepted protect produced (in-order stream),
         # with the same defect injected on the protected packets
-        out = res["fused"][0]
+        out = res["lplan"][0]
         prot = [(0, out[0][out[1][i]:out[2][i]].tobytes())
                 for i in range(len(pkts)) if out[3][i] == 0]
         if name == "reorder_mid":
@@ -119,12 +151,11 @@ def test_fused_equals_planner_and_general(suite, s0, torch_cuda):
         same(dres, name + "/unprotect")
 
 
-@pytest.mark.parametrize("suite", [1, 2])
+@pytest.mark.parametrize("suite", [1, 2, 5])
 def test_fused_forged_packets_fold_on_device(suite, torch_cuda):
-    """forged packets in several workgroups: the fused launch counts the
-    misses, the host then restores their ciphertext and folds the verdicts
-    on the device (no rejection); a forged packet followed by a rollover
-    the fold cannot settle is undone and folded on the host"""
+    """forged packets in several workgroups: the crypto launch counts the
+    misses, the host then restores their ciphertext (AES-CM) and folds the
+    verdicts on the device (no rejection)"""
     torch = torch_cuda
     rng = np.random.default_rng(33 + suite)
     key = keys_for(suite, 1)[0]
@@ -132,7 +163,7 @@ def test_fused_forged_packets_fold_on_device(suite, torch_cuda):
     pkts = batch(rng, seqs)
     res = run_modes(torch, suite, key, "srtp_encrypt", pkts)
     same(res, "protect")
-    out = res["fused"][0]
+    out = res["lplan"][0]
     prot = [(0, out[0][out[1][i]:out[2][i]].tobytes())
             for i in range(len(pkts))]
     for forged in ([17], [36], [3, 1500, 4096, N - 1], list(range(0, N, 97))):
@@ -143,9 +174,9 @@ def test_fused_forged_packets_fold_on_device(suite, torch_cuda):
             q[i] = (0, bytes(b))
         dres = run_modes(torch, suite, key, "srtp_decrypt", q)
         same(dres, "forged %d" % len(forged))
-        errs = dres["fused"][0][3]
+        errs = dres["lplan"][0][3]
         assert (errs[forged] == P.EAUTH).all()
-        assert dres["fused"][2] == (1, 0)
+        planned(dres, (1, 0), "forged")
 
 
 def test_fused_short_capacity_and_continuation(torch_cuda):
@@ -159,7 +190,7 @@ def test_fused_short_capacity_and_continuation(torch_cuda):
     pkts = batch(rng, seqs)
     res = run_modes(torch, 1, key, "srtp_encrypt", pkts, cap_short=(N - 2,))
     same(res, "short cap")
-    assert res["fused"][0][3][N - 2] != 0
+    assert res["lplan"][0][3][N - 2] != 0
     # two accepted batches back to back on one context, against one
     # batch of both through the separate planner
     a, b = batch(rng, seqs[:2100]), batch(rng, seqs[2100:])
@@ -203,22 +234,25 @@ def test_fused_many_launches_sizes_and_epoch_wrap(torch_cuda):
         parts.append(batch(rng, list(range(seq, seq + n))))
         seq += n
     outs = {}
-    for mode, tune in (("fused", {}), ("planner", {"noplanfuse": 1})):
+    for mode, tune, cname in (("lplan", {}, "lplans"),
+                              ("fused", {"fusedplan": 1}, "fused"),
+                              ("planner", {"noplanfuse": 1}, "dplans")):
         ctx = P.Srtp(1, key)
         res = []
-        f0 = P.counter("fused")
+        f0 = P.counter(cname)
         with P.tune(**tune):
             for k, part in enumerate(parts):
-                if mode == "fused" and k == 3:
+                if mode != "planner" and k == 3:
                     P.lib().srtp_gpu_tune(b"fzepoch", 0xfffe)
                 ar, pos, end, cap, _ = to_arena(part)
                 res.append(run_dev(torch, "srtp_encrypt", [ctx], ar, pos,
                                    end, cap, None))
-        outs[mode] = (res, states([ctx], [SSRC]), P.counter("fused") - f0)
+        outs[mode] = (res, states([ctx], [SSRC]), P.counter(cname) - f0)
         ctx.close()
-    assert outs["fused"][2] == len(sizes)
-    assert outs["planner"][2] == 0
-    assert outs["fused"][1] == outs["planner"][1]
-    for x, y in zip(outs["fused"][0], outs["planner"][0]):
-        for u, v in zip(x, y):
-            assert (u == v).all()
+    for mode in ("lplan", "fused", "planner"):
+        assert outs[mode][2] == len(sizes), mode
+    for mode in ("lplan", "fused"):
+        assert outs[mode][1] == outs["planner"][1]
+        for x, y in zip(outs[mode][0], outs["planner"][0]):
+            for u, v in zip(x, y):
+                assert (u == v).all()

@@ -97,6 +97,9 @@ def run_modes(torch, suite, key, op, pkts, state_from=None, cap_short=()):
             assert ctx.import_(state_from) == 0
         f0 = P.counter(cname) if cname else 0
         r0 = P.counter("rejects")
+        # every mode from the same first-batch hint (a rejected plan for a
+        # second SSRC of a fresh session sets it, re_srtp_batch.h)
+        P.lib().srtp_gpu_tune(b"freshmulti", 0)
         with P.tune(**tune):
             out = run_dev(torch, op, [ctx], arena, pos, end, cap, None)
         res[mode] = (out, states([ctx], [SSRC]),

@@ -217,7 +217,9 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 			f |= SPF_PARSE;
 		else if (((h.hdr_len ^ hl0) >> 2) & 3u)
 			f |= SPF_CLASS;
-		if (h.ssrc != ssrc0)
+		/* (an unparsable packet has no SSRC: SPF_PARSE alone, so the
+		 * host does not try the per-stream planner for it) */
+		if (h.ssrc != ssrc0 && h.hdr_len != 0xffffffffu)
 			f |= SPF_SSRC;
 		if (!PROT && h.hdr_len != 0xffffffffu && L - h.hdr_len < in.tag)
 			f |= SPF_PARSE;

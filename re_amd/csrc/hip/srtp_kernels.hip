@@ -1313,7 +1313,8 @@ extern "C" int sgpu_run_compact(uint8_t *arena, uint64_t arena_size,
 					   (hipStream_t)stream, a);
 			e = herr(hipGetLastError(), "refix launch");
 		}
-		else if (!e && !prot)
+		else if (!e && !prot && !c->flist)
+			/* no list: a full-grid pass finds the forged packets */
 			e = launch(nr == 10 ? sgpu_pick_ctr10_fast(0, 1)
 					    : sgpu_pick_ctr14_fast(0, 1),
 				   a, c->n, -1, (hipStream_t)stream,

@@ -21,7 +21,12 @@ kfn_f sgpu_pick_fused(int nr, int prot, int undo)
 
 kfn_f sgpu_pick_fzplan(int prot)
 {
-	return prot ? k_fz_plan<true> : k_fz_plan<false>;
+	return prot ? k_lp_plan<true> : k_lp_plan<false>;
+}
+
+unsigned sgpu_lp_wg(void)
+{
+	return LP_WG;
 }
 
 #ifdef FZ_WTIME

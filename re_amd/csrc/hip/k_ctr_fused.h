@@ -114,7 +114,7 @@ __device__ uint64_t g_fzw[FZ_WREC * FZ_WTIME_MAX];
  * to encrypt / decrypt (fp), -1 if it has none or the workgroup does
  * nothing.
  */
-template <bool PROT, bool FILL = true>
+template <bool PROT>
 __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 				       uint8_t *smem, FastPkt &fp)
 {
@@ -162,17 +162,11 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 			S.seq0 = h0.seq;
 			if (t == 0) {
 				/* the next launch's counters; the context index
-				 * for the launches behind this one; the class
-				 * guards of a crypto launch behind the plan-only
-				 * kernel (skip[q] beside out->fail: k_fz_plan) */
+				 * for the launches behind this one */
 				P.out_next->fail = 0;
 				P.out_next->nfail = 0;
 				if (P.cm_out)
 					*P.cm_out = P.comp;
-				for (uint32_t c = 0; c < 4; c++)
-					P.out->skip[c] =
-						h0.hdr_len == 0xffffffffu ||
-						((h0.hdr_len >> 2) & 3u) != c;
 			}
 		}
 		else if (base >= tid) {
@@ -188,11 +182,9 @@ __device__ __forceinline__ int fz_plan(const FArgs &fa, FShared &S,
 	}
 #ifndef FZ_FILL_LOOP
 	static_assert(FZ_BLOCK == 1024, "tt4_fill_b1024");
-	if (FILL)
-		tt4_fill_b1024(smem, a.t0);
+	tt4_fill_b1024(smem, a.t0);
 #else
-	if (FILL)
-		tt4_fill(smem, a.t0);
+	tt4_fill(smem, a.t0);
 #endif
 	FZ_STAMP(4);
 	if (live) {
@@ -437,18 +429,297 @@ k_ctr_fused(const FArgs fa)
  * out->fail): the one-launch single-stream planner (batch_dev.c lp_issue).
  * It writes what k_parse, k_plan_count / scan / desc / final and
  * k_plan_finish wrote (hdr, es, desc, the plan out, the results of every
- * packet planned), in one launch of many small workgroups instead of six,
- * and leaves the crypto launch its full LDS and registers (the in-launch
- * plan of k_ctr_fused costs each crypto workgroup ~15 us of latency, four
- * workgroups in turn per CU).
+ * packet planned) in one launch instead of six, and leaves the crypto
+ * launch its full LDS and registers (the in-launch plan of k_ctr_fused
+ * costs each crypto workgroup ~15 us of latency, four workgroups in turn
+ * per CU).  The steps of fz_plan, with LP_PPT packets per lane: a
+ * workgroup covers LP_PPT x 1024 packets (packet q = j * 1024 + lane id,
+ * loads coalesced per j and all of a lane's in flight together), so a 1M
+ * batch takes 256 tickets and one look-back chain of 256 instead of 1024.
  */
+#define LP_PPT 4
+#define LP_WG (FZ_BLOCK * LP_PPT)
+
+struct LpShared {
+	uint32_t t, fail, hl0, ssrc0, seq0, excl, xfail;
+	uint32_t wsum[LP_PPT][FZ_BLOCK / 64];   /* rollovers per (round, wave) */
+	uint32_t seq[LP_WG + 2];                /* packets base-2 .. */
+};
+
 template <bool PROT>
 __global__ void __launch_bounds__(FZ_BLOCK)
-k_fz_plan(const FArgs fa)
+k_lp_plan(const FArgs fa)
 {
-	__shared__ FShared S;
-	FastPkt f;
-	(void)fz_plan<PROT, false>(fa, S, nullptr, f);
+	__shared__ LpShared S;
+	const KArgs &a = fa.a;
+	const struct sgpu_fused &P = fa.p;
+	const struct sgpu_plan_in &in = P.in;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t lane = tid & 63u, wv = tid >> 6;
+	const uint64_t asz = a.asz;
+	const uint32_t n = in.n;
+
+	if (tid == 0) {
+		S.t = atomicAdd(P.ticket, 1u) - P.tbase;
+		S.fail = 0;
+	}
+	__syncthreads();
+	const uint32_t t = S.t;
+	const uint32_t base = t * LP_WG;
+	uint32_t pv[LP_PPT], ev[LP_PPT], cv[LP_PPT], w0[LP_PPT], w2[LP_PPT];
+#pragma unroll
+	for (int j = 0; j < LP_PPT; j++) {
+		const uint32_t i = base + j * FZ_BLOCK + tid;
+		pv[j] = ev[j] = cv[j] = 0;
+		if (i < n) {
+			pv[j] = P.pos[i];
+			ev[j] = P.end[i];
+			cv[j] = P.cap ? P.cap[i] : 0u;
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < LP_PPT; j++) {
+		const uint32_t p = pv[j], e = ev[j];
+		w0[j] = w2[j] = 0;
+		if (base + j * FZ_BLOCK + tid < n && e > p && e <= asz &&
+		    e - p >= 12 && !(p & 3u)) {
+			w0[j] = *(const uint32_t *)(a.arena + p);
+			w2[j] = *(const uint32_t *)(a.arena + p + 8);
+		}
+	}
+	if (tid < 3) {
+		if (tid == 0) {
+			/* packet 0: every packet's class and SSRC are checked
+			 * against it */
+			const uint32_t q = P.pos[0], qe = P.end[0];
+			const uint32_t left = (qe > q && qe <= asz) ? qe - q : 0u;
+			const struct sgpu_hdr h0 = parse_rtp_hdr(a.arena + q, q,
+								 left);
+			S.hl0 = h0.hdr_len;
+			S.ssrc0 = h0.ssrc;
+			S.seq0 = h0.seq;
+			if (t == 0) {
+				/* the next launch's counters; the context index
+				 * and the class guards for the crypto launch */
+				P.out_next->fail = 0;
+				P.out_next->nfail = 0;
+				if (P.cm_out)
+					*P.cm_out = P.comp;
+				for (uint32_t c = 0; c < 4; c++)
+					P.out->skip[c] =
+						h0.hdr_len == 0xffffffffu ||
+						((h0.hdr_len >> 2) & 3u) != c;
+			}
+		}
+		else if (base >= tid) {
+			/* seq of packet base - tid (the workgroup before) */
+			const uint32_t q = P.pos[base - tid];
+			uint32_t sv = 0;
+			if ((uint64_t)q + 4u <= asz)
+				sv = (uint32_t)a.arena[q + 2] << 8 | a.arena[q + 3];
+			S.seq[2 - tid] = sv;
+		}
+	}
+	struct sgpu_hdr hv[LP_PPT];
+#pragma unroll
+	for (int j = 0; j < LP_PPT; j++) {
+		const uint32_t i = base + j * FZ_BLOCK + tid;
+		hv[j].ssrc = 0; hv[j].seq = 0; hv[j].err_pos = 0;
+		hv[j].hdr_len = 0xffffffffu;
+		if (i >= n)
+			continue;
+		const uint32_t p = pv[j], e = ev[j];
+		const uint32_t left = (e > p && e <= asz) ? e - p : 0u;
+		if (left >= 12 && !(p & 3u) && !(w0[j] & 0x1fu)) {
+			/* no CSRC, no extension: the header is the two words */
+			hv[j].seq = (uint16_t)((w0[j] >> 8 & 0xff00u) |
+					       (w0[j] >> 24));
+			hv[j].ssrc = __builtin_bswap32(w2[j]);
+			hv[j].hdr_len = 12;
+		}
+		else {
+			hv[j] = parse_rtp_hdr(a.arena + p, p, left);
+		}
+		P.hdr[i] = hv[j];
+		P.es[i] = e;
+		S.seq[2 + j * FZ_BLOCK + tid] = hv[j].seq;
+	}
+	__syncthreads();
+
+	/* k_plan_count's checks (srtp_kernels.hip), as fz_plan */
+	const uint32_t hl0 = S.hl0;
+	const uint32_t ssrc0 = in.ssrc_any ? S.ssrc0 : in.ssrc;
+	const uint32_t s_l0 = in.fresh ? S.seq0 : in.s_l;       /* plan_sb(0) */
+	uint32_t f = 0;
+	uint32_t sbv[LP_PPT];
+	uint64_t wm[LP_PPT];
+#pragma unroll
+	for (int j = 0; j < LP_PPT; j++) {
+		const uint32_t q = j * FZ_BLOCK + tid, i = base + q;
+		const struct sgpu_hdr &h = hv[j];
+		bool wrap = false;
+		sbv[j] = 0;
+		if (i < n) {
+			const uint32_t p = pv[j], e = ev[j], cp = cv[j];
+			const uint32_t seq = h.seq;
+			const uint32_t sb = i == 0 ? s_l0 : S.seq[q + 1];
+			const uint32_t L = e - p;
+			sbv[j] = sb;
+			if (h.hdr_len == 0xffffffffu || hl0 == 0xffffffffu)
+				f |= SPF_PARSE;
+			else if (((h.hdr_len ^ hl0) >> 2) & 3u)
+				f |= SPF_CLASS;
+			if (h.ssrc != ssrc0 && h.hdr_len != 0xffffffffu)
+				f |= SPF_SSRC;
+			if (!PROT && h.hdr_len != 0xffffffffu &&
+			    L - h.hdr_len < in.tag)
+				f |= SPF_PARSE;
+			if (!PROT && (int)seq - (int)sb > 32768)
+				f |= SPF_TIMEOUT;
+			if (L >= in.maxlen)
+				f |= SPF_SIZE;
+			if ((p & 3u) || p > e || e > asz ||
+			    (P.cap && (e > cp || cp > asz)))
+				f |= SPF_BAD;
+			if (PROT && P.cap && (uint64_t)e + in.need > (uint64_t)cp)
+				f |= SPF_CAP;
+			wrap = plan_wrap(seq, sb);
+			if (i + 1 < n && !wrap && seq < sb)
+				f |= SPF_ORDER;
+			if (i == 0) {
+				P.out->ssrc0 = h.ssrc;
+				P.out->hl0 = h.hdr_len;
+			}
+		}
+		wm[j] = __ballot(wrap);
+		if (lane == 0)
+			S.wsum[j][wv] = (uint32_t)__popcll(wm[j]);
+	}
+	if (tid == 0 && in.pred && *in.pred)    /* sgpu_gate_pred */
+		f |= SPF_PRED;
+	if (f)
+		atomicOr(&S.fail, f);
+	__syncthreads();
+
+	if (wv == 0) {
+		/* aggregate, look-back, inclusive prefix (fz_plan step 3) */
+		uint32_t tot = 0;
+#pragma unroll
+		for (int j = 0; j < LP_PPT; j++)
+			tot += wave_sum(lane < FZ_BLOCK / 64u ? S.wsum[j][lane] : 0u);
+		const uint32_t lf = S.fail;
+		uint32_t excl = 0, xf = 0;
+		if (t != 0) {
+			if (lane == 0)
+				fz_store(&P.agg[t], fz_word(P.epoch, 1, lf, tot));
+			int32_t jj = (int32_t)t - 1;
+			for (;;) {
+				const int32_t k = jj - (int32_t)lane;
+				uint64_t w = 0;
+				uint32_t st = 2;
+				if (k >= 0) {
+					for (uint32_t spin = 0;; spin++) {
+						w = fz_load(&P.agg[k]);
+						st = (uint32_t)(w >> 46) & 3u;
+						if ((uint32_t)(w >> 48) == P.epoch &&
+						    st != 0)
+							break;
+						if (spin > (1u << 18)) {
+							w = fz_word(0, 2, SPF_SLOW, 0);
+							st = 2;
+							break;
+						}
+						__builtin_amdgcn_s_sleep(1);
+					}
+				}
+				const uint64_t inc = __ballot(st == 2);
+				const uint32_t first = inc ?
+					(uint32_t)__ffsll((long long)inc) - 1u : 64u;
+				const bool take = lane <= first;
+				excl += wave_sum(take ? (uint32_t)w : 0u);
+				xf |= wave_or(take ? (uint32_t)(w >> 32) & FZ_FMASK
+						   : 0u);
+				if (inc)
+					break;
+				jj -= 64;
+			}
+		}
+		if (lane == 0) {
+			fz_store(&P.agg[t], fz_word(P.epoch, 2, lf | xf,
+						    excl + tot));
+			S.excl = excl;
+			S.xfail = lf | xf;
+			if (lf | (xf & (SPF_BAD | SPF_SLOW)))
+				atomicOr(&P.out->fail,
+					 lf | (xf & (SPF_BAD | SPF_SLOW)));
+		}
+	}
+	__syncthreads();
+	const bool dead = S.xfail != 0;
+	uint32_t pre = S.excl;
+#pragma unroll
+	for (int j = 0; j < LP_PPT; j++) {
+		const uint32_t q = j * FZ_BLOCK + tid, i = base + q;
+		uint32_t wpre = (uint32_t)__popcll(wm[j] & ((1ull << lane) - 1ull));
+		for (uint32_t w = 0; w < wv; w++)
+			wpre += S.wsum[j][w];
+		const uint32_t rpre = pre + wpre;
+		for (uint32_t w = 0; w < FZ_BLOCK / 64u; w++)
+			pre += S.wsum[j][w];
+		if (i >= n)
+			continue;
+		if (dead) {
+			P.desc[i] = 0;          /* not planned */
+			continue;
+		}
+		/* fz_plan step 4: k_plan_desc (srtp_kernels.hip) */
+		const uint32_t seq = hv[j].seq, sb = sbv[j];
+		const bool wrap = (wm[j] >> lane) & 1ull;
+		const uint32_t roc = in.roc + rpre + (wrap ? 1u : 0u);
+		uint64_t ix;
+		uint32_t fl = SD_RUN | SD_CIPHER;
+		if (PROT) {
+			ix = 65536ull * roc + seq;                      /* srtp.c:215 */
+		}
+		else {
+			const int32_t v = plan_v(roc, wrap ? 0u : sb, seq);
+			ix = seq + (uint64_t)(int64_t)v * 65536ull;
+			if ((uint32_t)v != roc)
+				fl |= (uint32_t)v + 1u == roc ? SD_ROC_P1 : SD_ROC_M1;
+			bool ok;
+			if (i == 0) {
+				if (ix > in.lix)
+					ok = true;
+				else {
+					const uint64_t d = in.lix - ix;
+					ok = d < 64 && !(in.bitmap & (1ull << d));
+				}
+			}
+			else {
+				const uint32_t pseq = sb;       /* packet i-1's seq */
+				const uint32_t psb = i == 1 ? s_l0 : S.seq[q];
+				const bool pw = plan_wrap(pseq, psb);
+				const uint32_t proc = roc - (wrap ? 1u : 0u);
+				const int32_t pv2 = plan_v(proc, pw ? 0u : psb, pseq);
+				const uint64_t pix = pseq + (uint64_t)(int64_t)pv2 * 65536ull;
+				ok = ix > pix && ix > in.lix;
+			}
+			if (!ok)
+				atomicOr(&P.out->fail, (uint32_t)SPF_REPLAY);
+		}
+		P.desc[i] = d_desc(ix, fl);
+		const uint32_t t0 = n > SGPU_PLAN_TAIL ? n - SGPU_PLAN_TAIL : 0u;
+		if (i >= t0)
+			P.out->tail_ix[i - t0] = ix;
+		if (i + 1 == n) {
+			P.out->s_l_last = wrap ? seq : (seq > sb ? seq : sb);
+			P.out->wraps = roc - in.roc;
+		}
+		/* k_plan_finish's results (the host puts the ends back if the
+		 * plan fails anywhere) */
+		P.end[i] = ev[j] + (uint32_t)P.delta;
+		P.err[i] = 0;
+	}
 }
 
 /*

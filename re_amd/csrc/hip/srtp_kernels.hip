@@ -1129,6 +1129,7 @@ static int launch(kfn_t f, const KArgs &a, uint32_t n, int slot,
 typedef void (*kfn_f)(const FArgs);
 kfn_f sgpu_pick_fused(int nr, int prot, int undo);      /* fused.hip */
 kfn_f sgpu_pick_fzplan(int prot);                       /* fused.hip */
+unsigned sgpu_lp_wg(void);                              /* fused.hip */
 
 /* grid = n / block; jobs: the packets it processes (srtp_gpu_prof);
  * *pid: the profiling record of the launch (sgpu_prof_void), or 0 */
@@ -1464,7 +1465,8 @@ extern "C" int sgpu_run_fzplan(uint8_t *arena, uint64_t arena_size,
 	FArgs fa;
 	if (!f->in.n)
 		return EINVAL;
-	const uint32_t nwg = (f->in.n + FZ_BLOCK - 1) / FZ_BLOCK;
+	const uint32_t wg = sgpu_lp_wg();      /* packets per workgroup */
+	const uint32_t nwg = (f->in.n + wg - 1) / wg;
 	f->ntickets = nwg;
 	f->prof_id = 0;
 	fz_args(fa, arena, arena_size, f);

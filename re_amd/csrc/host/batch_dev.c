@@ -515,7 +515,7 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 /* ---- one stream, the one-launch planner in front of the lean kernels -- */
 
 /*
- * k_fz_plan (k_ctr_fused.h) plans the batch in one launch -- the in-launch
+ * k_lp_plan (k_ctr_fused.h) plans the batch in one launch -- the in-launch
  * plan of k_ctr_fused as a kernel of its own: hdr, es, desc, the plan out
  * with the class guards skip[], the results of every packet planned -- and
  * the lean crypto kernel runs behind it, guarded by skip[] and out->fail

@@ -128,7 +128,7 @@ uint64_t g_cnt_dplans;   /* single-stream planner launches (k_plan_*,
 uint64_t g_cnt_mplans;   /* multi-session device plans accepted */
 uint64_t g_cnt_rplans;   /* SRTCP device plans (k_plan_rtcp) accepted */
 uint64_t g_cnt_lplans;   /* single-stream batches planned by the
-				   one-launch planner (k_fz_plan), accepted */
+				   one-launch planner (k_lp_plan), accepted */
 uint64_t g_cnt_lbtimeout; /* fused launches rejected by a look-back
 				   wait past its bound (SPF_SLOW) */
 /* a session's first batch (no stream yet) goes to the per-stream planner

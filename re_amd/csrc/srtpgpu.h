@@ -334,7 +334,7 @@ struct sgpu_fused {
 	uint64_t prof_id;               /* (out) its srtp_gpu_prof record */
 };
 unsigned sgpu_fused_block(void);        /* packets per workgroup */
-/* the plan of sgpu_run_fused alone (k_fz_plan), for a lean crypto launch
+/* the plan of sgpu_run_fused alone (k_lp_plan), for a lean crypto launch
  * behind it: the same outputs, plus out->skip[] (the class guards; the
  * crypto launch's second guard word is out->fail) and the results of
  * every packet planned; no byte of the arena is written */

@@ -17,6 +17,6 @@ for tw in "${W[@]}"; do
   ks=$(find $O/$t -name '*kernel_stats.csv' | head -1)
   cp $ks $O/${t}_kernel_stats.csv
   python3 $R/scripts/step_gaps.py $kt 10 > $O/${t}_step_split.txt 2>&1 || exit $?
-  python3 $R/scripts/timeline.py $kt ${TL:-60} > $O/${t}_timeline.txt 2>&1 || exit $?
+  python3 $R/scripts/timeline.py $kt ${TL:-40} --crypto > $O/${t}_timeline.txt 2>&1 || exit $?
 done
 echo done > $O/done

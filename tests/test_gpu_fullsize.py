@@ -90,7 +90,7 @@ def session_states(ctxs, rtcp=False):
 # per (config, direction): the counters that must move by exactly the
 # given amount in that call ("rejects" and "folds" -- a host re-plan or a
 # host fold -- must stay 0 unless listed).  lplans: the one-launch plan
-# (k_fz_plan) in front of the lean kernel (AES-CM and GCM); fused: the
+# (k_lp_plan) in front of the lean kernel (AES-CM and GCM); fused: the
 # in-launch plan (k_ctr_fused, srtp_gpu_tune fusedplan); dplans: the
 # separate single-stream planner launches (noplanfuse);
 # mplans: the multi-session planner; rplans: the SRTCP planner; devfolds:

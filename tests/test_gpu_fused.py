@@ -2,7 +2,7 @@
 k_ctr_fused.h (parse, every check, the ROC prefix over 1024-packet
 workgroups), in its two forms:
 
-  lplan   the default: the plan as a launch of its own (k_fz_plan, host
+  lplan   the default: the plan as a launch of its own (k_lp_plan, host
           lp_issue / lp_finish) in front of the lean crypto kernel -- AES-CM
           (k_ctr_fast_any) and AES-GCM (k_gcmu);
   fused   srtp_gpu_tune fusedplan (AES-CM only): the plan inside the crypto

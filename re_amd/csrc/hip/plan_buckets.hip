@@ -155,7 +155,7 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 {
 	__shared__ uint32_t hist[SGPU_BP_NBMAX], base[SGPU_BP_NBMAX];
 	__shared__ uint32_t oh[BP_OBINS], ob[BP_OBINS];
-	__shared__ uint32_t bf;
+	__shared__ uint32_t bf, hl0s;
 	const uint32_t tid = threadIdx.x, nb = P.nb;
 	for (uint32_t k = tid; k < nb; k += BPB)
 		hist[k] = 0;
@@ -163,6 +163,11 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		oh[tid] = 0;
 	if (tid == 0) {
 		bf = 0;
+		/* packet 0's header: every packet's class is checked against
+		 * it (k_mp_count's SPF_CLASS) */
+		const uint32_t q = P.pos[0], qe = P.end[0];
+		hl0s = parse_rtp_hdr(arena + q, q, (qe > q && qe <= asz) ?
+						   qe - q : 0u).hdr_len;
 		if (blockIdx.x == 0) {
 			/* the call's outs: nothing else writes them before the
 			 * plan kernel (the crypto launch's miss counter too) */
@@ -176,7 +181,7 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		}
 	}
 	uint32_t bk[SGPU_BP_PPT], rk[SGPU_BP_PPT], wd[SGPU_BP_PPT];
-	uint32_t orank[SGPU_BP_PPT];
+	uint32_t orank[SGPU_BP_PPT], wy[SGPU_BP_PPT], wz[SGPU_BP_PPT];
 	uint32_t pv[SGPU_BP_PPT], ev[SGPU_BP_PPT], cv[SGPU_BP_PPT];
 	uint32_t sv[SGPU_BP_PPT], w0[SGPU_BP_PPT], w2[SGPU_BP_PPT];
 	uint32_t f = 0;
@@ -207,11 +212,12 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		}
 	}
 	__syncthreads();
+	const uint32_t hl0 = hl0s;
 #pragma unroll
 	for (int j = 0; j < SGPU_BP_PPT; j++) {
 		const uint32_t i = i0 + j * BPB;
 		bk[j] = 0xffffffffu;
-		rk[j] = wd[j] = orank[j] = 0;
+		rk[j] = wd[j] = orank[j] = wy[j] = wz[j] = 0;
 		if (i >= P.n)
 			continue;
 		const uint32_t p = pv[j], e = ev[j], c = cv[j];
@@ -256,6 +262,10 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 			f |= SPF_BAD;
 			s = P.nsess - 1u;
 		}
+		if (hl0 == 0xffffffffu)
+			f |= SPF_PARSE;
+		else if (h.hdr_len != 0xffffffffu && ((h.hdr_len ^ hl0) >> 2) & 3u)
+			f |= SPF_CLASS;
 		/* the crypto launch order's class: descending 64-B chunks */
 		const uint32_t L = e >= p ? e - p : 0u, ch = (L + 63u) >> 6;
 		const uint32_t bin = (BP_OBINS - 1u) -
@@ -264,6 +274,10 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		rk[j] = atomicAdd(&hist[bk[j]], 1u);
 		orank[j] = atomicAdd(&oh[bin], 1u);
 		wd[j] = i | bin << 26;
+		/* the plan kernel's whole view of the packet, so it gathers
+		 * nothing: seq, session in bucket, SSRC */
+		wy[j] = (uint32_t)h.seq | (s - (bk[j] << P.bshift)) << 16;
+		wz[j] = h.ssrc;
 	}
 	if (blockIdx.x == 0 && tid == 0 && P.pred && *P.pred)
 		f |= SPF_PRED;          /* sgpu_gate_pred */
@@ -281,10 +295,11 @@ k_bp_scatter(const uint8_t *__restrict__ arena, uint64_t asz,
 		 * stay together there, so a crypto wave reads neighbouring
 		 * slots of the arena (arrival order, not bucket order: the
 		 * bucket-major order measured 1.73 ms per launch against 0.98) */
-		P.ooff[wd[j] & BP_IMASK] = ob[wd[j] >> 26] + orank[j];
 		const uint32_t slot = base[bk[j]] + rk[j];
 		if (slot < P.cap)
-			P.tmp[(size_t)bk[j] * P.cap + slot] = wd[j];
+			P.tmp[(size_t)bk[j] * P.cap + slot] =
+				make_uint4(wd[j], wy[j], wz[j],
+					   ob[wd[j] >> 26] + orank[j]);
 		else
 			f |= SPF_SEG;   /* the bucket overflows: radix re-plan */
 	}
@@ -318,7 +333,7 @@ struct BpPlanLds {
 	uint32_t wlo[SGPU_BP_NSB], whi[SGPU_BP_NSB];    /* replay bits */
 	uint32_t bb[BP_OBINS];
 	uint32_t wsum[BPB / 64];
-	uint32_t bf, hl0;
+	uint32_t bf;
 };
 
 /* speculated s_l seen by sorted position k (its segment l starting at f):
@@ -385,32 +400,17 @@ k_bp_plan(const struct sgpu_bplan P)
 		f |= SPF_SEG;           /* (the scatter flagged it too) */
 		m = 0;
 	}
-	/* the entries' loads first (EPT per thread, all in flight), then
-	 * their headers and sessions */
-	uint32_t wv[BP_EPT], seqv[BP_EPT], ssv[BP_EPT], hlv[BP_EPT],
-		 sesv[BP_EPT];
+	/* the bucket's entries (EPT per thread, all in flight): index and
+	 * length bin, seq and session, SSRC, place in the bin */
+	uint4 ev4[BP_EPT];
 #pragma unroll
 	for (int j = 0; j < BP_EPT; j++) {
 		const uint32_t k = tid + j * BPB;
-		wv[j] = k < m ? P.tmp[(size_t)b * P.cap + k] : 0u;
+		ev4[j] = k < m ? P.tmp[(size_t)b * P.cap + k]
+			       : make_uint4(0, 0, 0, 0);
 	}
-#pragma unroll
-	for (int j = 0; j < BP_EPT; j++) {
-		const uint32_t k = tid + j * BPB;
-		seqv[j] = ssv[j] = hlv[j] = sesv[j] = 0;
-		if (k < m) {
-			const uint32_t i = wv[j] & BP_IMASK;
-			const uint32_t *hw = (const uint32_t *)(P.hdr + i);
-			ssv[j] = hw[0];
-			seqv[j] = hw[1] & 0xffffu;
-			hlv[j] = hw[2];
-			sesv[j] = P.sess[i];
-		}
-	}
-	if (tid == 0) {
+	if (tid == 0)
 		S.bf = 0;
-		S.hl0 = P.hdr[0].hdr_len;
-	}
 	if (tid < BP_OBINS)
 		S.bb[tid] = P.obins[tid];       /* the bins' totals */
 	if (tid < ns) {
@@ -432,27 +432,20 @@ k_bp_plan(const struct sgpu_bplan P)
 		S.wlo[tid] = S.whi[tid] = 0;
 	}
 	__syncthreads();
-	const uint32_t hl0 = S.hl0;
-	/* the entries: seq, session, rank in session */
+	/* the entries: seq, session, rank in session (the header checks
+	 * were the scatter's) */
 #pragma unroll
 	for (int j = 0; j < BP_EPT; j++) {
 		const uint32_t k = tid + j * BPB;
 		if (k >= m)
 			continue;
-		uint32_t s = sesv[j];
-		if (s >= P.nsess)
-			s = P.nsess - 1u;       /* SPF_BAD from the scatter */
-		const uint32_t l = s - s0;
-		S.ent[k] = wv[j];
-		S.sq[k] = (uint16_t)seqv[j];
+		const uint32_t l = ev4[j].y >> 16;
+		S.ent[k] = ev4[j].x;
+		S.sq[k] = (uint16_t)ev4[j].y;
 		S.sl[k] = (uint8_t)l;
 		S.srt[k] = (uint16_t)atomicAdd(&S.cnt[l], 1u);
-		atomicMin(&S.smin[l], ssv[j]);
-		atomicMax(&S.smax[l], ssv[j]);
-		if (hlv[j] == 0xffffffffu || hl0 == 0xffffffffu)
-			f |= SPF_PARSE;
-		else if (((hlv[j] ^ hl0) >> 2) & 3u)
-			f |= SPF_CLASS;
+		atomicMin(&S.smin[l], ev4[j].z);
+		atomicMax(&S.smax[l], ev4[j].z);
 	}
 	__syncthreads();
 	/* segment starts (sessions, <= 256: wave 0) and the length bins'
@@ -514,9 +507,9 @@ k_bp_plan(const struct sgpu_bplan P)
 			const uint32_t k = tid + j * BPB;
 			if (k >= m)
 				continue;
-			const uint32_t i = wv[j] & BP_IMASK;
+			const uint32_t i = ev4[j].x & BP_IMASK;
 			S.un[S.start[S.sl[k]] + S.srt[k]] = (uint16_t)k;
-			P.order[S.bb[wv[j] >> 26] + P.ooff[i]] = i;
+			P.order[S.bb[ev4[j].x >> 26] + ev4[j].w] = i;
 		}
 	}
 	__syncthreads();
@@ -999,7 +992,8 @@ extern "C" size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
 				     uint32_t cap)
 {
 	const size_t na = (n + BPB * SGPU_BP_PPT - 1) / (BPB * SGPU_BP_PPT);
-	return 2 * bp_align((size_t)nb * cap * 4) + /* tmp, sorted */
+	return bp_align((size_t)nb * cap * 16) +    /* tmp */
+	       bp_align((size_t)nb * cap * 4) +     /* sorted */
 	       bp_align(na * 4) +                    /* afail */
 	       bp_align((size_t)nsess * 4) +         /* sseg */
 	       bp_align((size_t)nsess * 32);         /* sout */

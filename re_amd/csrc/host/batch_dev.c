@@ -1207,7 +1207,7 @@ static int mfold(struct dcall *k, int phase, const uint32_t *nfail,
  *
  * w->bp: ticket words | bin counters | bucket counters (BP_HEAD, zero
  * between calls) | bucket entries | sorted | fail words | sseg | sout |
- * launch order | bin places
+ * launch order
  */
 #define BP_HEAD (512u + 4u * SGPU_BP_NBMAX)
 
@@ -1252,7 +1252,7 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		err = pool_reserve(w, &w->bp, BP_HEAD +
 				   sgpu_bplan_scratch((uint32_t)n,
 						      (uint32_t)nsess, nb, cap) +
-				   2 * (n * 4 + 256));
+				   n * 4 + 256);
 	if (err)
 		return err;
 	if (w->bp_d != w->bp.d) {
@@ -1297,13 +1297,12 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		(ptr) = (void *)p;                                           \
 		p += ((size_t)(bytes) + 255) & ~(size_t)255;                 \
 	} while (0)
-	BP_TAKE(B->tmp, (size_t)nb * cap * 4);
+	BP_TAKE(B->tmp, (size_t)nb * cap * 16);
 	BP_TAKE(B->sorted, (size_t)nb * cap * 4);
 	BP_TAKE(B->afail, na * 4);
 	BP_TAKE(B->sseg, nsess * 4);
 	BP_TAKE(B->sout, nsess * sizeof(struct sgpu_sstate));
 	BP_TAKE(B->order, n * 4);
-	BP_TAKE(B->ooff, n * 4);
 #undef BP_TAKE
 	B->sst = sgpu_sst_table();
 	B->out = (struct sgpu_plan_out *)w->pl.d;

@@ -510,8 +510,9 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  *   sgpu_bplan_scatter  per packet: header parse (rtp_hdr_decode), window
  *                       checks, end copy; its bucket slot by an atomic per
  *                       (workgroup, bucket), the entry packed as
- *                       index | length bin << 26 (SPF_SEG past cap); its
- *                       place in its length bin likewise (ooff)
+ *                       16-byte entry of everything the plan needs
+ *                       (SPF_SEG past cap); its place in its length bin
+ *                       likewise
  *   sgpu_bplan_plan     per bucket (one workgroup): the sessions' resident
  *                       states (+ uploads), the entries sorted by session
  *                       and packet index in LDS, the speculation of
@@ -537,6 +538,11 @@ int   sgpu_mplan_rtp(const struct sgpu_mplan_in *in,
  * taken only when there are misses).  bcount / obins / ticket must be zero
  * before the first launch of a workspace; every call leaves them so.
  */
+#ifdef __HIPCC__
+typedef uint4 uint4_t_;
+#else
+typedef struct { uint32_t x, y, z, w; } uint4_t_;
+#endif
 #define SGPU_BP_BLOCK 1024
 #define SGPU_BP_PPT 4           /* scatter: packets per thread */
 #define SGPU_BP_CAPMAX 4096     /* entries per bucket */
@@ -561,11 +567,12 @@ struct sgpu_bplan {
 	struct sgpu_hdr *hdr;
 	uint64_t *desc;
 	uint32_t *order;                /* crypto launch order (n) */
-	uint32_t *tmp;                  /* nb x cap bucket entries */
+	uint4_t_ *tmp;                  /* nb x cap bucket entries: index |
+					   bin << 26, seq | session in bucket
+					   << 16, SSRC, place in the bin */
 	uint32_t *sorted;               /* nb x cap: packet index by session */
 	uint32_t *bcount;               /* nb: entries per bucket (zeroed) */
 	uint32_t *obins;                /* 64: packets per length bin (zeroed) */
-	uint32_t *ooff;                 /* n: a packet's place in its bin */
 	uint32_t *ticket;               /* the fold's last-workgroup ticket
 					   (zero between calls) */
 	uint32_t *afail;                /* per scatter workgroup */

@@ -641,6 +641,135 @@ extern "C" int sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
 			      uint64_t *desc, struct sgpu_plan_out *out,
 			      void *stream);
 
+/* the E || index word of SRTCP packet i (k_parse's eix word for the
+ * stream's tag length) */
+__device__ __forceinline__ uint32_t rp_word(const uint8_t *arena, uint64_t asz,
+					    uint32_t p, uint32_t e,
+					    uint32_t tag)
+{
+	const uint32_t left = (e > p && e <= asz) ? e - p : 0u;
+	if (left < 12u + tag)
+		return 0;
+	const uint8_t *q = arena + e - 4u - tag;
+	return (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 |
+	       (uint32_t)q[2] << 8 | q[3];
+}
+
+/* k_parse (SRTCP form) + k_plan_rtcp + k_plan_finish's results in one
+ * launch (srtpgpu.h struct sgpu_rfused; srtcp.c:31-140, 143-287) */
+__global__ void __launch_bounds__(PLAN_BLOCK)
+k_rp_plan(const uint8_t *__restrict__ arena, uint64_t asz,
+	  const struct sgpu_rfused R)
+{
+	__shared__ uint32_t ssrc0s, vw[PLAN_BLOCK + 1];
+	const struct sgpu_rplan_in &in = R.in;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t i = blockIdx.x * PLAN_BLOCK + tid;
+	if (tid == 0) {
+		/* packet 0's SSRC (get_rtcp_ssrc, srtcp.c:19-29) */
+		const uint32_t q = R.pos[0], qe = R.end[0];
+		const uint32_t left = (qe > q && qe <= asz) ? qe - q : 0u;
+		ssrc0s = left >= 8 ? (uint32_t)arena[q + 4] << 24 |
+				     (uint32_t)arena[q + 5] << 16 |
+				     (uint32_t)arena[q + 6] << 8 | arena[q + 7]
+				   : 0u;
+		if (blockIdx.x == 0) {
+			/* the next launch's counters; the context index */
+			R.out_next->fail = 0;
+			R.out_next->nfail = 0;
+			if (R.cm_out)
+				*R.cm_out = R.comp;
+		}
+		/* the packet before the workgroup's first (the replay order) */
+		vw[0] = (!in.prot && i > 0 && i - 1 < in.n) ?
+			rp_word(arena, asz, R.pos[i - 1], R.end[i - 1], in.tag)
+			: 0u;
+	}
+	const bool live = i < in.n;
+	uint32_t p = 0, e = 0, c = 0, v = 0;
+	struct sgpu_hdr h;
+	h.ssrc = 0; h.seq = 0; h.err_pos = 0; h.hdr_len = 0xffffffffu;
+	if (live) {
+		p = R.pos[i];
+		e = R.end[i];
+		c = R.cap ? R.cap[i] : 0u;
+		const uint32_t left = (e > p && e <= asz) ? e - p : 0u;
+		if (left >= 8) {
+			const uint8_t *b = arena + p;
+			h.ssrc = (uint32_t)b[4] << 24 | (uint32_t)b[5] << 16 |
+				 (uint32_t)b[6] << 8 | b[7];
+			h.hdr_len = 8;
+		}
+		if (!in.prot)
+			v = rp_word(arena, asz, p, e, in.tag);
+		R.hdr[i] = h;
+		R.es[i] = e;
+	}
+	vw[tid + 1] = v;
+	__syncthreads();
+	if (!live)
+		return;
+	const uint32_t ssrc0 = in.ssrc_any ? ssrc0s : in.ssrc;
+	const uint32_t L = e - p;
+	uint32_t f = 0;
+	if (h.hdr_len == 0xffffffffu)
+		f |= SPF_PARSE;                 /* < 8 bytes: EBADMSG */
+	else if (h.ssrc != ssrc0)
+		f |= SPF_SSRC;
+	if ((p & 3u) || p > e || e > asz || (R.cap && (e > c || c > asz)))
+		f |= SPF_BAD;
+	if (L >= in.maxlen)
+		f |= SPF_SIZE;
+	uint32_t ix, E;
+	if (in.prot) {
+		if (R.cap && (uint64_t)e + in.need > (uint64_t)c)
+			f |= SPF_CAP;           /* ENOMEM (cap_short) */
+		ix = (in.rtcp_index + i + 1u) & 0x7fffffffu;    /* srtcp.c:54 */
+		E = in.encrypted;
+	}
+	else {
+		/* srtcp.c:166-172 (and 239-241 for GCM) */
+		if (L < 8u + 4u + in.tag + (in.gcm ? 16u : 0u))
+			f |= SPF_PARSE;
+		ix = v & 0x7fffffffu;
+		E = v >> 31;
+		if (in.hmac) {
+			/* replay (srtcp.c:208-209), speculated: every index new
+			 * and increasing */
+			bool ok;
+			if (i == 0) {
+				if (ix > in.lix) {
+					ok = true;
+				}
+				else {
+					const uint64_t dl = in.lix - ix;
+					ok = dl < 64 && !(in.bitmap & (1ull << dl));
+				}
+			}
+			else {
+				ok = ix > (vw[tid] & 0x7fffffffu);
+			}
+			if (!ok)
+				f |= SPF_REPLAY;
+		}
+	}
+	R.desc[i] = ((uint64_t)(ix & 0x7fffffffu)) | ((uint64_t)E << 31) |
+		    ((uint64_t)SD_RUN << 48);
+	const uint32_t t0 = in.n > SGPU_PLAN_TAIL ? in.n - SGPU_PLAN_TAIL : 0u;
+	if (i >= t0)
+		R.out->tail_ix[i - t0] = ix;
+	if (i == 0) {
+		R.out->ssrc0 = h.ssrc;
+		R.out->hl0 = 8;
+	}
+	/* k_plan_finish's results (the host puts the ends back if the plan
+	 * fails anywhere) */
+	R.end[i] = e + (uint32_t)R.delta;
+	R.err[i] = 0;
+	if (f)
+		atomicOr(&R.out->fail, f);
+}
+
 /* ================================================================== */
 /* C-ABI shim                                                          */
 
@@ -2105,6 +2234,18 @@ extern "C" int sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
 	hipLaunchKernelGGL(k_plan_results, dim3((n + 255) / 256), dim3(256), 0,
 			   (hipStream_t)stream, guard, end0, end, err, n, delta);
 	return herr(hipGetLastError(), "results launch");
+}
+
+extern "C" int sgpu_run_rpplan(const uint8_t *arena, uint64_t arena_size,
+			       const struct sgpu_rfused *r, void *stream)
+{
+	if (!r->in.n)
+		return EINVAL;
+	hipLaunchKernelGGL(k_rp_plan, dim3((r->in.n + PLAN_BLOCK - 1) /
+					   PLAN_BLOCK),
+			   dim3(PLAN_BLOCK), 0, (hipStream_t)stream, arena,
+			   arena_size, *r);
+	return herr(hipGetLastError(), "rtcp plan launch");
 }
 
 extern "C" int sgpu_memcpy_d2d(void *dst, const void *src, size_t n,

@@ -526,6 +526,34 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
  * fold after the synchronisation; queued behind for asynchronous calls).
  * Same workspace state as fz_issue (w->fz: tickets, epochs, plan outs).
  */
+/* the fused / one-launch planners' workspace state (w->fz: ticket |
+ * (plan out, fold out) x 2 | look-back words for nblk workgroups), zeroed
+ * on a new pool, an epoch wrap or the fzepoch hook */
+static int fz_prepare(struct ws *w, uint32_t nblk, void *stream)
+{
+	int err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_SLOT +
+			       (size_t)nblk * 8);
+	const long e = __atomic_exchange_n(&g_env.fzepoch, 0,
+					   __ATOMIC_RELAXED);
+	if (err)
+		return err;
+	if (e > 0 && e <= 0xffff)
+		w->fz_d = NULL;
+	if (w->fz_d != w->fz.d || w->fz_epoch == 0 ||
+	    w->fz_epoch > 0xffffu) {
+		err = sgpu_memset(w->fz.d, 0, w->fz.cap, stream);
+		if (err)
+			return err;
+		w->fz_d = w->fz.d;
+		w->fz_epoch = 1;
+		w->fz_tbase = 0;
+		w->fz_par = 0;
+	}
+	if (e > 0 && e <= 0xffff)
+		w->fz_epoch = (uint32_t)e;
+	return 0;
+}
+
 static int lp_issue(struct dcall *k, int sync)
 {
 	const int prot = k->op == OP_RTP_ENC;
@@ -557,29 +585,10 @@ static int lp_issue(struct dcall *k, int sync)
 	if (!err)
 		err = pool_reserve(w, &w->pl, 64 + (n / 256 + 4) * 20);
 	if (!err)
-		err = pool_reserve(w, &w->fz, FZ_HEAD + 2 * FZ_SLOT +
-				   (size_t)nblk * 8);
+		err = fz_prepare(w, nblk, stream);
 	if (err)
 		return err;
 	fz = w->fz.d;
-	{
-		const long e = __atomic_exchange_n(&g_env.fzepoch, 0,
-						   __ATOMIC_RELAXED);
-		if (e > 0 && e <= 0xffff)
-			w->fz_d = NULL;
-		if (w->fz_d != fz || w->fz_epoch == 0 ||
-		    w->fz_epoch > 0xffffu) {
-			err = sgpu_memset(fz, 0, w->fz.cap, stream);
-			if (err)
-				return err;
-			w->fz_d = fz;
-			w->fz_epoch = 1;
-			w->fz_tbase = 0;
-			w->fz_par = 0;
-		}
-		if (e > 0 && e <= 0xffff)
-			w->fz_epoch = (uint32_t)e;
-	}
 	poff = FZ_HEAD + (size_t)w->fz_par * FZ_SLOT;
 	k->foff = poff;
 
@@ -1022,15 +1031,177 @@ int dev_splanned(int op, struct srtp *s, struct srtp_batch_dev *d)
 	return dev_splanned_finish(&k);
 }
 
+/* the SRTCP plan input of a batch of n packets on session s */
+static void rplan_in(struct sgpu_rplan_in *in, const struct srtp *s,
+		     uint32_t n, int prot)
+{
+	const struct comp *c0 = &s->rtcp;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const uint32_t T = c0->tag_len;             /* 0 for GCM */
+	memset(in, 0, sizeof(*in));
+	in->n = n;
+	in->prot = (uint32_t)prot;
+	in->ssrc_any = !s->nstreams;
+	in->ssrc = s->nstreams ? s->streams[0].ssrc : 0;
+	in->rtcp_index = s->nstreams ? s->streams[0].rtcp_index : 0;
+	in->lix = s->nstreams ? s->streams[0].replay_rtcp.lix : 0;
+	in->bitmap = s->nstreams ? s->streams[0].replay_rtcp.bitmap : 0;
+	in->tag = T;
+	in->gcm = (uint32_t)gcm;
+	in->hmac = (uint32_t)c0->has_hmac;
+	in->encrypted = (uint32_t)(gcm ? c0->encrypted : c0->has_aes);
+	in->need = 4u + T + (gcm ? 16u : 0u);
+	in->maxlen = SGPU_CACHED_MAX(c0->mode);
+}
+
+/* the stream (stream.c:45-67) and its SRTCP state after an accepted
+ * plan; *old: the state before */
+static void rplan_apply(struct srtp *s, const struct sgpu_plan_out *po,
+			int prot, size_t n, struct srtp_stream *old)
+{
+	if (!s->nstreams) {
+		memset(&s->streams[0], 0, sizeof(s->streams[0]));
+		s->streams[0].ssrc = po->ssrc0;
+		s->nstreams = 1;
+	}
+	*old = s->streams[0];
+	if (prot)
+		s->streams[0].rtcp_index =
+			(s->streams[0].rtcp_index + (uint32_t)n) & 0x7fffffffu;
+	else if (s->rtcp.has_hmac)
+		s->streams[0].replay_rtcp =
+			plan_replay(&s->streams[0].replay_rtcp, po->tail_ix, n);
+}
+
+/*
+ * Single-stream SRTCP batch planned in one launch (k_rp_plan: the parse,
+ * every check of k_plan_rtcp, desc, the optimistic results) in front of
+ * the single-key crypto kernel, which it guards with out->fail and whose
+ * misses it counts in out->nfail; one copy and one synchronisation.
+ * -1: not plannable (the ends put back) or a forged packet (undone), else
+ * 0 / errno.
+ */
+static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
+{
+	const int prot = op == OP_RTCP_ENC;
+	const struct comp *c0 = &s->rtcp;
+	const int gcm = c0->mode == SGPU_MODE_GCM;
+	const size_t n = d->n;
+	const uint32_t grow = 4u + c0->tag_len + (gcm ? 16u : 0u);
+	const unsigned ns0 = s->nstreams;
+	struct srtp_stream old;
+	struct sgpu_rfused R;
+	struct sgpu_plan_out *po, *po_d;
+	uint8_t *vd_d;
+	uint32_t *save_d;
+	void *stream = d->stream;
+	struct ws *w = ws_get();
+	size_t poff;
+	int err;
+
+	if (!w)
+		return ENOMEM;
+	err = pool_reserve(w, &w->hd, n * sizeof(struct sgpu_hdr));
+	if (!err)
+		err = pool_reserve(w, &w->dsc, n * 8);
+	if (!err)
+		err = pool_reserve(w, &w->vs, n * 5 + 64);
+	if (!err)
+		err = pool_reserve(w, &w->cm, 4);
+	if (!err)
+		err = pool_reserve(w, &w->es, n * 4);
+	if (!err)
+		err = fz_prepare(w, 1, stream);
+	if (err)
+		return err;
+	poff = FZ_HEAD + (size_t)w->fz_par * FZ_SLOT;
+	po = (struct sgpu_plan_out *)(w->fz.h + poff);
+	po_d = (struct sgpu_plan_out *)(w->fz.d + poff);
+	save_d = (uint32_t *)(w->vs.d + 64);
+	vd_d = w->vs.d + 64 + n * 4;
+	memset(&R, 0, sizeof(R));
+	rplan_in(&R.in, s, (uint32_t)n, prot);
+	R.pos = d->pos;
+	R.end = d->end;
+	R.cap = d->cap;
+	R.err = d->err;
+	R.es = (uint32_t *)w->es.d;
+	R.hdr = (struct sgpu_hdr *)w->hd.d;
+	R.desc = (uint64_t *)w->dsc.d;
+	R.out = po_d;
+	R.out_next = (struct sgpu_plan_out *)(w->fz.d + FZ_HEAD +
+					      (size_t)(w->fz_par ^ 1) * FZ_SLOT);
+	R.cm_out = (uint32_t *)w->cm.d;
+	R.comp = c0->dev;
+	R.delta = prot ? (int32_t)grow : -(int32_t)grow;
+	err = sgpu_run_rpplan(d->arena, d->arena_size, &R, stream);
+	if (err) {
+		w->fz_d = NULL;
+		return err;
+	}
+	w->fz_par ^= 1;
+	{
+		/* CTR: the lean kernel's SRTCP form (srtp_gpu_tune nolean: the
+		 * general compact kernel) */
+		struct sgpu_compact C = {
+			d->pos, R.es, R.hdr, R.desc, NULL, R.cm_out, NULL, 0,
+			(uint32_t)n, vd_d, save_d, &po_d->nfail, 0,
+			gcm || g_env.nolean ? 1 : 4, &po_d->fail, 1, NULL, NULL};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	if (po->fail) {
+		/* the crypto launch did nothing: the ends go back */
+		count(&g_cnt_rejects, 1);
+		err = sgpu_memcpy_d2d(d->end, R.es, n * 4, stream);
+		if (!err)
+			err = sgpu_stream_sync(stream);
+		return err ? err : -1;
+	}
+	count(&g_cnt_rplans, 1);
+	rplan_apply(s, po, prot, n, &old);
+	if (!po->nfail)
+		return 0;
+	count(&g_cnt_misses, po->nfail);
+	count(&g_cnt_folds, 1);
+	/* a forged packet: undo on the device, fold on the host engine */
+	{
+		struct sgpu_compact C = {
+			d->pos, R.es, R.hdr, R.desc, NULL, R.cm_out, NULL, 0,
+			(uint32_t)n, vd_d, save_d, &po_d->nfail, 1, gcm ? 0 : 1,
+			&po_d->fail, 1, NULL, NULL};
+		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
+				       (int)c0->nr, gcm ? 0 : 2, 0, stream);
+	}
+	if (!err)
+		err = sgpu_memcpy_d2d(d->end, R.es, n * 4, stream);
+	if (!err)
+		err = sgpu_stream_sync(stream);
+	if (err)
+		return err;
+	s->streams[0] = old;
+	s->nstreams = ns0;
+	return -1;
+}
+
 /*
  * Single-stream SRTCP batch planned and processed on the device (the
- * SRTCP counterpart of dev_planned): k_parse (with the E || index words),
+ * SRTCP counterpart of dev_planned): by default the one-launch plan above;
+ * srtp_gpu_tune noplanfuse: k_parse (with the E || index words),
  * k_plan_rtcp, the compact crypto launch, the per-packet results; one host
  * synchronisation.  -1: not plannable or a forged packet (undone), else 0
  * / errno.
  */
 int dev_planned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 {
+	if (!g_env.noplanfuse)
+		return dev_lplanned_rtcp(op, s, d);
 	const int prot = op == OP_RTCP_ENC;
 	const struct comp *c0 = &s->rtcp;
 	const int gcm = c0->mode == SGPU_MODE_GCM;

@@ -630,6 +630,29 @@ struct sgpu_rplan_in {
 	uint32_t pad;
 };
 
+/* the same plan in one launch with the header parse and the results
+ * (k_rp_plan): per packet hdr, es, desc and, optimistically, end / err
+ * (the host puts the ends back if the plan fails); out is the call's
+ * plan out (fail, nfail zeroed by the launch before, through out_next),
+ * out->fail the crypto launch's guard, out->nfail its miss counter;
+ * *cm_out = comp */
+struct sgpu_rfused {
+	struct sgpu_rplan_in in;
+	const uint32_t *pos;
+	uint32_t *end;
+	const uint32_t *cap;            /* or NULL */
+	int32_t *err;
+	uint32_t *es;
+	struct sgpu_hdr *hdr;
+	uint64_t *desc;
+	struct sgpu_plan_out *out, *out_next;
+	uint32_t *cm_out;
+	uint32_t comp;
+	int32_t delta;
+};
+int   sgpu_run_rpplan(const uint8_t *arena, uint64_t arena_size,
+		      const struct sgpu_rfused *r, void *stream);
+
 int   sgpu_plan_rtcp(const struct sgpu_rplan_in *in,
 		     const struct sgpu_hdr *hdr, const uint32_t *eix,
 		     const uint32_t *pos, const uint32_t *end,

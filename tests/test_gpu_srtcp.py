@@ -1,5 +1,6 @@
-"""SRTCP batches planned on the device (srtcp_*_batch_dev, dev_planned_rtcp
-and k_plan_rtcp), through the C-ABI library, against the oracle called one
+"""SRTCP batches planned on the device (srtcp_*_batch_dev, dev_planned_rtcp:
+the one-launch plan k_rp_plan, and with srtp_gpu_tune noplanfuse k_parse +
+k_plan_rtcp), through the C-ABI library, against the oracle called one
 packet at a time (srtcp_encrypt srtcp.c:31-140, srtcp_decrypt
 srtcp.c:143-287): every suite, SRTP_UNENCRYPTED_SRTCP, two consecutive
 batches per direction (the SRTCP index and replay window carried over),
@@ -71,9 +72,17 @@ def counters():
     return P.counter("rejects"), P.counter("folds")
 
 
+@pytest.mark.parametrize("sep", [0, 1])
 @pytest.mark.parametrize("flags", [0, P.SRTP_UNENCRYPTED_SRTCP])
 @pytest.mark.parametrize("suite", list(range(6)))
-def test_srtcp_device_planned_vs_oracle(torch_cuda, suite, flags):
+def test_srtcp_device_planned_vs_oracle(torch_cuda, suite, flags, sep):
+    """sep: the separate planner launches (noplanfuse) instead of the
+    one-launch plan"""
+    with P.tune(noplanfuse=sep):
+        srtcp_planned_vs_oracle(torch_cuda, suite, flags)
+
+
+def srtcp_planned_vs_oracle(torch_cuda, suite, flags):
     torch = torch_cuda
     rng = np.random.default_rng(31 + suite + 7 * flags)
     key = keys_for(suite, 1)[0]
@@ -101,8 +110,14 @@ def test_srtcp_device_planned_vs_oracle(torch_cuda, suite, flags):
         ob.free(c)
 
 
+@pytest.mark.parametrize("sep", [0, 1])
 @pytest.mark.parametrize("suite", [1, 4])
-def test_srtcp_fallbacks_vs_oracle(torch_cuda, suite):
+def test_srtcp_fallbacks_vs_oracle(torch_cuda, suite, sep):
+    with P.tune(noplanfuse=sep):
+        srtcp_fallbacks_vs_oracle(torch_cuda, suite)
+
+
+def srtcp_fallbacks_vs_oracle(torch_cuda, suite):
     torch = torch_cuda
     rng = np.random.default_rng(77 + suite)
     key = keys_for(suite, 1)[0]

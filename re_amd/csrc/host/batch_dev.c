@@ -639,39 +639,20 @@ static int lp_issue(struct dcall *k, int sync)
 		if (err)
 			return err;
 	}
-	k->devfold = !sync && !prot && !g_env.nodevfold;
-	if (!sync) {
-		/* queued behind: forged packets' ciphertext (AES-CM) and the
-		 * verdict fold (unprotect), the chained gate word */
-		struct sgpu_fold_out *fo_d =
-			(struct sgpu_fold_out *)(fz + poff + FZ_FO_OFF);
-		uint32_t *fscr = (uint32_t *)(w->pl.d + 64);
-		if (k->devfold) {
-			if (!gcm)
-				err = sgpu_fused_refix(d->arena, d->arena_size, F,
-						       (int)c0->nr, stream);
-			if (!err)
-				err = sgpu_fold_rtp(1, &F->out->nfail, &F->in,
-						    F->hdr, F->desc, F->verdict,
-						    F->es, d->pos, d->end, d->err,
-						    gcm, fscr, fo_d, stream);
-		}
-		if (!err && k->gate)
-			err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0,
-					       0, &F->out->nfail, k->gate, NULL,
-					       k->devfold ? &fo_d->fail : NULL,
-					       stream);
-		if (!err && k->devfold)
-			err = sgpu_fold_rtp(2, &F->out->nfail, &F->in, F->hdr,
-					    F->desc, F->verdict, F->es, d->pos,
-					    d->end, d->err, gcm, fscr, fo_d,
-					    stream);
-	}
+	/* asynchronous calls: only the chained gate word is queued behind
+	 * (set if the plan failed or a tag did not verify).  Forged packets'
+	 * restore and verdict fold run when the call is waited for, as for a
+	 * synchronous call -- a chained call queued behind one with misses
+	 * is then gated and re-run (the zero-miss fold launches cost every
+	 * call ~25 us; a miss costs the call behind it a host round trip) */
+	k->devfold = 0;
+	if (!sync && k->gate)
+		err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0, 0,
+				       &F->out->nfail, k->gate, NULL, NULL,
+				       stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
-				      k->devfold ? FZ_SLOT
-						 : sizeof(struct sgpu_plan_out),
-				      stream);
+				      sizeof(struct sgpu_plan_out), stream);
 	return err;
 }
 
@@ -718,7 +699,8 @@ static int lp_finish(struct dcall *k, int sync)
 	if (!po->nfail)
 		return 0;
 	count(&g_cnt_misses, po->nfail);
-	if (sync && !g_env.nodevfold) {
+	(void)sync;
+	if (!g_env.nodevfold) {
 		struct sgpu_fold_out *fo_d =
 			(struct sgpu_fold_out *)(w->fz.d + poff + FZ_FO_OFF);
 		err = 0;

@@ -687,6 +687,10 @@ static int lp_finish(struct dcall *k, int sync)
 		if ((po->fail & SPF_SSRC) && !ns0)
 			__atomic_store_n(&g_fresh_multi, 1, __ATOMIC_RELAXED);
 		count(&g_cnt_rejects, 1);
+		if (g_env.times)
+			fprintf(stderr, "re_srtp plan n=%zu %s: rejected "
+				"(SPF %#x)\n", n, prot ? "protect" : "unprotect",
+				po->fail);
 		/* the crypto launch did nothing: only the ends the plan wrote
 		 * go back */
 		err = sgpu_memcpy_d2d(d->end, F->es, n * 4, stream);
@@ -1141,6 +1145,10 @@ static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (po->fail) {
 		/* the crypto launch did nothing: the ends go back */
 		count(&g_cnt_rejects, 1);
+		if (g_env.times)
+			fprintf(stderr, "re_srtp rtcp plan n=%zu %s: rejected "
+				"(SPF %#x)\n", n, prot ? "protect" : "unprotect",
+				po->fail);
 		err = sgpu_memcpy_d2d(d->end, R.es, n * 4, stream);
 		if (!err)
 			err = sgpu_stream_sync(stream);

@@ -655,8 +655,8 @@ __device__ __forceinline__ uint32_t rp_word(const uint8_t *arena, uint64_t asz,
 	       (uint32_t)q[2] << 8 | q[3];
 }
 
-/* k_parse (SRTCP form) + k_plan_rtcp + k_plan_finish's results in one
- * launch (srtpgpu.h struct sgpu_rfused; srtcp.c:31-140, 143-287) */
+/* k_parse (SRTCP form) + k_plan_rtcp in one launch (srtpgpu.h struct
+ * sgpu_rfused; srtcp.c:31-140, 143-287) */
 __global__ void __launch_bounds__(PLAN_BLOCK)
 k_rp_plan(const uint8_t *__restrict__ arena, uint64_t asz,
 	  const struct sgpu_rfused R)
@@ -762,10 +762,8 @@ k_rp_plan(const uint8_t *__restrict__ arena, uint64_t asz,
 		R.out->ssrc0 = h.ssrc;
 		R.out->hl0 = 8;
 	}
-	/* k_plan_finish's results (the host puts the ends back if the plan
-	 * fails anywhere) */
-	R.end[i] = e + (uint32_t)R.delta;
-	R.err[i] = 0;
+	/* (no results here: the workgroup after this one reads this
+	 * packet's end for its replay order) */
 	if (f)
 		atomicOr(&R.out->fail, f);
 }

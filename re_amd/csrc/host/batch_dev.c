@@ -1061,11 +1061,11 @@ static void rplan_apply(struct srtp *s, const struct sgpu_plan_out *po,
 
 /*
  * Single-stream SRTCP batch planned in one launch (k_rp_plan: the parse,
- * every check of k_plan_rtcp, desc, the optimistic results) in front of
- * the single-key crypto kernel, which it guards with out->fail and whose
- * misses it counts in out->nfail; one copy and one synchronisation.
- * -1: not plannable (the ends put back) or a forged packet (undone), else
- * 0 / errno.
+ * every check of k_plan_rtcp, desc) in front of the single-key crypto
+ * kernel, which it guards with out->fail and whose misses it counts in
+ * out->nfail, then the guarded results; one copy and one
+ * synchronisation.  -1: not plannable (nothing modified) or a forged
+ * packet (undone), else 0 / errno.
  */
 static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 {
@@ -1136,6 +1136,9 @@ static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_run_compact(d->arena, d->arena_size, &C, c0->mode,
 				       (int)c0->nr, gcm ? 0 : 2, prot, stream);
 	}
+	if (!err)   /* the results, guarded by the plan */
+		err = sgpu_plan_results(&po_d->fail, R.es, d->end, d->err,
+					(uint32_t)n, R.delta, stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
 	if (!err)
@@ -1143,16 +1146,13 @@ static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (err)
 		return err;
 	if (po->fail) {
-		/* the crypto launch did nothing: the ends go back */
+		/* the crypto launch and the results did nothing */
 		count(&g_cnt_rejects, 1);
 		if (g_env.times)
 			fprintf(stderr, "re_srtp rtcp plan n=%zu %s: rejected "
 				"(SPF %#x)\n", n, prot ? "protect" : "unprotect",
 				po->fail);
-		err = sgpu_memcpy_d2d(d->end, R.es, n * 4, stream);
-		if (!err)
-			err = sgpu_stream_sync(stream);
-		return err ? err : -1;
+		return -1;
 	}
 	count(&g_cnt_rplans, 1);
 	rplan_apply(s, po, prot, n, &old);

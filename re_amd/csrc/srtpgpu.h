@@ -630,9 +630,10 @@ struct sgpu_rplan_in {
 	uint32_t pad;
 };
 
-/* the same plan in one launch with the header parse and the results
- * (k_rp_plan): per packet hdr, es, desc and, optimistically, end / err
- * (the host puts the ends back if the plan fails); out is the call's
+/* the same plan in one launch with the header parse (k_rp_plan): per
+ * packet hdr, es and desc (not the results: the workgroup after reads a
+ * packet's end for the replay order -- sgpu_plan_results behind the
+ * crypto launch writes them); out is the call's
  * plan out (fail, nfail zeroed by the launch before, through out_next),
  * out->fail the crypto launch's guard, out->nfail its miss counter;
  * *cm_out = comp */

@@ -232,6 +232,9 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * "perclass" (one CTR launch per header class), "nolean" (the general
  * CTR kernels for device-planned batches), "nocoop" (small host-planned
  * CTR launches keep the cipher in the one-packet-per-lane kernel),
+ * "lplan" (single-stream AES-CM batches planned by the one-launch planner
+ * in front of the lean kernel instead of inside the crypto launch; GCM
+ * batches always take the one-launch planner),
  * "mpradix" (multi-session plans group packets by the radix sort),
  * "nobucket" (multi-session plans by the counting grouping of
  * plan_multi.hip instead of the four-launch bucket planner),

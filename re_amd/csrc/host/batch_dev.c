@@ -41,7 +41,7 @@ static int lp_finish(struct dcall *k, int sync);
 int dev_planned_issue(struct dcall *k)
 {
 	if (!g_env.noplanfuse) {
-		if (k->sessv[0]->rtp.mode == SGPU_MODE_CTR && g_env.fusedplan) {
+		if (k->sessv[0]->rtp.mode == SGPU_MODE_CTR && !g_env.lplan) {
 			k->fused = 1;
 			return fz_issue(k, 0);
 		}
@@ -793,7 +793,7 @@ int dev_planned(int op, struct srtp *s, struct srtp_batch_dev *d,
 	struct dcall k;
 	int err;
 	if (!g_env.noplanfuse) {
-		if (s->rtp.mode == SGPU_MODE_CTR && g_env.fusedplan)
+		if (s->rtp.mode == SGPU_MODE_CTR && !g_env.lplan)
 			return dev_fused(op, s, d, pfail);
 		return dev_lplanned(op, s, d, pfail);
 	}

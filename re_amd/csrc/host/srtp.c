@@ -254,8 +254,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nocombine = value > 0;
 	else if (!strcmp(name, "nosmall"))
 		g_env.nosmall = value > 0;
-	else if (!strcmp(name, "fusedplan"))
-		g_env.fusedplan = value > 0;
+	else if (!strcmp(name, "lplan"))
+		g_env.lplan = value > 0;
 	else if (!strcmp(name, "noplanfuse"))
 		g_env.noplanfuse = value > 0;
 	else if (!strcmp(name, "fzepoch"))

@@ -116,10 +116,12 @@ struct srtp_env {
 	int smallsync;          /* srtp_gpu_tune smallsync: wait for a small
 				   launch by a stream synchronisation, not
 				   its completion word */
-	int fusedplan;          /* srtp_gpu_tune fusedplan: single-stream
-				   AES-CM batches planned inside the crypto
-				   launch (k_ctr_fused), not by the one-launch
-				   planner in front of the lean kernel */
+	int lplan;              /* srtp_gpu_tune lplan: single-stream AES-CM
+				   batches planned by the one-launch planner
+				   (k_lp_plan) in front of the lean kernel,
+				   not inside the crypto launch (k_ctr_fused,
+				   the default: measured 498 vs 490 GiB/s on
+				   one box, profiles/r06/lplan_ab.txt) */
 	int noplanfuse;         /* srtp_gpu_tune noplanfuse: single-stream
 				   batches take the separate device planner
 				   (k_parse + k_plan_*), not the plan inside

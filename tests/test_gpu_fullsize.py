@@ -89,23 +89,23 @@ def session_states(ctxs, rtcp=False):
 
 # per (config, direction): the counters that must move by exactly the
 # given amount in that call ("rejects" and "folds" -- a host re-plan or a
-# host fold -- must stay 0 unless listed).  lplans: the one-launch plan
-# (k_lp_plan) in front of the lean kernel (AES-CM and GCM); fused: the
-# in-launch plan (k_ctr_fused, srtp_gpu_tune fusedplan); dplans: the
-# separate single-stream planner launches (noplanfuse);
+# host fold -- must stay 0 unless listed).  fused: the in-launch plan of
+# single-stream AES-CM batches (k_ctr_fused); lplans: the one-launch plan
+# (k_lp_plan) in front of the lean kernel (GCM); dplans: the separate
+# single-stream planner launches (noplanfuse);
 # mplans: the multi-session planner; rplans: the SRTCP planner; devfolds:
 # forged packets' verdicts folded on the device.
 COUNTERS = ("lplans", "fused", "dplans", "mplans", "rplans", "rejects",
             "folds", "devfolds")
 PATHS = {
-    (1, "protect"): {"lplans": 1}, (1, "unprotect"): {"lplans": 1},
-    (2, "protect"): {"lplans": 1}, (2, "unprotect"): {"lplans": 1},
+    (1, "protect"): {"fused": 1}, (1, "unprotect"): {"fused": 1},
+    (2, "protect"): {"fused": 1}, (2, "unprotect"): {"fused": 1},
     (3, "protect"): {"lplans": 1}, (3, "unprotect"): {"lplans": 1},
     (4, "protect"): {"mplans": 1}, (4, "unprotect"): {"mplans": 1},
     (7, "protect"): {"rplans": 1}, (7, "unprotect"): {"rplans": 1},
     (8, "protect"): {"rplans": 1}, (8, "unprotect"): {"rplans": 1},
-    (9, "protect"): {"lplans": 1},
-    (9, "unprotect"): {"lplans": 1, "devfolds": 1},
+    (9, "protect"): {"fused": 1},
+    (9, "unprotect"): {"fused": 1, "devfolds": 1},
     (10, "protect"): {"mplans": 1},
     (10, "unprotect"): {"mplans": 1, "devfolds": 1},
     (11, "protect"): {"lplans": 1},

@@ -2,11 +2,11 @@
 k_ctr_fused.h (parse, every check, the ROC prefix over 1024-packet
 workgroups), in its two forms:
 
-  lplan   the default: the plan as a launch of its own (k_lp_plan, host
-          lp_issue / lp_finish) in front of the lean crypto kernel -- AES-CM
-          (k_ctr_fast_any) and AES-GCM (k_gcmu);
-  fused   srtp_gpu_tune fusedplan (AES-CM only): the plan inside the crypto
-          launch (k_ctr_fused, host dev_fused).
+  fused   the AES-CM default: the plan inside the crypto launch
+          (k_ctr_fused, host dev_fused);
+  lplan   the plan as a launch of its own (k_lp_plan, host lp_issue /
+          lp_finish) in front of the lean crypto kernel -- AES-GCM always,
+          AES-CM with srtp_gpu_tune lplan (k_ctr_fast_any).
 
 Both must give exactly the separate device planner's results
 (srtp_gpu_tune noplanfuse: k_parse + k_plan_* + the lean kernel, pinned by
@@ -75,9 +75,9 @@ GCM = (4, 5)
 
 def modes(suite):
     """(mode, tune knobs, the counter its accepted plans move)"""
-    m = [("lplan", {}, "lplans")]
+    m = [("lplan", {"lplan": 1}, "lplans")]
     if suite not in GCM:
-        m.append(("fused", {"fusedplan": 1}, "fused"))
+        m.append(("fused", {}, "fused"))
     return m + [("planner", {"noplanfuse": 1}, None),
                 ("general", {"general": 1}, None)]
 
@@ -237,8 +237,8 @@ def test_fused_many_launches_sizes_and_epoch_wrap(torch_cuda):
         parts.append(batch(rng, list(range(seq, seq + n))))
         seq += n
     outs = {}
-    for mode, tune, cname in (("lplan", {}, "lplans"),
-                              ("fused", {"fusedplan": 1}, "fused"),
+    for mode, tune, cname in (("lplan", {"lplan": 1}, "lplans"),
+                              ("fused", {}, "fused"),
                               ("planner", {"noplanfuse": 1}, "dplans")):
         ctx = P.Srtp(1, key)
         res = []

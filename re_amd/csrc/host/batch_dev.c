@@ -358,39 +358,19 @@ static int fz_issue(struct dcall *k, int sync)
 	w->fz_tbase += F->ntickets;
 	w->fz_epoch++;
 	w->fz_par ^= 1;
-	k->devfold = !sync && !prot && !g_env.nodevfold;
-	if (!sync) {
-		/* queued behind the launch: forged packets' ciphertext and the
-		 * verdict fold (unprotect), the gate word of the next chained
-		 * call (set if this call must be completed on the host) */
-		struct sgpu_fold_out *fo_d =
-			(struct sgpu_fold_out *)(fz + poff + FZ_FO_OFF);
-		uint32_t *fscr = (uint32_t *)(w->pl.d + 64);
-		if (k->devfold) {
-			err = sgpu_fused_refix(d->arena, d->arena_size, F,
-					       (int)c0->nr, stream);
-			if (!err)
-				err = sgpu_fold_rtp(1, &F->out->nfail, &F->in,
-						    F->hdr, F->desc, F->verdict,
-						    F->es, d->pos, d->end, d->err,
-						    0, fscr, fo_d, stream);
-		}
-		if (!err && k->gate)
-			err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0,
-					       0, &F->out->nfail, k->gate, NULL,
-					       k->devfold ? &fo_d->fail : NULL,
-					       stream);
-		if (!err && k->devfold)
-			err = sgpu_fold_rtp(2, &F->out->nfail, &F->in, F->hdr,
-					    F->desc, F->verdict, F->es, d->pos,
-					    d->end, d->err, 0, fscr, fo_d,
-					    stream);
-	}
+	/* asynchronous calls: only the chained gate word is queued behind
+	 * (set if the plan failed or a tag did not verify); forged packets'
+	 * restore and verdict fold run when the call is waited for, as for a
+	 * synchronous call (lp_issue: the zero-miss fold launches cost every
+	 * call ~20 us; a miss costs the chained call behind a host re-run) */
+	k->devfold = 0;
+	if (!sync && k->gate)
+		err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0, 0,
+				       &F->out->nfail, k->gate, NULL, NULL,
+				       stream);
 	if (!err)
 		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
-				      k->devfold ? FZ_SLOT
-						 : sizeof(struct sgpu_plan_out),
-				      stream);
+				      sizeof(struct sgpu_plan_out), stream);
 	return err;
 }
 
@@ -436,7 +416,8 @@ static int fz_finish(struct dcall *k, int sync)
 	if (!po->nfail)
 		return 0;
 	count(&g_cnt_misses, po->nfail);
-	if (sync && !g_env.nodevfold) {
+	(void)sync;
+	if (!g_env.nodevfold) {
 		/* forged packets: ciphertext back, verdicts folded on the
 		 * device; its outcome comes back in one copy */
 		struct sgpu_fold_out *fo_d =

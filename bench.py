@@ -782,10 +782,13 @@ def main():
     torch.cuda.synchronize()
     c_rerun0 = (P.counter("rejects"), P.counter("folds"), P.counter("gated"))
     voided0 = P.counter("prof_voided")
+    SPLIT = ("sync_calls", "sync_ns_issue", "sync_ns_wait", "sync_ns_finish")
+    split0 = [P.counter(c) for c in SPLIT]
     t0 = time.perf_counter()
     errors = run_steps(sess_sets)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    split = [P.counter(c) - v for c, v in zip(SPLIT, split0)]
     if world > 1:
         dist.barrier()
     prof = P.prof_read_named()
@@ -966,6 +969,18 @@ def main():
                               (T / 1) / 1e9 / HBM_PEAK_GBS, 4),
         "errors": int(tot_err),
         "forged_per_batch": nforge,
+        # where a synchronous one-stream call's host time goes (DESIGN
+        # §10.6): issue (plan-out bookkeeping + launches), the stream
+        # wait, completion; "outside" = the rest of the call's share of
+        # the step (the Python loop, the ctypes call, the entry point)
+        "sync_split_us": ({
+            "calls_per_step": round(split[0] / args.steps, 2),
+            "issue": round(split[1] / split[0] / 1e3, 2),
+            "wait": round(split[2] / split[0] / 1e3, 2),
+            "finish": round(split[3] / split[0] / 1e3, 2),
+            "outside": round(elapsed / split[0] * 1e6 -
+                             sum(split[1:]) / split[0] / 1e3, 2),
+        } if split[0] else None),
         "folds": {"device": P.counter("devfolds"),
                   "host": P.counter("folds")},
         "plans": {"rejected": P.counter("rejects"),

@@ -234,7 +234,9 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * CTR launches keep the cipher in the one-packet-per-lane kernel),
  * "lplan" (single-stream AES-CM batches planned by the one-launch planner
  * in front of the lean kernel instead of inside the crypto launch; GCM
- * batches always take the one-launch planner),
+ * batches always take the one-launch planner), "nopost" (single-stream
+ * plan outs come back by a copy and the asynchronous gate word by a launch
+ * of its own, instead of one post launch that does both),
  * "mpradix" (multi-session plans group packets by the radix sort),
  * "nobucket" (multi-session plans by the counting grouping of
  * plan_multi.hip instead of the four-launch bucket planner),

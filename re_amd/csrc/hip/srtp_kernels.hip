@@ -2223,6 +2223,33 @@ extern "C" int sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
 	return herr(hipGetLastError(), "finish launch");
 }
 
+/* the plan out to the caller's pinned mirror with vector stores, and the
+ * chained call's gate word (k_plan_finish's rule): one launch in place of
+ * the gate launch + the blit copy behind every single-stream call (the
+ * copy's completion cost ~10 us before the next launch could start,
+ * profiles/r06 config2a timeline) */
+__global__ void __launch_bounds__(256)
+k_plan_post(const uint32_t *__restrict__ src, uint32_t *__restrict__ host,
+	    uint32_t nwords, uint32_t *gate)
+{
+	const uint32_t i = threadIdx.x;
+	for (uint32_t w = i; w < nwords; w += blockDim.x)
+		host[w] = src[w];
+	if (i == 0 && gate) {
+		const struct sgpu_plan_out *o = (const struct sgpu_plan_out *)src;
+		*gate = o->fail || o->nfail;
+	}
+}
+
+extern "C" int sgpu_plan_post(const void *out, void *host, uint32_t bytes,
+			      uint32_t *gate, void *stream)
+{
+	hipLaunchKernelGGL(k_plan_post, dim3(1), dim3(256), 0,
+			   (hipStream_t)stream, (const uint32_t *)out,
+			   (uint32_t *)host, (bytes + 3u) / 4u, gate);
+	return herr(hipGetLastError(), "post launch");
+}
+
 extern "C" int sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
 				 uint32_t *end, int32_t *err, uint32_t n,
 				 int32_t delta, void *stream)

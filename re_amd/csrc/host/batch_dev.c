@@ -261,6 +261,29 @@ int dev_planned_finish(struct dcall *k)
 #define FZ_FO_OFF ((sizeof(struct sgpu_plan_out) + 63u) & ~(size_t)63)
 #define FZ_SLOT (FZ_FO_OFF + 64u)
 
+/* a single-stream call's plan out back to its pinned mirror, behind the
+ * crypto launch; an asynchronous call also sets its chained gate word
+ * (out->fail || out->nfail: the plan failed or a tag did not verify --
+ * forged packets' restore and verdict fold run when the call is waited
+ * for, as for a synchronous call, and a chained call queued behind one
+ * with misses is gated and re-run; the zero-miss fold launches cost every
+ * call ~25 us, a miss costs the call behind it a host round trip) */
+static int plan_out_back(struct dcall *k, int sync, struct sgpu_plan_out *out,
+			 void *host, void *stream)
+{
+	int err = 0;
+	k->devfold = 0;
+	if (!g_env.nopost)
+		return sgpu_plan_post(out, host, sizeof(*out),
+				      sync ? NULL : k->gate, stream);
+	if (!sync && k->gate)
+		err = sgpu_plan_finish(&out->fail, NULL, NULL, NULL, 0, 0,
+				       &out->nfail, k->gate, NULL, NULL, stream);
+	if (!err)
+		err = sgpu_memcpy_d2h(host, out, sizeof(*out), stream);
+	return err;
+}
+
 static int fz_issue(struct dcall *k, int sync)
 {
 	const int prot = k->op == OP_RTP_ENC;
@@ -358,20 +381,7 @@ static int fz_issue(struct dcall *k, int sync)
 	w->fz_tbase += F->ntickets;
 	w->fz_epoch++;
 	w->fz_par ^= 1;
-	/* asynchronous calls: only the chained gate word is queued behind
-	 * (set if the plan failed or a tag did not verify); forged packets'
-	 * restore and verdict fold run when the call is waited for, as for a
-	 * synchronous call (lp_issue: the zero-miss fold launches cost every
-	 * call ~20 us; a miss costs the chained call behind a host re-run) */
-	k->devfold = 0;
-	if (!sync && k->gate)
-		err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0, 0,
-				       &F->out->nfail, k->gate, NULL, NULL,
-				       stream);
-	if (!err)
-		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
-				      sizeof(struct sgpu_plan_out), stream);
-	return err;
+	return plan_out_back(k, sync, F->out, w->fz.h + poff, stream);
 }
 
 /* ... after its launches completed: 0 / errno, -1 not plannable or a
@@ -483,12 +493,24 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 	*pfail = 0;
 	if (!k.w)
 		return ENOMEM;
-	err = fz_issue(&k, 1);
-	if (!err)
-		err = sgpu_stream_sync(d->stream);
-	if (err)
-		return err;
-	err = fz_finish(&k, 1);
+	{
+		/* where a synchronous call's host time goes (counters
+		 * sync_ns_issue / _wait / _finish) */
+		const uint64_t t0 = mono_ns();
+		uint64_t t1, t2;
+		err = fz_issue(&k, 1);
+		t1 = mono_ns();
+		if (!err)
+			err = sgpu_stream_sync(d->stream);
+		t2 = mono_ns();
+		if (err)
+			return err;
+		err = fz_finish(&k, 1);
+		count(&g_cnt_sync_calls, 1);
+		count(&g_ns_sync_issue, t1 - t0);
+		count(&g_ns_sync_wait, t2 - t1);
+		count(&g_ns_sync_finish, mono_ns() - t2);
+	}
 	*pfail = k.pfail;
 	return err;
 }
@@ -620,21 +642,7 @@ static int lp_issue(struct dcall *k, int sync)
 		if (err)
 			return err;
 	}
-	/* asynchronous calls: only the chained gate word is queued behind
-	 * (set if the plan failed or a tag did not verify).  Forged packets'
-	 * restore and verdict fold run when the call is waited for, as for a
-	 * synchronous call -- a chained call queued behind one with misses
-	 * is then gated and re-run (the zero-miss fold launches cost every
-	 * call ~25 us; a miss costs the call behind it a host round trip) */
-	k->devfold = 0;
-	if (!sync && k->gate)
-		err = sgpu_plan_finish(&F->out->fail, NULL, NULL, NULL, 0, 0,
-				       &F->out->nfail, k->gate, NULL, NULL,
-				       stream);
-	if (!err)
-		err = sgpu_memcpy_d2h(w->fz.h + poff, F->out,
-				      sizeof(struct sgpu_plan_out), stream);
-	return err;
+	return plan_out_back(k, sync, F->out, w->fz.h + poff, stream);
 }
 
 static int lp_finish(struct dcall *k, int sync)
@@ -1121,7 +1129,9 @@ static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 		err = sgpu_plan_results(&po_d->fail, R.es, d->end, d->err,
 					(uint32_t)n, R.delta, stream);
 	if (!err)
-		err = sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream);
+		err = g_env.nopost ? sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream)
+				   : sgpu_plan_post(po_d, po, sizeof(*po), NULL,
+						    stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)

@@ -150,6 +150,9 @@ uint64_t g_cnt_gated;    /* asynchronous calls gated behind one the
 uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
 /* pc_run_fused: host time before the launch and after the sync (ns) */
 uint64_t g_ns_fused_prep, g_ns_fused_post;
+/* synchronous one-stream device calls (dev_fused): host time to issue,
+ * waiting for the stream, completing (ns) */
+uint64_t g_cnt_sync_calls, g_ns_sync_issue, g_ns_sync_wait, g_ns_sync_finish;
 
 /* fault injection (srtp_gpu_tune "fail_grow", like the reference's
  * mem_threshold_set, src/mem/mem.c:45): the k-th workspace growth from
@@ -209,6 +212,14 @@ uint64_t srtp_gpu_counter(const char *name)
 		return __atomic_load_n(&g_ns_fused_prep, __ATOMIC_RELAXED);
 	if (!strcmp(name, "fused_ns_post"))
 		return __atomic_load_n(&g_ns_fused_post, __ATOMIC_RELAXED);
+	if (!strcmp(name, "sync_calls"))
+		return __atomic_load_n(&g_cnt_sync_calls, __ATOMIC_RELAXED);
+	if (!strcmp(name, "sync_ns_issue"))
+		return __atomic_load_n(&g_ns_sync_issue, __ATOMIC_RELAXED);
+	if (!strcmp(name, "sync_ns_wait"))
+		return __atomic_load_n(&g_ns_sync_wait, __ATOMIC_RELAXED);
+	if (!strcmp(name, "sync_ns_finish"))
+		return __atomic_load_n(&g_ns_sync_finish, __ATOMIC_RELAXED);
 	if (!strcmp(name, "mbufs_ns"))
 		return __atomic_load_n(&g_ns_mbufs, __ATOMIC_RELAXED);
 	if (!strcmp(name, "freshmulti"))
@@ -256,6 +267,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.nosmall = value > 0;
 	else if (!strcmp(name, "lplan"))
 		g_env.lplan = value > 0;
+	else if (!strcmp(name, "nopost"))
+		g_env.nopost = value > 0;
 	else if (!strcmp(name, "noplanfuse"))
 		g_env.noplanfuse = value > 0;
 	else if (!strcmp(name, "fzepoch"))

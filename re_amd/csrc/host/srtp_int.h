@@ -122,6 +122,10 @@ struct srtp_env {
 				   not inside the crypto launch (k_ctr_fused,
 				   the default: measured 498 vs 490 GiB/s on
 				   one box, profiles/r06/lplan_ab.txt) */
+	int nopost;             /* srtp_gpu_tune nopost: single-stream plan
+				   outs come back by a blit copy (and the
+				   asynchronous gate by its own launch), not
+				   by one k_plan_post launch (A/B) */
 	int noplanfuse;         /* srtp_gpu_tune noplanfuse: single-stream
 				   batches take the separate device planner
 				   (k_parse + k_plan_*), not the plan inside
@@ -266,6 +270,8 @@ extern __thread int t_noplan;   /* batch_host.c: a rejected device plan's
 				   fallback runs without device planners */
 extern uint64_t g_cnt_small, g_ns_small_launch, g_ns_small_sync, g_ns_mbufs;
 extern uint64_t g_ns_fused_prep, g_ns_fused_post;
+extern uint64_t g_cnt_sync_calls, g_ns_sync_issue, g_ns_sync_wait,
+		g_ns_sync_finish;
 
 static inline uint64_t mono_ns(void)
 {

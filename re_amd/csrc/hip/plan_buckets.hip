@@ -20,13 +20,15 @@
  *                 entries grouped by session (counting) and ranked by
  *                 packet index inside each session, the single-stream
  *                 speculation per session segment (k_mp_count / desc /
- *                 final of plan_multi.hip), the launch order; the last
- *                 workgroup folds every fail word and re-zeroes the bucket
- *                 counters
- *   k_bp_finish   results, the touched states committed; with speculation
- *                 misses the verdict fold per bucket (k_mf_* of
- *                 plan_multi.hip) and, in the last workgroup, the forged
- *                 packets' EAUTH results and the commit
+ *                 final of plan_multi.hip), the launch order (length bins
+ *                 in arrival order); each workgroup ORs a share of the
+ *                 scatter's fail words into the plan out (no last-workgroup
+ *                 ticket: its release fences cost ~40 us per call)
+ *   k_bp_finish   results; the bucket workgroups re-zero the bucket and
+ *                 bin counters and commit the touched states; with
+ *                 speculation misses the verdict fold per bucket (k_mf_*
+ *                 of plan_multi.hip) and, in the last workgroup, the
+ *                 forged packets' EAUTH results and the commit
  *
  * A batch the buckets cannot hold (a bucket over cap, a session over
  * SGPU_BP_SEGMAX packets in it) fails with SPF_SEG and is re-planned by the

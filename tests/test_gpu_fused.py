@@ -6,7 +6,9 @@ workgroups), in its two forms:
           (k_ctr_fused, host dev_fused);
   lplan   the plan as a launch of its own (k_lp_plan, host lp_issue /
           lp_finish) in front of the lean crypto kernel -- AES-GCM always,
-          AES-CM with srtp_gpu_tune lplan (k_ctr_fast_any).
+          AES-CM with srtp_gpu_tune lplan (k_ctr_fast_any);
+  *_copy  either with the plan out brought back by a blit copy
+          (srtp_gpu_tune nopost) instead of the k_plan_post launch.
 
 Both must give exactly the separate device planner's results
 (srtp_gpu_tune noplanfuse: k_parse + k_plan_* + the lean kernel, pinned by
@@ -75,14 +77,17 @@ GCM = (4, 5)
 
 def modes(suite):
     """(mode, tune knobs, the counter its accepted plans move)"""
-    m = [("lplan", {"lplan": 1}, "lplans")]
+    m = [("lplan", {"lplan": 1}, "lplans"),
+         # the plan out back by a blit copy instead of the post launch
+         ("lplan_copy", {"lplan": 1, "nopost": 1}, "lplans")]
     if suite not in GCM:
         m.append(("fused", {}, "fused"))
+        m.append(("fused_copy", {"nopost": 1}, "fused"))
     return m + [("planner", {"noplanfuse": 1}, None),
                 ("general", {"general": 1}, None)]
 
 
-PLANNED = ("lplan", "fused")
+PLANNED = ("lplan", "fused", "lplan_copy", "fused_copy")
 
 
 def run_modes(torch, suite, key, op, pkts, state_from=None, cap_short=()):

@@ -718,6 +718,18 @@ __device__ __forceinline__ void bp_forged(const struct sgpu_bplan &P,
 	P.endw[i] = P.gcm ? P.es[i] : P.es[i] + (uint32_t)P.delta;
 }
 
+/* the call's outcome (plan out, fold out) to the caller's pinned mirror
+ * with vector stores, once it is final: no blit copy behind the launch */
+__device__ __forceinline__ void bp_post(const struct sgpu_bplan &P,
+					uint32_t tid)
+{
+	if (!P.outh)
+		return;
+	const uint32_t *src = (const uint32_t *)P.out;
+	for (uint32_t w = tid; w < P.outbytes / 4u; w += BPB)
+		P.outh[w] = src[w];
+}
+
 __global__ void __launch_bounds__(BPB)
 k_bp_finish(const struct sgpu_bplan P)
 {
@@ -772,6 +784,8 @@ k_bp_finish(const struct sgpu_bplan P)
 			*P.gate = fail ? 1u : 0u;
 	}
 	__syncthreads();
+	if (b == 0 && (fail || !nf))
+		bp_post(P, tid);
 	if (fail || !nf) {
 		/* every tag verified: the touched states replace the resident
 		 * ones (k_sst_commit) */
@@ -953,6 +967,8 @@ k_bp_finish(const struct sgpu_bplan P)
 		if (P.gate)     /* sgpu_gate_set: completed here, or not */
 			*P.gate = ff ? 1u : 0u;
 	}
+	__syncthreads();
+	bp_post(P, tid);
 }
 
 /* ---- host side ------------------------------------------------------ */

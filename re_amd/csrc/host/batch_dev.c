@@ -1528,15 +1528,18 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		err = run_classes(d->arena, d->arena_size, C, c0,
 				  B->out, prot, stream);
 	}
+	/* plan out and fold out back in one piece: written by the finish
+	 * launch itself (srtp_gpu_tune nopost: one copy behind it) */
+	B->outbytes = (uint32_t)(k->foff + sizeof(struct sgpu_fold_out));
+	B->outh = g_env.nopost ? NULL : (uint32_t *)w->pl.h;
 	if (!err)
 		err = sgpu_bplan_finish(B, stream);
 	if (err) {
 		w->bp_d = NULL;
 		return err;
 	}
-	/* plan out and fold out in one copy */
-	err = sgpu_memcpy_d2h(w->pl.h, w->pl.d, k->foff + sizeof(struct sgpu_fold_out),
-			      stream);
+	if (g_env.nopost)
+		err = sgpu_memcpy_d2h(w->pl.h, w->pl.d, B->outbytes, stream);
 	k->t[2] = times ? now_ms() : 0;
 	return err;
 }

@@ -590,6 +590,10 @@ struct sgpu_bplan {
 					   (zeroed by the scatter) */
 	const uint8_t *verdict;
 	const uint32_t *flist;          /* CTR: forged packets, or NULL */
+	uint32_t *outh;                 /* or NULL: the call's outcome (the
+					   outbytes from out, fo behind it) to
+					   this pinned mirror by k_bp_finish */
+	uint32_t outbytes;
 };
 size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
 			  uint32_t cap);

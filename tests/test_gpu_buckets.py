@@ -87,7 +87,9 @@ def run_modes(torch, suite, nsess, batches, forged=None, modes=None):
     keys = keys_for(suite, nsess)
     res = {}
     for mode in modes or ("bucket", "count", "general"):
-        knobs = {"nobucket": 1} if mode == "count" else {}
+        # bucket_copy: the outcome back by a blit copy, not by k_bp_finish
+        knobs = ({"nobucket": 1} if mode == "count" else
+                 {"nopost": 1} if mode == "bucket_copy" else {})
         tx = [P.Srtp(suite, k) for k in keys]
         rx = [P.Srtp(suite, k) for k in keys]
         outs, deltas = [], []
@@ -150,8 +152,10 @@ def test_bucket_planner_many_sessions(suite, frac, torch_cuda):
         cand = [i for i, (_, q) in enumerate(b2) if q[2:4] != b"\x00\x00"]
         forged[1] = sorted(rng.choice(cand, max(1, int(frac * len(b2))),
                                       replace=False).tolist())
-    res = run_modes(torch_cuda, suite, nsess, [b1, b2], forged)
+    res = run_modes(torch_cuda, suite, nsess, [b1, b2], forged,
+                    ("bucket", "bucket_copy", "count", "general"))
     d = res["bucket"][3]
+    assert res["bucket_copy"][3] == d
     for bi in range(2):
         assert d[bi][0] == {"mplans": 1, "rejects": 0, "devfolds": 0,
                             "folds": 0}, d

@@ -978,21 +978,35 @@ static size_t bp_align(size_t x)
 	return (x + 255) & ~(size_t)255;
 }
 
+/* srtp_gpu_tune bpexp (A/B): the expected entries per bucket the
+ * geometry aims at instead of SGPU_BP_EXP (0: the default) */
+static uint32_t g_bp_exp;
+
+extern "C" void sgpu_bplan_set_exp(uint32_t e)
+{
+	__atomic_store_n(&g_bp_exp, e, __ATOMIC_RELAXED);
+}
+
 extern "C" int sgpu_bplan_geometry(uint32_t n, uint32_t nsess,
 				   uint32_t *bshift, uint32_t *nb,
 				   uint32_t *cap)
 {
 	if (n == 0 || n > SGPU_BP_NMAX || nsess < 2)
 		return -1;
+	const uint32_t ge = __atomic_load_n(&g_bp_exp, __ATOMIC_RELAXED);
+	const uint64_t emax = ge ? ge : SGPU_BP_EXP;
 	/* the most sessions per bucket (<= 256) that keep the expected
-	 * entries per bucket <= SGPU_BP_EXP (a workgroup of 1024 lanes: ~one
-	 * packet each, two workgroups per CU); at most SGPU_BP_NBMAX buckets */
+	 * entries per bucket <= SGPU_BP_EXP (a workgroup of 1024 lanes, ~two
+	 * packets each, two workgroups per CU: one round over the chip at
+	 * 64K sessions); the region holds twice the expected entries at most
+	 * (a fuller bucket: SPF_SEG, the radix grouping); at most
+	 * SGPU_BP_NBMAX buckets */
 	for (int sh = 8; sh >= 0; sh--) {
 		const uint64_t nbk = ((uint64_t)nsess + (1ull << sh) - 1) >> sh;
 		const uint64_t exp = ((uint64_t)n << sh) / nsess + 1;
 		if (nbk > SGPU_BP_NBMAX)
 			return -1;      /* fewer sessions per bucket: more */
-		if (exp > SGPU_BP_EXP)
+		if (exp > emax)
 			continue;
 		uint64_t c = 2 * exp + 1024;
 		c = (c + BPB - 1) / BPB * BPB;

@@ -269,6 +269,9 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.lplan = value > 0;
 	else if (!strcmp(name, "nopost"))
 		g_env.nopost = value > 0;
+	else if (!strcmp(name, "bpexp"))
+		sgpu_bplan_set_exp(value > 0 && value <= SGPU_BP_CAPMAX ?
+				   (uint32_t)value : 0u);
 	else if (!strcmp(name, "noplanfuse"))
 		g_env.noplanfuse = value > 0;
 	else if (!strcmp(name, "fzepoch"))

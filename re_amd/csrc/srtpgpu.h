@@ -546,9 +546,13 @@ typedef struct { uint32_t x, y, z, w; } uint4_t_;
 #define SGPU_BP_BLOCK 1024
 #define SGPU_BP_PPT 4           /* scatter: packets per thread */
 #define SGPU_BP_CAPMAX 4096     /* entries per bucket */
-#define SGPU_BP_EXP 1088        /* expected entries per bucket, at most
-				   (64K sessions x 1M packets: 64 sessions,
-				   ~1025 entries per bucket) */
+#define SGPU_BP_EXP 2100        /* expected entries per bucket, at most
+				   (64K sessions x 1M packets: 128 sessions,
+				   ~2049 entries in a 4096-entry region;
+				   against 1088 -- 64 sessions, twice the
+				   buckets -- the planner launches took 169
+				   instead of 190 us per config-4 step,
+				   profiles/r06/bucket_geometry_ab.txt) */
 #define SGPU_BP_NSB 256         /* sessions per bucket, at most */
 #define SGPU_BP_NBMAX 4096      /* buckets, at most */
 #define SGPU_BP_NMAX (1u << 26) /* packets per call, at most */
@@ -595,6 +599,8 @@ struct sgpu_bplan {
 					   this pinned mirror by k_bp_finish */
 	uint32_t outbytes;
 };
+/* the geometry's target of expected entries per bucket (0: SGPU_BP_EXP) */
+void sgpu_bplan_set_exp(uint32_t e);
 size_t sgpu_bplan_scratch(uint32_t n, uint32_t nsess, uint32_t nb,
 			  uint32_t cap);
 /* geometry for n packets over nsess sessions: 0 and bshift/nb/cap, or -1

@@ -239,7 +239,8 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * of its own, instead of one post launch that does both),
  * "mpradix" (multi-session plans group packets by the radix sort),
  * "nobucket" (multi-session plans by the counting grouping of
- * plan_multi.hip instead of the four-launch bucket planner),
+ * plan_multi.hip instead of the bucket planner), "bpexp" (value: the
+ * bucket planner's target of expected packets per bucket, 0 = default),
  * "nodevfold" (forged packets
  * of a device-planned batch fold on the host), "nocombine" (per-packet
  * calls of different threads do not share launches), "nosmall" (the

@@ -437,7 +437,9 @@ k_ctr_fused(const FArgs fa)
  * loads coalesced per j and all of a lane's in flight together), so a 1M
  * batch takes 256 tickets and one look-back chain of 256 instead of 1024.
  */
+#ifndef LP_PPT
 #define LP_PPT 4
+#endif
 #define LP_WG (FZ_BLOCK * LP_PPT)
 
 struct LpShared {

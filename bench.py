@@ -396,7 +396,7 @@ def main():
                          "stream state)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (traffic, integer roofline) to "
-                         "attach; default profiles/r05_pmc.json")
+                         "attach; default profiles/r06_pmc.json")
     ap.add_argument("--room", type=int, default=None,
                     help="A/B: bytes of slack per packet slot (default 16: "
                          "1216-B slots for 1200-B packets; 80: 1280-B, "
@@ -896,7 +896,7 @@ def main():
     wl = "config%d%s%s%s" % (cfg_id, "_rtcp" if args.rtcp else "",
                              "_ssrc%d" % K if K > 1 else "",
                              "_room%d" % args.room if args.room else "")
-    pj = args.traffic_json or os.path.join(ROOT, "profiles", "r05_pmc.json")
+    pj = args.traffic_json or os.path.join(ROOT, "profiles", "r06_pmc.json")
     ent = None
     if dom and os.path.exists(pj):
         for e in json.load(open(pj)).get("entries", []):

@@ -752,6 +752,11 @@ int small_launch(uint8_t *arena, uint64_t arena_size,
 		 const uint32_t *t0, int prot, uint32_t *done_cnt,
 		 uint32_t *done_flag, uint32_t done_seq, void *stream);
 
+int small_srv_launch(const struct sgpu_comp *comps, const uint32_t *t0,
+		     struct sgpu_srv_mb *mb, struct sgpu_srv_bc *bc,
+		     uint32_t grid, uint32_t linger_us, uint32_t life_us,
+		     uint32_t *done_cnt, uint32_t *done_flag, void *stream);
+
 /* kernel pickers, one per translation unit */
 unsigned sgpu_ctr_block(bool uni, int prot);
 kfn_t sgpu_pick_ctr10(bool compact, bool uni, int shift, int prot);

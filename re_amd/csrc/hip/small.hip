@@ -676,31 +676,31 @@ __device__ __forceinline__ void small_done(const KArgs &a)
 
 } /* namespace */
 
-/* MODE 0 unprotect, 1 protect, 2 per job (SJ_PROTECT): the operations of
- * one shared per-packet launch in one grid (host pc_run_fused) */
-template <int MODE>
-__global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
+/* a workgroup's LDS for one job */
+struct SmallLds {
+	uint32_t T[256];
+	uint32_t rk[60];                /* plain round keys */
+	alignas(16) uint32_t buf[SMALL_MAX / 4];
+	alignas(16) uint32_t ksb[SMALL_MAX / 4];
+	alignas(16) uint32_t WK[SMALL_NB * 80];
+	uint32_t s_tag_ok;
+};
+static_assert(SMALL_NB * 80 * 4 >= 595 * 16, "gcm_small scratch");
+
+/* job i by the calling workgroup.  mode 0 unprotect, 1 protect, 2 per job
+ * (SJ_PROTECT): the operations of one shared per-packet launch in one
+ * grid (host pc_run_fused) */
+__device__ __forceinline__ void small_job(const KArgs &a, uint32_t i,
+					  int mode, SmallLds &L)
 {
-	__shared__ uint32_t T[256];
-	__shared__ uint32_t rk[60];     /* plain round keys */
-	__shared__ __attribute__((aligned(16))) uint32_t buf[SMALL_MAX / 4];
-	__shared__ __attribute__((aligned(16))) uint32_t ksb[SMALL_MAX / 4];
-	__shared__ __attribute__((aligned(16))) uint32_t WK[SMALL_NB * 80];
-	static_assert(SMALL_NB * 80 * 4 >= 595 * 16, "gcm_small scratch");
-	__shared__ uint32_t s_tag_ok;
-	const uint32_t i = blockIdx.x, tid = threadIdx.x;
-	/* every return below runs small_done first: the last workgroup's
-	 * count is what publishes the launch's completion word */
-	if (i >= a.njobs) {
-		small_done(a);
-		return;
-	}
+	uint32_t *T = L.T, *rk = L.rk, *buf = L.buf, *ksb = L.ksb, *WK = L.WK;
+	uint32_t &s_tag_ok = L.s_tag_ok;
+	const uint32_t tid = threadIdx.x;
 	const struct sgpu_job j = a.jobs[i];
-	const bool PROT = MODE == 2 ? (j.flags & SJ_PROTECT) != 0 : MODE == 1;
+	const bool PROT = mode == 2 ? (j.flags & SJ_PROTECT) != 0 : mode == 1;
 	if (j.flags & SJ_SKIP) {
 		if (tid == 0 && a.verdict)
 			a.verdict[i] = 0;
-		small_done(a);
 		return;
 	}
 	const struct sgpu_comp *cp = a.comps +
@@ -856,7 +856,159 @@ __global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
 		dst[w] = buf[w];
 	if (tid == 0 && a.verdict)
 		a.verdict[i] = vd;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_ctr_small(const KArgs a)
+{
+	__shared__ SmallLds L;
+	/* the last workgroup's count publishes the launch's completion word */
+	if (blockIdx.x < a.njobs)
+		small_job(a, blockIdx.x, MODE, L);
 	small_done(a);
+}
+
+/*
+ * The lingering form (srtp_gpu_tune pclinger, round 6 A/B): one launch
+ * serves a workspace's successive small batches.  Workgroup 0 polls the
+ * pinned mailbox (struct sgpu_srv_mb, coherent host memory) and hands each
+ * posted batch to the grid through a device word; every workgroup runs its
+ * jobs i = blockIdx.x + k * gridDim.x; the last one to finish stores the
+ * batch's sequence number into the completion word, as small_done does.
+ * Workgroup 0 ends the launch only when the last batch is complete and it
+ * has been idle for `linger` ticks of the 100 MHz clock (or the host asked
+ * it to stop, or the launch has lived `life` ticks): it tells the grid to
+ * exit, then stores `gone` into the mailbox, so the host knows a batch
+ * posted after its last look was not taken and launches again.  Every wave
+ * reaches that exit: the lifetime bound holds under any traffic.
+ */
+#define SRV_EXIT 0xffffffffu
+
+__device__ __forceinline__ uint64_t srv_now()
+{
+	return __builtin_amdgcn_s_memrealtime();
+}
+
+__global__ void __launch_bounds__(256)
+k_small_srv(const KArgs a0, struct sgpu_srv_mb *mb, struct sgpu_srv_bc *bc,
+	    uint32_t linger, uint32_t life)
+{
+	__shared__ SmallLds L;
+	__shared__ uint32_t s_seq;
+	const uint32_t tid = threadIdx.x;
+	const uint64_t t_start = srv_now();
+	uint64_t t_idle = t_start;
+	uint32_t cur = 0;               /* the batch last taken (bc zeroed) */
+	for (;;) {
+		if (tid == 0) {
+			uint32_t s;
+			for (;;) {
+				const uint64_t now = srv_now();
+				if (blockIdx.x == 0) {
+					/* (relaxed polls: an acquire per poll
+					 * would invalidate the caches under
+					 * other kernels every few hundred ns) */
+					s = __hip_atomic_load(&mb->post,
+							      __ATOMIC_RELAXED,
+							      __HIP_MEMORY_SCOPE_SYSTEM);
+					if (s != cur && s != 0) {
+						__builtin_amdgcn_fence(__ATOMIC_ACQUIRE,
+								       "");
+						/* the batch's arguments to the grid */
+						bc->njobs = __hip_atomic_load(&mb->njobs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->mode = __hip_atomic_load(&mb->mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->arena = __hip_atomic_load(&mb->arena, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->asz = __hip_atomic_load(&mb->asz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->jobs = __hip_atomic_load(&mb->jobs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->verdict = __hip_atomic_load(&mb->verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->save = __hip_atomic_load(&mb->save, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						bc->comps = __hip_atomic_load(&mb->comps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						__hip_atomic_store(&bc->seq, s,
+								   __ATOMIC_RELEASE,
+								   __HIP_MEMORY_SCOPE_AGENT);
+						break;
+					}
+					const bool idle =
+						__hip_atomic_load(&bc->done,
+								  __ATOMIC_RELAXED,
+								  __HIP_MEMORY_SCOPE_AGENT) == cur;
+					if (!idle)
+						t_idle = now;
+					else if (now - t_idle > linger ||
+						 now - t_start > life ||
+						 __hip_atomic_load(&mb->stop,
+								   __ATOMIC_RELAXED,
+								   __HIP_MEMORY_SCOPE_SYSTEM)) {
+						__hip_atomic_store(&bc->seq, SRV_EXIT,
+								   __ATOMIC_RELEASE,
+								   __HIP_MEMORY_SCOPE_AGENT);
+						__hip_atomic_store(&mb->last, cur,
+								   __ATOMIC_RELAXED,
+								   __HIP_MEMORY_SCOPE_SYSTEM);
+						__hip_atomic_store(&mb->gone, 1u,
+								   __ATOMIC_RELEASE,
+								   __HIP_MEMORY_SCOPE_SYSTEM);
+						s = SRV_EXIT;
+						break;
+					}
+					__builtin_amdgcn_s_sleep(2);
+				}
+				else {
+					s = __hip_atomic_load(&bc->seq,
+							      __ATOMIC_RELAXED,
+							      __HIP_MEMORY_SCOPE_AGENT);
+					if (s != cur) {
+						__builtin_amdgcn_fence(__ATOMIC_ACQUIRE,
+								       "agent");
+						break;
+					}
+					/* (workgroup 0 ends the grid within its
+					 * lifetime bound; this one is a backstop) */
+					if (now - t_start > 2ull * life + linger) {
+						s = SRV_EXIT;
+						break;
+					}
+					__builtin_amdgcn_s_sleep(8);
+				}
+			}
+			s_seq = s;
+		}
+		__syncthreads();
+		const uint32_t s = s_seq;
+		if (s == SRV_EXIT)
+			return;
+		cur = s;
+		KArgs a = a0;
+		const uint32_t nj = bc->njobs;
+		const int mode = (int)bc->mode;
+		a.arena = (uint8_t *)bc->arena;
+		a.asz = bc->asz;
+		a.jobs = (const struct sgpu_job *)bc->jobs;
+		a.njobs = nj;
+		a.verdict = (uint8_t *)bc->verdict;
+		a.save = (uint32_t *)bc->save;
+		a.comps = (const struct sgpu_comp *)bc->comps;
+		for (uint32_t i = blockIdx.x; i < nj; i += gridDim.x) {
+			small_job(a, i, mode, L);
+			__syncthreads();
+		}
+		/* completion (small_done), and the device copy of it that
+		 * workgroup 0's idle test reads */
+		__builtin_amdgcn_s_waitcnt(0);
+		__syncthreads();
+		if (tid == 0) {
+			__threadfence_system();
+			if (atomicAdd(a0.done_cnt, 1u) + 1u == gridDim.x) {
+				*a0.done_cnt = 0;
+				__hip_atomic_store(a0.done_flag, s, __ATOMIC_RELEASE,
+						   __HIP_MEMORY_SCOPE_SYSTEM);
+				__hip_atomic_store(&bc->done, s, __ATOMIC_RELEASE,
+						   __HIP_MEMORY_SCOPE_AGENT);
+			}
+		}
+		t_idle = srv_now();
+		__syncthreads();
+	}
 }
 
 int small_launch(uint8_t *arena, uint64_t arena_size,
@@ -882,5 +1034,21 @@ int small_launch(uint8_t *arena, uint64_t arena_size,
 	hipLaunchKernelGGL(prot == 2 ? k_ctr_small<2>
 			   : prot ? k_ctr_small<1> : k_ctr_small<0>,
 			   dim3(njobs), dim3(256), 0, (hipStream_t)stream, a);
+	return hipGetLastError() == hipSuccess ? 0 : EIO;
+}
+
+int small_srv_launch(const struct sgpu_comp *comps, const uint32_t *t0,
+		     struct sgpu_srv_mb *mb, struct sgpu_srv_bc *bc,
+		     uint32_t grid, uint32_t linger_us, uint32_t life_us,
+		     uint32_t *done_cnt, uint32_t *done_flag, void *stream)
+{
+	KArgs a = {};
+	a.comps = comps;
+	a.t0 = t0;
+	a.done_cnt = done_cnt;
+	a.done_flag = done_flag;
+	hipLaunchKernelGGL(k_small_srv, dim3(grid), dim3(256), 0,
+			   (hipStream_t)stream, a, mb, bc, linger_us * 100u,
+			   life_us * 100u);
 	return hipGetLastError() == hipSuccess ? 0 : EIO;
 }

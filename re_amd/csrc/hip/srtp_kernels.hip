@@ -1399,6 +1399,26 @@ extern "C" int sgpu_run_small(uint8_t *arena, uint64_t arena_size,
 			    done_cnt, done_flag, done_seq, stream);
 }
 
+/* the lingering small kernel (small.hip k_small_srv) on a workspace's
+ * stream */
+extern "C" int sgpu_run_small_srv(struct sgpu_srv_mb *mb,
+				  struct sgpu_srv_bc *bc, uint32_t grid,
+				  uint32_t linger_us, uint32_t life_us,
+				  uint32_t *done_cnt, uint32_t *done_flag,
+				  void *stream)
+{
+	return small_srv_launch((const struct sgpu_comp *)g_table, g_T0_dev,
+				mb, bc, grid, linger_us, life_us, done_cnt,
+				done_flag, stream);
+}
+
+/* the session table's device address now (a lingering small kernel's
+ * batches carry it: the table moves when it grows) */
+extern "C" const void *sgpu_table_ptr(void)
+{
+	return g_table;
+}
+
 /* srtp_gpu_tune nocoop (A/B): small general launches fused as usual */
 extern "C" void sgpu_set_coop(int on)
 {
@@ -1737,6 +1757,17 @@ extern "C" void *sgpu_host_alloc(size_t n)
 }
 
 extern "C" void sgpu_host_free(void *p) { if (p) (void)hipHostFree(p); }
+
+/* pinned host memory the device reads while a kernel runs (the lingering
+ * small kernel's mailbox): coherent, not cached on the device */
+extern "C" void *sgpu_host_alloc_coherent(size_t n)
+{
+	void *p = NULL;
+	if (herr(hipHostMalloc(&p, n ? n : 1, hipHostMallocCoherent),
+		 "hipHostMalloc coherent"))
+		return NULL;
+	return p;
+}
 
 extern "C" int sgpu_memcpy_h2d(void *dst, const void *src, size_t n,
 			       void *stream)

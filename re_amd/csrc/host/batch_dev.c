@@ -1497,6 +1497,7 @@ static int dev_bplanned_issue(struct dcall *k, uint32_t bshift, uint32_t nb,
 		sgpu_stream_sync(stream);
 		return ENOMEM;
 	}
+	srv_stop(w);
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->stream);
 	if (!err && k->nup)
 		err = sgpu_memcpy_h2d(up_d, up_h,
@@ -1690,6 +1691,7 @@ int dev_mplanned_issue(struct dcall *k)
 		w->upev = sgpu_event_create();
 	if (!w->upev)
 		return ENOMEM;
+	srv_stop(w);
 	err = sgpu_memcpy_h2d(w->cm.d, cm_h, nsess * 4, w->stream);
 	if (!err && k->nup)
 		err = sgpu_memcpy_h2d(up_d, up_h,

@@ -291,6 +291,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.pcrunners = value > 0 ? value : 0;
 	else if (!strcmp(name, "pchold"))
 		g_env.pchold = value > 0 ? value : 0;
+	else if (!strcmp(name, "pclinger"))
+		g_env.pclinger = value > 0 ? (value < 10000 ? value : 10000) : 0;
 	else if (!strcmp(name, "pcspin"))
 		g_env.pcspin = value > 0 ? value : 0;
 	else if (!strcmp(name, "trace"))
@@ -1282,6 +1284,7 @@ struct ws *ws_get(void)
  * dropped and the next small_run allocates and zeroes a fresh one */
 static int small_reset(struct ws *w, int err)
 {
+	srv_stop(w);
 	if (!w->sm_cnt)
 		return err;
 	if (!sgpu_stream_sync(w->stream) &&
@@ -1293,6 +1296,68 @@ static int small_reset(struct ws *w, int err)
 	return err;
 }
 
+/*
+ * The lingering small kernel (srtp_gpu_tune pclinger; struct sgpu_srv_mb):
+ * a batch is posted into the workspace's mailbox; the kernel on the GPU
+ * since an earlier batch takes it, or -- when none is there, or it left
+ * (gone) before taking it -- a new launch does.  Exactly one launch takes
+ * each batch: a kernel that stores gone has completed everything it took
+ * and takes nothing after, and a new launch runs behind it on the stream.
+ */
+enum { SRV_GRID = 64, SRV_LIFE_US = 20000 };
+
+static int srv_launch(struct ws *w)
+{
+	int err;
+	w->srv_mb->stop = 0;
+	__atomic_store_n(&w->srv_mb->gone, 0, __ATOMIC_RELEASE);
+	err = sgpu_memset(w->srv_bc, 0, sizeof(*w->srv_bc), w->stream);
+	if (!err)
+		err = sgpu_run_small_srv(w->srv_mb, w->srv_bc, SRV_GRID,
+					 (uint32_t)g_env.pclinger, SRV_LIFE_US,
+					 w->sm_cnt, w->sm_flag, w->stream);
+	w->srv_on = !err;
+	return err;
+}
+
+/* before other work is queued on the workspace's stream: the lingering
+ * kernel (idle: the thread that owns the workspace waited for its last
+ * batch) is asked to stop and waited for */
+void srv_stop(struct ws *w)
+{
+	unsigned long k;
+	if (!w->srv_on)
+		return;
+	__atomic_store_n(&w->srv_mb->stop, 1u, __ATOMIC_RELEASE);
+	for (k = 1; !__atomic_load_n(&w->srv_mb->gone, __ATOMIC_ACQUIRE); k++) {
+		if (k & 1023) {
+			__builtin_ia32_pause();
+			continue;
+		}
+		if (sgpu_stream_query(w->stream) != EAGAIN)
+			break;  /* not running (a fault): nothing to wait for */
+	}
+	w->srv_on = 0;
+}
+
+/* the server's mailbox and broadcast block, once per workspace */
+static int srv_ready(struct ws *w)
+{
+	if (w->srv_mb)
+		return 1;
+	w->srv_mb = sgpu_host_alloc_coherent(sizeof(*w->srv_mb));
+	w->srv_bc = fi_sgpu_malloc(sizeof(*w->srv_bc));
+	if (!w->srv_mb || !w->srv_bc) {
+		sgpu_host_free(w->srv_mb);
+		sgpu_free(w->srv_bc);
+		w->srv_mb = NULL;
+		w->srv_bc = NULL;
+		return 0;
+	}
+	memset(w->srv_mb, 0, sizeof(*w->srv_mb));
+	return 1;
+}
+
 int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 		     const struct sgpu_job *jobs, uint32_t m, uint8_t *vh,
 		     uint32_t *sv, int prot, uint64_t *t_launch)
@@ -1300,7 +1365,7 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 	const uint64_t t0 = mono_ns();
 	unsigned long k;
 	uint32_t seq;
-	int err;
+	int err, srv;
 
 	if (!w->sm_flag && !g_env.smallsync) {
 		w->sm_cnt = fi_sgpu_malloc(4);
@@ -1316,8 +1381,27 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 		}
 	}
 	seq = ++w->sm_seq ? w->sm_seq : ++w->sm_seq;   /* never 0 */
-	{
+	srv = g_env.pclinger > 0 && w->sm_flag && !g_env.smallsync &&
+	      srv_ready(w);
+	if (srv) {
+		struct sgpu_srv_mb *mb = w->srv_mb;
+		mb->njobs = m;
+		mb->mode = (uint32_t)prot;
+		mb->arena = (uint64_t)(uintptr_t)arena;
+		mb->asz = asz;
+		mb->jobs = (uint64_t)(uintptr_t)jobs;
+		mb->verdict = (uint64_t)(uintptr_t)vh;
+		mb->save = (uint64_t)(uintptr_t)sv;
+		mb->comps = (uint64_t)(uintptr_t)sgpu_table_ptr();
+		__atomic_store_n(&mb->post, seq, __ATOMIC_RELEASE);
+		err = w->srv_on ? 0 : srv_launch(w);
+		*t_launch = mono_ns() - t0;
+		if (err)
+			return small_reset(w, err);
+	}
+	else {
 		uint32_t *flag = g_env.smallsync ? NULL : w->sm_flag;
+		srv_stop(w);
 		err = sgpu_run_small(arena, asz, jobs, m, vh, sv, prot,
 				     w->sm_cnt, flag, seq, w->stream);
 		*t_launch = mono_ns() - t0;
@@ -1330,6 +1414,16 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 		int q;
 		if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
 			return 0;
+		if (srv && __atomic_load_n(&w->srv_mb->gone, __ATOMIC_ACQUIRE)) {
+			/* the lingering kernel left before it took this batch
+			 * (it completes what it takes before it leaves) */
+			if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
+				return 0;
+			err = srv_launch(w);
+			if (err)
+				return small_reset(w, err);
+			continue;
+		}
 		if (k & 1023) {
 			__builtin_ia32_pause();
 			continue;
@@ -1339,6 +1433,8 @@ int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 			continue;
 		if (__atomic_load_n(w->sm_flag, __ATOMIC_ACQUIRE) == seq)
 			return 0;
+		if (srv && __atomic_load_n(&w->srv_mb->gone, __ATOMIC_ACQUIRE))
+			continue;       /* left meanwhile: launched again above */
 		/* done without its word: a fault */
 		return small_reset(w, q ? q : EIO);
 	}
@@ -1353,6 +1449,7 @@ int pool_reserve(struct ws *w, struct pool *p, size_t bytes)
 	    __atomic_sub_fetch(&g_fail_grow, 1, __ATOMIC_RELAXED) == 0)
 		return ENOMEM;
 	c = bytes + bytes / 2 + 4096;
+	srv_stop(w);
 	sgpu_stream_sync(w->stream);
 	sgpu_host_free(p->h);
 	sgpu_free(p->d);
@@ -1853,6 +1950,7 @@ int mbc_round(struct mbc *c, struct ws *w)
 		mbc_ran(c, w->stage.h);
 		return 0;
 	}
+	srv_stop(w);
 	err = sgpu_memcpy_h2d(w->stage.d, w->stage.h, bytes, w->stream);
 	if (!err)
 		err = round_launch(w, E, SEL_RUN, w->stage.d, bytes, c->soff,

@@ -108,6 +108,10 @@ struct srtp_env {
 	long pchold;            /* srtp_gpu_tune pchold: us a new per-packet
 				   runner holds its launch while other
 				   runners are in flight (percall.c) */
+	long pclinger;          /* srtp_gpu_tune pclinger: us a small-kernel
+				   launch stays on the GPU after its batch,
+				   taking the workspace's next batches from a
+				   mailbox (0: off, one launch per batch) */
 	long pcspin;            /* srtp_gpu_tune pcspin: pause loops a waiting
 				   per-packet caller spins before it sleeps
 				   (default 1000) */
@@ -231,6 +235,11 @@ struct ws {
 	uint32_t *sm_cnt;       /* device */
 	uint32_t *sm_flag;      /* pinned host */
 	uint32_t sm_seq;
+	/* the lingering small kernel (srtp_gpu_tune pclinger): its mailbox
+	 * (coherent pinned host), broadcast block (device), running */
+	struct sgpu_srv_mb *srv_mb;
+	struct sgpu_srv_bc *srv_bc;
+	int srv_on;
 	/* multi-session batches of the bucket planner (plan_buckets.hip,
 	 * batch_dev.c dev_bplanned_issue): its counters are zero between
 	 * calls once bp.d has been zeroed (bp_d) */
@@ -302,6 +311,7 @@ int pool_reserve(struct ws *w, struct pool *p, size_t bytes);
 int idx_reserve(struct ws *w, size_t n);
 size_t small_fits(const struct engine *E);
 void collect_rec(struct rec *r, uint8_t v, uint32_t save);
+void srv_stop(struct ws *w);
 int small_run(struct ws *w, uint8_t *arena, uint64_t asz,
 	      const struct sgpu_job *jobs, uint32_t m, uint8_t *vh,
 	      uint32_t *sv, int prot, uint64_t *t_launch);

@@ -127,6 +127,33 @@ int   sgpu_run_small(uint8_t *arena, uint64_t arena_size,
 		     uint8_t *verdict, uint32_t *save, int prot,
 		     uint32_t *done_cnt, uint32_t *done_flag,
 		     uint32_t done_seq, void *stream);
+/* The lingering form of that kernel (srtp_gpu_tune pclinger): one launch
+ * serves successive batches posted through a mailbox in coherent pinned
+ * host memory (sgpu_host_alloc_coherent); bc is a device block zeroed on
+ * the stream before each launch.  The host writes a batch's arguments,
+ * then post = its sequence number (never 0); the kernel stores it into
+ * done_flag when the batch is complete.  The kernel exits when the last
+ * batch is complete and it has been idle for linger_us (or stop is set,
+ * or it has lived life_us), storing last = the batch it completed last and
+ * gone = 1: a batch posted after that was not taken. */
+struct sgpu_srv_mb {
+	uint32_t post;                  /* host */
+	uint32_t stop;                  /* host */
+	uint32_t gone;                  /* device, at exit */
+	uint32_t last;                  /* device, at exit */
+	uint32_t njobs;                 /* host: the batch posted */
+	uint32_t mode;                  /* 0 / 1 / 2 as sgpu_run_small's prot */
+	uint64_t arena, asz, jobs, verdict, save, comps;
+};
+struct sgpu_srv_bc {
+	uint32_t seq, done, njobs, mode;
+	uint64_t arena, asz, jobs, verdict, save, comps;
+};
+int   sgpu_run_small_srv(struct sgpu_srv_mb *mb, struct sgpu_srv_bc *bc,
+			 uint32_t grid, uint32_t linger_us, uint32_t life_us,
+			 uint32_t *done_cnt, uint32_t *done_flag, void *stream);
+const void *sgpu_table_ptr(void);
+void *sgpu_host_alloc_coherent(size_t n);
 int   sgpu_run_class(uint8_t *arena, uint64_t arena_size,
 		     const struct sgpu_job *jobs, uint32_t njobs,
 		     uint8_t *verdict, uint32_t *save, int mode, int nr,

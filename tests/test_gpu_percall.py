@@ -102,15 +102,20 @@ def oracle_backend(suite, key):
                                                                0)[0])
 
 
-@pytest.mark.parametrize("suites,fuse,runners,hold", [
-    (SUITES, 1, 0, 0), (SUITES, 0, 0, 0), (SUITES, 1, 1, 0),
+@pytest.mark.parametrize("suites,fuse,runners,hold,linger", [
+    (SUITES, 1, 0, 0, 0), (SUITES, 0, 0, 0, 0), (SUITES, 1, 1, 0, 0),
     # CTR suites only, one runner (its queue gathers every thread's next
     # call): lists mixing operations run as one fused launch
-    ([1, 0, 3, 2], 1, 1, 0), ([1, 0, 3, 2], 0, 1, 0), ([1, 0, 3, 2], 1, 0, 0),
+    ([1, 0, 3, 2], 1, 1, 0, 0), ([1, 0, 3, 2], 0, 1, 0, 0),
+    ([1, 0, 3, 2], 1, 0, 0, 0),
     # a new runner holding its launch 20 us while others run (pchold)
-    (SUITES, 1, 0, 20)])
+    (SUITES, 1, 0, 20, 0),
+    # the lingering small kernel (pclinger): batches posted to a launch
+    # already on the GPU, relaunched when it left
+    (SUITES, 1, 0, 0, 100), ([1, 0, 3, 2], 1, 1, 0, 30),
+    (SUITES, 0, 0, 0, 5)])
 def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners,
-                                        hold):
+                                        hold, linger):
     T = 16
     keys = [bytes((13 * t + i) & 0xff for i in range(46)) for t in range(T)]
     want, got = {}, {}
@@ -126,7 +131,8 @@ def test_threads_share_launches_exactly(torch_cuda, suites, fuse, runners,
         k = keys[t][:P.key_len(s) + P.salt_len(s)]
         ths.append(threading.Thread(target=run_thread,
                                     args=(t, s, k, dev_backend, got)))
-    with P.tune(nofuse=0 if fuse else 1, pcrunners=runners, pchold=hold):
+    with P.tune(nofuse=0 if fuse else 1, pcrunners=runners, pchold=hold,
+                pclinger=linger):
         for th in ths:
             th.start()
         for th in ths:
@@ -192,3 +198,60 @@ def test_helper_thread_handoff_stress(torch_cuda):
     assert not bad, bad[:4]
     assert sorted(done) == list(range(T)), "threads hung: %d of %d done" % (
         len(done), T)
+
+
+def test_linger_sequence_and_other_streams(torch_cuda):
+    """One thread's calls through the lingering small kernel (pclinger):
+    exact against the oracle across its gaps (calls spaced past the linger
+    time, so the kernel leaves and is launched again), a staging pool that
+    grows under it (the kernel is stopped before the workspace's stream is
+    synchronised), and a device batch on another stream right after a call
+    (it runs while the kernel lingers, or behind it: at most the linger
+    time on a shared hardware queue)."""
+    import time
+    torch = torch_cuda
+    key = bytes(range(30))
+    want = {}
+    run_thread(0, 1, key, oracle_backend, want)
+    got = {}
+    with P.tune(pclinger=200):
+        tx, rx = dev_backend(1, key)
+        rng = np.random.default_rng(5)
+        res, prot = [], {}
+        for i, (op, arg) in enumerate(script(0)):
+            if isinstance(arg, tuple):
+                kind, j = arg
+                data = bytearray(prot[j])
+                if kind == "forge":
+                    data[-1] ^= 1
+                data = bytes(data)
+            else:
+                data = arg
+            ctx = tx if op.endswith("encrypt") else rx
+            e, po, en, b = ctx(op, data)
+            prot[i] = b[:en] if op.endswith("encrypt") else None
+            res.append((e, po, en, b[:max(en, len(data))]))
+            if i % 37 == 5:
+                time.sleep(0.002)       # past the linger: the kernel left
+            if i == 50:
+                # a device batch of another session right behind a call
+                from tests.test_gpu_fastpath import run_dev
+                pk = [rtp_packet(rng, k, 0x77, plen=100) for k in range(64)]
+                arena = np.zeros(64 * 256, dtype=np.uint8)
+                pos = np.arange(64, dtype=np.int64) * 256
+                end = pos.copy()
+                for k, q in enumerate(pk):
+                    arena[k * 256:k * 256 + len(q)] = np.frombuffer(
+                        q, dtype=np.uint8)
+                    end[k] = k * 256 + len(q)
+                s = P.Srtp(1, key)
+                t0 = time.perf_counter()
+                _, _, _, err = run_dev(torch, "srtp_encrypt", [s], arena,
+                                       pos, end, pos + 256, None)
+                assert time.perf_counter() - t0 < 0.5
+                assert not err.any()
+                s.close()
+        got[0] = res
+    for i, (g, w) in enumerate(zip(got[0], want[0])):
+        assert g[:3] == w[:3], i
+        assert g[3][:len(w[3])] == w[3][:len(g[3])], i

@@ -992,13 +992,16 @@ k_small_srv(const KArgs a0, struct sgpu_srv_mb *mb, struct sgpu_srv_bc *bc,
 			small_job(a, i, mode, L);
 			__syncthreads();
 		}
-		/* completion (small_done), and the device copy of it that
-		 * workgroup 0's idle test reads */
+		/* completion (small_done) by the workgroups that had a job
+		 * (workgroup 0 alone for an empty batch), and the device copy
+		 * of it that workgroup 0's idle test reads */
+		const uint32_t parts = nj < gridDim.x ? (nj ? nj : 1u)
+						      : gridDim.x;
 		__builtin_amdgcn_s_waitcnt(0);
 		__syncthreads();
-		if (tid == 0) {
+		if (tid == 0 && blockIdx.x < parts) {
 			__threadfence_system();
-			if (atomicAdd(a0.done_cnt, 1u) + 1u == gridDim.x) {
+			if (atomicAdd(a0.done_cnt, 1u) + 1u == parts) {
 				*a0.done_cnt = 0;
 				__hip_atomic_store(a0.done_flag, s, __ATOMIC_RELEASE,
 						   __HIP_MEMORY_SCOPE_SYSTEM);

@@ -127,19 +127,54 @@ def cpu_baseline(cfg, rtcp=False):
                                    (r["errors"], out.strip()))
             runs[t] = r
         r, r1 = runs[threads], runs[1]
-        return {"value": round(r["gib_s"], 4), "unit": "GiB/s",
-                "mpkt_s": round(r["mpairs_s"], 4), "cores": threads,
+        procs = None
+        if threads > 1:
+            # the same work as one single-threaded process per core: the
+            # threaded run contends on OpenSSL 3.0's shared HMAC state
+            # (SURVEY §6), separate processes do not -- the reference's
+            # best all-core figure on this host
+            per = 60000 if cfg["suite"] < 4 else 150000
+            ps = [subprocess.Popen(
+                [ref, str(cfg["suite"]), str(length), str(per), "1",
+                 str(cfg["nsess"])], stdout=subprocess.PIPE, text=True)
+                for _ in range(threads)]
+            rs = []
+            for q in ps:
+                out, _ = q.communicate(timeout=600)
+                if q.returncode:
+                    raise RuntimeError("ref_bench process: rc %d" %
+                                       q.returncode)
+                rs.append(json.loads(out.strip().splitlines()[-1]))
+            if any(x["errors"] for x in rs):
+                raise RuntimeError("ref_bench processes: errors")
+            sec = max(x["seconds"] for x in rs)
+            pairs = sum(x["pairs"] for x in rs)
+            gib = sum(x["gib_s"] * x["seconds"] for x in rs) / sec
+            procs = {"gib_s": gib, "mpairs_s": pairs / sec / 1e6,
+                     "pairs": pairs, "seconds": sec}
+        best = procs if procs and procs["gib_s"] > r["gib_s"] else None
+        return {"value": round((best or r)["gib_s"], 4), "unit": "GiB/s",
+                "mpkt_s": round((best or r)["mpairs_s"], 4),
+                "cores": threads,
+                "value_threads": round(r["gib_s"], 4),
+                "value_processes": (round(procs["gib_s"], 4) if procs
+                                    else None),
                 "value_1core": round(r1["gib_s"], 4),
                 "mpkt_s_1core": round(r1["mpairs_s"], 4),
                 "kind": "reference", "nproc": nproc, "usable_cores": usable,
                 "cores_limit": limit,
                 "cpu_model": model, "openssl": r.get("openssl"),
                 "sample": "%d protect+unprotect pairs of %s-B RTP packets "
-                          "on %d threads (%d pairs on 1), %d session(s) "
-                          "per thread, reference src/srtp" % (
+                          "on %d threads of one process, and %s pairs on %d "
+                          "single-threaded processes (value: the faster of "
+                          "the two), %d pairs on 1 core; %d session(s) per "
+                          "thread, reference src/srtp" % (
                               r["pairs"], length or "200/1400", threads,
-                              r1["pairs"], cfg["nsess"]),
-                "seconds": round(r["seconds"] + r1["seconds"], 3)}
+                              procs["pairs"] if procs else 0,
+                              threads if procs else 0, r1["pairs"],
+                              cfg["nsess"]),
+                "seconds": round(r["seconds"] + r1["seconds"] +
+                                 (procs["seconds"] if procs else 0), 3)}
     from tests import oracle_lib as O
     n = 3000
     t0 = time.perf_counter()

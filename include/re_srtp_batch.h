@@ -241,6 +241,9 @@ int srtp_alloc_many(struct srtp **srtpv, size_t n, enum srtp_suite suite,
  * "nobucket" (multi-session plans by the counting grouping of
  * plan_multi.hip instead of the bucket planner), "bpexp" (value: the
  * bucket planner's target of expected packets per bucket, 0 = default),
+ * "syncspin" (a synchronous one-stream call waits on its post launch's
+ * completion word instead of synchronising the stream; the stream may
+ * then still run that launch's tail on return),
  * "pclinger" (value: us a per-packet small-kernel launch stays on the
  * GPU after its batch, taking the workspace's next batches from a pinned
  * mailbox; 0 = off, the default -- while it lingers, other streams mapped

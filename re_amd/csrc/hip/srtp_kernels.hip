@@ -2261,7 +2261,7 @@ extern "C" int sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
  * profiles/r06 config2a timeline) */
 __global__ void __launch_bounds__(256)
 k_plan_post(const uint32_t *__restrict__ src, uint32_t *__restrict__ host,
-	    uint32_t nwords, uint32_t *gate)
+	    uint32_t nwords, uint32_t *gate, uint32_t *done, uint32_t seq)
 {
 	const uint32_t i = threadIdx.x;
 	for (uint32_t w = i; w < nwords; w += blockDim.x)
@@ -2270,14 +2270,26 @@ k_plan_post(const uint32_t *__restrict__ src, uint32_t *__restrict__ host,
 		const struct sgpu_plan_out *o = (const struct sgpu_plan_out *)src;
 		*gate = o->fail || o->nfail;
 	}
+	if (done) {
+		/* the completion word (small_done's pattern): after every
+		 * thread's stores */
+		__builtin_amdgcn_s_waitcnt(0);
+		__syncthreads();
+		if (i == 0) {
+			__threadfence_system();
+			__hip_atomic_store(done, seq, __ATOMIC_RELEASE,
+					   __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+	}
 }
 
 extern "C" int sgpu_plan_post(const void *out, void *host, uint32_t bytes,
-			      uint32_t *gate, void *stream)
+			      uint32_t *gate, uint32_t *done, uint32_t seq,
+			      void *stream)
 {
 	hipLaunchKernelGGL(k_plan_post, dim3(1), dim3(256), 0,
 			   (hipStream_t)stream, (const uint32_t *)out,
-			   (uint32_t *)host, (bytes + 3u) / 4u, gate);
+			   (uint32_t *)host, (bytes + 3u) / 4u, gate, done, seq);
 	return herr(hipGetLastError(), "post launch");
 }
 

@@ -261,6 +261,43 @@ int dev_planned_finish(struct dcall *k)
 #define FZ_FO_OFF ((sizeof(struct sgpu_plan_out) + 63u) & ~(size_t)63)
 #define FZ_SLOT (FZ_FO_OFF + 64u)
 
+/* the workspace's pinned completion word for synchronous single-stream
+ * calls (srtp_gpu_tune syncspin), once */
+static int sync_word(struct ws *w)
+{
+	if (!w->sy_word) {
+		w->sy_word = fi_sgpu_host_alloc(4);
+		if (w->sy_word)
+			*w->sy_word = 0;
+	}
+	return w->sy_word != NULL;
+}
+
+/* wait for a synchronous call: its post's completion word when it has one
+ * (spinning, the stream asked now and then whether it stopped without
+ * it: a fault), else the stream */
+static int sync_wait(struct dcall *k, void *stream)
+{
+	unsigned long i;
+	if (!k->spin)
+		return sgpu_stream_sync(stream);
+	for (i = 1;; i++) {
+		int q;
+		if (__atomic_load_n(k->w->sy_word, __ATOMIC_ACQUIRE) == k->spin)
+			return 0;
+		if (i & 1023) {
+			__builtin_ia32_pause();
+			continue;
+		}
+		q = sgpu_stream_query(stream);
+		if (q == EAGAIN)
+			continue;
+		if (__atomic_load_n(k->w->sy_word, __ATOMIC_ACQUIRE) == k->spin)
+			return 0;
+		return q ? q : EIO;
+	}
+}
+
 /* a single-stream call's plan out back to its pinned mirror, behind the
  * crypto launch; an asynchronous call also sets its chained gate word
  * (out->fail || out->nfail: the plan failed or a tag did not verify --
@@ -273,9 +310,19 @@ static int plan_out_back(struct dcall *k, int sync, struct sgpu_plan_out *out,
 {
 	int err = 0;
 	k->devfold = 0;
-	if (!g_env.nopost)
+	if (!g_env.nopost) {
+		/* a synchronous call with srtp_gpu_tune syncspin: waited for
+		 * by the post's completion word, not a stream synchronisation */
+		uint32_t *done = NULL;
+		if (sync && g_env.syncspin && sync_word(k->w))
+			done = k->w->sy_word;
+		k->spin = done ? ++k->w->sy_seq : 0;
+		if (k->spin == 0 && done)
+			k->spin = ++k->w->sy_seq;       /* never 0 */
 		return sgpu_plan_post(out, host, sizeof(*out),
-				      sync ? NULL : k->gate, stream);
+				      sync ? NULL : k->gate, done, k->spin,
+				      stream);
+	}
 	if (!sync && k->gate)
 		err = sgpu_plan_finish(&out->fail, NULL, NULL, NULL, 0, 0,
 				       &out->nfail, k->gate, NULL, NULL, stream);
@@ -501,7 +548,7 @@ static int dev_fused(int op, struct srtp *s, struct srtp_batch_dev *d,
 		err = fz_issue(&k, 1);
 		t1 = mono_ns();
 		if (!err)
-			err = sgpu_stream_sync(d->stream);
+			err = sync_wait(&k, d->stream);
 		t2 = mono_ns();
 		if (err)
 			return err;
@@ -1131,7 +1178,7 @@ static int dev_lplanned_rtcp(int op, struct srtp *s, struct srtp_batch_dev *d)
 	if (!err)
 		err = g_env.nopost ? sgpu_memcpy_d2h(po, po_d, sizeof(*po), stream)
 				   : sgpu_plan_post(po_d, po, sizeof(*po), NULL,
-						    stream);
+						    NULL, 0, stream);
 	if (!err)
 		err = sgpu_stream_sync(stream);
 	if (err)

@@ -291,6 +291,8 @@ int srtp_gpu_tune(const char *name, long value)
 		g_env.pcrunners = value > 0 ? value : 0;
 	else if (!strcmp(name, "pchold"))
 		g_env.pchold = value > 0 ? value : 0;
+	else if (!strcmp(name, "syncspin"))
+		g_env.syncspin = value > 0;
 	else if (!strcmp(name, "pclinger"))
 		g_env.pclinger = value > 0 ? (value < 10000 ? value : 10000) : 0;
 	else if (!strcmp(name, "pcspin"))

@@ -108,6 +108,10 @@ struct srtp_env {
 	long pchold;            /* srtp_gpu_tune pchold: us a new per-packet
 				   runner holds its launch while other
 				   runners are in flight (percall.c) */
+	int syncspin;           /* srtp_gpu_tune syncspin: a synchronous
+				   one-stream call waits by spinning on its
+				   post launch's completion word instead of a
+				   stream synchronisation (A/B) */
 	long pclinger;          /* srtp_gpu_tune pclinger: us a small-kernel
 				   launch stays on the GPU after its batch,
 				   taking the workspace's next batches from a
@@ -237,6 +241,9 @@ struct ws {
 	uint32_t sm_seq;
 	/* the lingering small kernel (srtp_gpu_tune pclinger): its mailbox
 	 * (coherent pinned host), broadcast block (device), running */
+	uint32_t *sy_word;      /* pinned: synchronous calls' completion
+				   word (srtp_gpu_tune syncspin) */
+	uint32_t sy_seq;
 	struct sgpu_srv_mb *srv_mb;
 	struct sgpu_srv_bc *srv_bc;
 	int srv_on;
@@ -349,6 +356,8 @@ struct dcall {
 	uint32_t pfail;         /* finish: the rejected plan's SPF_* bits */
 	struct sgpu_splan_in sin; /* several streams: the plan input */
 	int devfold;            /* fold queued on the device */
+	uint32_t spin;          /* synchronous: the post's completion word
+				   value to wait for (0: the stream) */
 	int radix;              /* ... grouped by the radix sort */
 	int fused;              /* single stream planned inside the crypto
 				   launch (fz_issue / fz_finish), 2: by the

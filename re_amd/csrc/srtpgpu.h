@@ -764,9 +764,11 @@ int   sgpu_plan_finish(const uint32_t *guard, const uint32_t *end0,
 		       uint32_t *nfail_out, const uint32_t *ffail,
 		       void *stream);
 /* out (struct sgpu_plan_out, bytes of it) to pinned host memory with
- * vector stores; gate (or NULL) = out->fail || out->nfail */
+ * vector stores; gate (or NULL) = out->fail || out->nfail; done (pinned
+ * host word, or NULL) = seq after all of it */
 int   sgpu_plan_post(const void *out, void *host, uint32_t bytes,
-		     uint32_t *gate, void *stream);
+		     uint32_t *gate, uint32_t *done, uint32_t seq,
+		     void *stream);
 int   sgpu_plan_results(const uint32_t *guard, const uint32_t *end0,
 			uint32_t *end, int32_t *err, uint32_t n, int32_t delta,
 			void *stream);

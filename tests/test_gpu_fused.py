@@ -83,11 +83,13 @@ def modes(suite):
     if suite not in GCM:
         m.append(("fused", {}, "fused"))
         m.append(("fused_copy", {"nopost": 1}, "fused"))
+        # waited for by the post's completion word, not the stream
+        m.append(("fused_spin", {"syncspin": 1}, "fused"))
     return m + [("planner", {"noplanfuse": 1}, None),
                 ("general", {"general": 1}, None)]
 
 
-PLANNED = ("lplan", "fused", "lplan_copy", "fused_copy")
+PLANNED = ("lplan", "fused", "lplan_copy", "fused_copy", "fused_spin")
 
 
 def run_modes(torch, suite, key, op, pkts, state_from=None, cap_short=()):

@@ -156,10 +156,36 @@ def test_tune_knobs_and_counters():
     (no GPU needed: neither touches the device)"""
     L = P.load()
     for k in ("noplan", "general", "perclass", "nolean", "nodevfold",
-              "splan", "nomk", "freshmulti", "trace", "times"):
+              "splan", "nomk", "freshmulti", "trace", "times",
+              # round 6: the one-launch planner for AES-CM, the counting
+              # grouping, the copy instead of the post launch, the
+              # completion-word wait, the bucket target, the linger
+              "lplan", "nobucket", "nopost", "syncspin"):
         assert L.srtp_gpu_tune(k.encode(), 1) == 0, k
+        assert L.srtp_gpu_tune(k.encode(), 0) == 0, k
+    for k, v in (("bpexp", 2100), ("pclinger", 100)):
+        assert L.srtp_gpu_tune(k.encode(), v) == 0, k
         assert L.srtp_gpu_tune(k.encode(), 0) == 0, k
     assert L.srtp_gpu_tune(b"no-such-knob", 1) != 0
     for c in ("misses", "folds", "rejects", "devfolds", "splans",
-              "freshmulti"):
+              "freshmulti", "fused", "lplans", "dplans", "mplans", "rplans",
+              "lbtimeouts", "sync_calls", "sync_ns_issue", "sync_ns_wait",
+              "sync_ns_finish"):
         assert P.counter(c) >= 0, c
+
+
+def test_cpu_baseline_threads_and_processes():
+    """bench.py's cpu_baseline: the reference src/srtp (oracle/_ref/ref_bench,
+    built from the reference's own sources) on 1 core, as threads of one
+    process and as single-threaded processes; value is the faster all-core
+    leg, every leg error-free (a run with reference errors fails loudly)"""
+    import bench
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_bench")):
+        pytest.skip("oracle/_ref/ref_bench not built")
+    cb = bench.cpu_baseline({"suite": 4, "length": 160, "nsess": 1})
+    assert cb["kind"] == "reference"
+    assert cb["value_1core"] > 0 and cb["value_threads"] > 0
+    if cb["cores"] > 1:
+        assert cb["value_processes"] > 0
+        assert cb["value"] == max(cb["value_threads"],
+                                  cb["value_processes"])
